@@ -1,0 +1,429 @@
+// G1 (over Fp) and G2 (over Fp2) group law for gfx950, homogeneous projective coordinates
+// with the Renes-Costello-Batina complete formulas (a = 0).  Replaces blst's POINTonE1/E2
+// code reached through @chainsafe/bls PublicKey.aggregate (packages/beacon-node/src/chain/
+// bls/utils.ts:11), Signature.fromBytes(..., validate) (maybeBatch.ts:23,36) and the
+// Pairing.mul_n_aggregate randomizer multiplications.
+#pragma once
+#include "lsg_field.hpp"
+
+// ---- overload set so one template serves G1 and G2
+LSG_INL fp_t fadd(const fp_t& a, const fp_t& b) { return fp_add(a, b); }
+LSG_INL fp2_t fadd(const fp2_t& a, const fp2_t& b) { return fp2_add(a, b); }
+LSG_INL fp_t fsub(const fp_t& a, const fp_t& b) { return fp_sub(a, b); }
+LSG_INL fp2_t fsub(const fp2_t& a, const fp2_t& b) { return fp2_sub(a, b); }
+LSG_INL fp_t fmul(const fp_t& a, const fp_t& b) { return fp_mul(a, b); }
+LSG_INL fp2_t fmul(const fp2_t& a, const fp2_t& b) { return fp2_mul(a, b); }
+LSG_INL fp_t fsqr(const fp_t& a) { return fp_sqr(a); }
+LSG_INL fp2_t fsqr(const fp2_t& a) { return fp2_sqr(a); }
+LSG_INL fp_t fneg(const fp_t& a) { return fp_neg(a); }
+LSG_INL fp2_t fneg(const fp2_t& a) { return fp2_neg(a); }
+LSG_INL fp_t fmul_b3(const fp_t& a) { return fp_mul12(a); }
+LSG_INL fp2_t fmul_b3(const fp2_t& a) { return fp2_mul_b3(a); }
+LSG_INL bool fis_zero(const fp_t& a) { return fp_is_zero(a); }
+LSG_INL bool fis_zero(const fp2_t& a) { return fp2_is_zero(a); }
+LSG_INL bool feq(const fp_t& a, const fp_t& b) { return fp_eq(a, b); }
+LSG_INL bool feq(const fp2_t& a, const fp2_t& b) { return fp2_eq(a, b); }
+LSG_INL fp_t fselect(bool c, const fp_t& a, const fp_t& b) { return fp_select(c, a, b); }
+LSG_INL fp2_t fselect(bool c, const fp2_t& a, const fp2_t& b) { return fp2_select(c, a, b); }
+LSG_INL fp_t finv(const fp_t& a) { return fp_inv(a); }
+LSG_INL fp2_t finv(const fp2_t& a) { return fp2_inv(a); }
+template <class F> LSG_INL F fzero();
+template <> LSG_INL fp_t fzero<fp_t>() { return fp_zero(); }
+template <> LSG_INL fp2_t fzero<fp2_t>() { return fp2_zero(); }
+template <class F> LSG_INL F fone();
+template <> LSG_INL fp_t fone<fp_t>() { return FP_ONE; }
+template <> LSG_INL fp2_t fone<fp2_t>() { return fp2_one(); }
+
+template <class F>
+struct aff_t {
+  F x, y;
+};
+template <class F>
+struct proj_t {
+  F X, Y, Z;
+};
+typedef aff_t<fp_t> g1a_t;
+typedef aff_t<fp2_t> g2a_t;
+typedef proj_t<fp_t> g1p_t;
+typedef proj_t<fp2_t> g2p_t;
+
+template <class F>
+LSG_INL proj_t<F> proj_inf() {
+  proj_t<F> r;
+  r.X = fzero<F>();
+  r.Y = fone<F>();
+  r.Z = fzero<F>();
+  return r;
+}
+
+template <class F>
+LSG_INL proj_t<F> proj_from_aff(const aff_t<F>& a) {
+  proj_t<F> r;
+  r.X = a.x;
+  r.Y = a.y;
+  r.Z = fone<F>();
+  return r;
+}
+
+template <class F>
+LSG_INL bool proj_is_inf(const proj_t<F>& a) {
+  return fis_zero(a.Z);
+}
+
+template <class F>
+LSG_INL proj_t<F> proj_neg(const proj_t<F>& a) {
+  proj_t<F> r = a;
+  r.Y = fneg(a.Y);
+  return r;
+}
+
+// RCB 2016 algorithm 7 (complete addition, a = 0)
+template <class F>
+LSG_INL proj_t<F> proj_add(const proj_t<F>& p, const proj_t<F>& q) {
+  F t0 = fmul(p.X, q.X);
+  F t1 = fmul(p.Y, q.Y);
+  F t2 = fmul(p.Z, q.Z);
+  F t3 = fmul(fadd(p.X, p.Y), fadd(q.X, q.Y));
+  F t4 = fadd(t0, t1);
+  t3 = fsub(t3, t4);
+  t4 = fmul(fadd(p.Y, p.Z), fadd(q.Y, q.Z));
+  F X3 = fadd(t1, t2);
+  t4 = fsub(t4, X3);
+  X3 = fmul(fadd(p.X, p.Z), fadd(q.X, q.Z));
+  F Y3 = fadd(t0, t2);
+  Y3 = fsub(X3, Y3);
+  X3 = fadd(t0, t0);
+  t0 = fadd(X3, t0);
+  t2 = fmul_b3(t2);
+  F Z3 = fadd(t1, t2);
+  t1 = fsub(t1, t2);
+  Y3 = fmul_b3(Y3);
+  X3 = fmul(t4, Y3);
+  t2 = fmul(t3, t1);
+  X3 = fsub(t2, X3);
+  Y3 = fmul(Y3, t0);
+  t1 = fmul(t1, Z3);
+  Y3 = fadd(t1, Y3);
+  t0 = fmul(t0, t3);
+  Z3 = fmul(Z3, t4);
+  Z3 = fadd(Z3, t0);
+  proj_t<F> r;
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+  return r;
+}
+
+// RCB 2016 algorithm 8 (mixed addition, q affine and finite, a = 0)
+template <class F>
+LSG_INL proj_t<F> proj_add_mixed(const proj_t<F>& p, const aff_t<F>& q) {
+  F t0 = fmul(p.X, q.x);
+  F t1 = fmul(p.Y, q.y);
+  F t3 = fmul(fadd(q.x, q.y), fadd(p.X, p.Y));
+  F t4 = fadd(t0, t1);
+  t3 = fsub(t3, t4);
+  t4 = fadd(fmul(q.y, p.Z), p.Y);
+  F Y3 = fadd(fmul(q.x, p.Z), p.X);
+  F X3 = fadd(t0, t0);
+  t0 = fadd(X3, t0);
+  F t2 = fmul_b3(p.Z);
+  F Z3 = fadd(t1, t2);
+  t1 = fsub(t1, t2);
+  Y3 = fmul_b3(Y3);
+  X3 = fmul(t4, Y3);
+  t2 = fmul(t3, t1);
+  X3 = fsub(t2, X3);
+  Y3 = fmul(Y3, t0);
+  t1 = fmul(t1, Z3);
+  Y3 = fadd(t1, Y3);
+  t0 = fmul(t0, t3);
+  Z3 = fmul(Z3, t4);
+  Z3 = fadd(Z3, t0);
+  proj_t<F> r;
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+  return r;
+}
+
+// RCB 2016 algorithm 9 (doubling, a = 0)
+template <class F>
+LSG_INL proj_t<F> proj_dbl(const proj_t<F>& p) {
+  F t0 = fsqr(p.Y);
+  F Z3 = fadd(t0, t0);
+  Z3 = fadd(Z3, Z3);
+  Z3 = fadd(Z3, Z3);
+  F t1 = fmul(p.Y, p.Z);
+  F t2 = fmul_b3(fsqr(p.Z));
+  F X3 = fmul(t2, Z3);
+  F Y3 = fadd(t0, t2);
+  Z3 = fmul(t1, Z3);
+  t1 = fadd(t2, t2);
+  t2 = fadd(t1, t2);
+  t0 = fsub(t0, t2);
+  Y3 = fmul(t0, Y3);
+  Y3 = fadd(X3, Y3);
+  t1 = fmul(p.X, p.Y);
+  X3 = fmul(t0, t1);
+  X3 = fadd(X3, X3);
+  proj_t<F> r;
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+  return r;
+}
+
+// Non-inlined wrappers (keep call sites small: one G2 op expands to ~12 Fp2 muls)
+LSG_NOINL g1p_t g1_add(g1p_t p, g1p_t q) { return proj_add(p, q); }
+LSG_NOINL g1p_t g1_add_mixed(g1p_t p, g1a_t q) { return proj_add_mixed(p, q); }
+LSG_NOINL g1p_t g1_dbl(g1p_t p) { return proj_dbl(p); }
+LSG_NOINL g2p_t g2_add(g2p_t p, g2p_t q) { return proj_add(p, q); }
+LSG_NOINL g2p_t g2_add_mixed(g2p_t p, g2a_t q) { return proj_add_mixed(p, q); }
+LSG_NOINL g2p_t g2_dbl(g2p_t p) { return proj_dbl(p); }
+
+LSG_INL g1p_t gadd(const g1p_t& p, const g1p_t& q) { return g1_add(p, q); }
+LSG_INL g2p_t gadd(const g2p_t& p, const g2p_t& q) { return g2_add(p, q); }
+LSG_INL g1p_t gdbl(const g1p_t& p) { return g1_dbl(p); }
+LSG_INL g2p_t gdbl(const g2p_t& p) { return g2_dbl(p); }
+
+// [k]P for a 64-bit scalar, MSB-first double-and-add (k is per lane: the add is a select)
+template <class F>
+LSG_INL proj_t<F> proj_mul_u64(const proj_t<F>& p, uint64_t k) {
+  proj_t<F> acc = proj_inf<F>();
+  for (int b = 63; b >= 0; b--) {
+    acc = gdbl(acc);
+    proj_t<F> s = gadd(acc, p);
+    bool bit = (k >> b) & 1u;
+    acc.X = fselect(bit, s.X, acc.X);
+    acc.Y = fselect(bit, s.Y, acc.Y);
+    acc.Z = fselect(bit, s.Z, acc.Z);
+  }
+  return acc;
+}
+
+// [|x|]P for the BLS parameter |x| = 0xd201000000010000 (public, uniform branch)
+template <class F>
+LSG_INL proj_t<F> proj_mul_xabs(const proj_t<F>& p) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  proj_t<F> acc = p;
+  for (int b = 62; b >= 0; b--) {
+    acc = gdbl(acc);
+    if ((xa >> b) & 1u) acc = gadd(acc, p);
+  }
+  return acc;
+}
+
+template <class F>
+LSG_INL bool proj_eq(const proj_t<F>& a, const proj_t<F>& b) {
+  bool ia = proj_is_inf(a), ib = proj_is_inf(b);
+  if (ia || ib) return ia && ib;
+  return feq(fmul(a.X, b.Z), fmul(b.X, a.Z)) && feq(fmul(a.Y, b.Z), fmul(b.Y, a.Z));
+}
+
+template <class F>
+LSG_INL aff_t<F> proj_to_aff(const proj_t<F>& p) {
+  F zi = finv(p.Z);
+  aff_t<F> r;
+  r.x = fmul(p.X, zi);
+  r.y = fmul(p.Y, zi);
+  return r;
+}
+
+// ---- psi endomorphism of E2 (untwist-Frobenius-twist), valid on projective points
+LSG_INL g2p_t g2_psi(const g2p_t& p) {
+  g2p_t r;
+  r.X = fp2_mul(fp2_conj(p.X), PSI_CX);
+  r.Y = fp2_mul(fp2_conj(p.Y), PSI_CY);
+  r.Z = fp2_conj(p.Z);
+  return r;
+}
+LSG_INL g2p_t g2_psi2(const g2p_t& p) {
+  g2p_t r;
+  r.X = fp2_mul_fp(p.X, PSI2_CX);
+  r.Y = fp2_mul_fp(p.Y, PSI2_CY);
+  r.Z = p.Z;
+  return r;
+}
+
+// Scott's G2 membership test: psi(P) == [x]P (x < 0)
+LSG_NOINL bool g2_in_group(g2p_t p) {
+  if (proj_is_inf(p)) return true;
+  g2p_t xp = proj_neg(proj_mul_xabs(p));
+  return proj_eq(g2_psi(p), xp);
+}
+
+LSG_INL bool g1_on_curve_aff(const g1a_t& a) {
+  fp_t rhs = fp_add(fp_mul(fp_sqr(a.x), a.x), FP_B_G1);
+  return fp_eq(fp_sqr(a.y), rhs);
+}
+LSG_INL bool g2_on_curve_aff(const g2a_t& a) {
+  fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), FP2_B_G2);
+  return fp2_eq(fp2_sqr(a.y), rhs);
+}
+
+// ------------------------------------------------------------------ byte <-> Fp
+// 48 big-endian bytes -> canonical limbs (top 3 flag bits masked off by the caller)
+LSG_INL fp_t fp_from_be48(const uint8_t* b) {
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  return r;
+}
+LSG_INL void fp_to_be48(uint8_t* b, const fp_t& a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.l[i] >> 24);
+    q[1] = (uint8_t)(a.l[i] >> 16);
+    q[2] = (uint8_t)(a.l[i] >> 8);
+    q[3] = (uint8_t)a.l[i];
+  }
+}
+// canonical value < p ?
+LSG_INL bool fp_canon_lt_p(const fp_t& a) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], LSG_P[i], br, &br);
+  return br != 0;
+}
+
+// Status codes, numerically equal to blst's BLST_ERROR (+ wrapper's size error)
+enum {
+  LSG_BLST_SUCCESS = 0,
+  LSG_BLST_BAD_ENCODING = 1,
+  LSG_BLST_POINT_NOT_ON_CURVE = 2,
+  LSG_BLST_POINT_NOT_IN_GROUP = 3,
+  LSG_BLST_AGGR_TYPE_MISMATCH = 4,
+  LSG_BLST_VERIFY_FAIL = 5,
+  LSG_BLST_PK_IS_INFINITY = 6,
+  LSG_BLST_BAD_SCALAR = 7,
+  LSG_BLST_INVALID_SIZE = 10,
+};
+
+// blst POINTonE2_Uncompress_Z (96 bytes).  Sets *inf for the infinity encoding.
+LSG_INL int g2_uncompress(g2a_t& out, bool& inf, const uint8_t* in) {
+  uint8_t in0 = in[0];
+  inf = false;
+  if (!(in0 & 0x80)) return LSG_BLST_BAD_ENCODING;
+  if (in0 & 0x40) {
+    uint32_t acc = in0 & 0x3f;
+    for (int i = 1; i < 96; i++) acc |= in[i];
+    if (acc == 0) {
+      inf = true;
+      out.x = fp2_zero();
+      out.y = fp2_zero();
+      return LSG_BLST_SUCCESS;
+    }
+    return LSG_BLST_BAD_ENCODING;
+  }
+  fp_t x1 = fp_from_be48(in);
+  x1.l[11] &= 0x1fffffffu;
+  fp_t x0 = fp_from_be48(in + 48);
+  if (!fp_canon_lt_p(x1) || !fp_canon_lt_p(x0)) return LSG_BLST_BAD_ENCODING;
+  fp2_t x = fp2_make(fp_to_mont(x0), fp_to_mont(x1));
+  fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), FP2_B_G2);
+  fp2_t y;
+  if (!fp2_sqrt(y, rhs)) return LSG_BLST_POINT_NOT_ON_CURVE;
+  bool want = (in0 & 0x20) != 0;
+  if (fp2_lexi_largest(y) != want) y = fp2_neg(y);
+  out.x = x;
+  out.y = y;
+  if (fp2_is_zero(x)) return LSG_BLST_POINT_NOT_IN_GROUP;
+  return LSG_BLST_SUCCESS;
+}
+
+// blst POINTonE2_Deserialize_Z for 192-byte uncompressed input
+LSG_INL int g2_deserialize_uncompressed(g2a_t& out, bool& inf, const uint8_t* in) {
+  uint8_t in0 = in[0];
+  inf = false;
+  if (in0 & 0x80) return LSG_BLST_BAD_ENCODING;
+  if (in0 & 0x40) {
+    uint32_t acc = in0 & 0x3f;
+    for (int i = 1; i < 192; i++) acc |= in[i];
+    if (acc == 0) {
+      inf = true;
+      out.x = fp2_zero();
+      out.y = fp2_zero();
+      return LSG_BLST_SUCCESS;
+    }
+    return LSG_BLST_BAD_ENCODING;
+  }
+  if (in0 & 0x20) return LSG_BLST_BAD_ENCODING;
+  fp_t v[4];
+  for (int k = 0; k < 4; k++) {
+    v[k] = fp_from_be48(in + 48 * k);
+    if (k == 0) v[k].l[11] &= 0x1fffffffu;
+    if (!fp_canon_lt_p(v[k])) return LSG_BLST_BAD_ENCODING;
+  }
+  out.x = fp2_make(fp_to_mont(v[1]), fp_to_mont(v[0]));
+  out.y = fp2_make(fp_to_mont(v[3]), fp_to_mont(v[2]));
+  if (!g2_on_curve_aff(out)) return LSG_BLST_POINT_NOT_ON_CURVE;
+  if (fp2_is_zero(out.x)) return LSG_BLST_POINT_NOT_IN_GROUP;
+  return LSG_BLST_SUCCESS;
+}
+
+// blst_p1_deserialize: 96-byte uncompressed or 48-byte compressed
+LSG_INL int g1_deserialize(g1a_t& out, bool& inf, const uint8_t* in, int len) {
+  uint8_t in0 = in[0];
+  inf = false;
+  bool compressed = (in0 & 0x80) != 0;
+  if (compressed != (len == 48)) return LSG_BLST_BAD_ENCODING;
+  if (in0 & 0x40) {
+    uint32_t acc = in0 & 0x3f;
+    for (int i = 1; i < len; i++) acc |= in[i];
+    if (acc == 0) {
+      inf = true;
+      out.x = fp_zero();
+      out.y = fp_zero();
+      return LSG_BLST_SUCCESS;
+    }
+    return LSG_BLST_BAD_ENCODING;
+  }
+  if (!compressed && (in0 & 0x20)) return LSG_BLST_BAD_ENCODING;
+  fp_t x = fp_from_be48(in);
+  x.l[11] &= 0x1fffffffu;
+  if (!fp_canon_lt_p(x)) return LSG_BLST_BAD_ENCODING;
+  out.x = fp_to_mont(x);
+  if (compressed) {
+    fp_t rhs = fp_add(fp_mul(fp_sqr(out.x), out.x), FP_B_G1);
+    fp_t y = fp_pow_fixed(rhs, LSG_EXP_P_PLUS_1_DIV_4);
+    if (!fp_eq(fp_sqr(y), rhs)) return LSG_BLST_POINT_NOT_ON_CURVE;
+    bool want = (in0 & 0x20) != 0;
+    if (fp_canon_gt_half(fp_from_mont(y)) != want) y = fp_neg(y);
+    out.y = y;
+  } else {
+    fp_t y = fp_from_be48(in + 48);
+    if (!fp_canon_lt_p(y)) return LSG_BLST_BAD_ENCODING;
+    out.y = fp_to_mont(y);
+    if (!g1_on_curve_aff(out)) return LSG_BLST_POINT_NOT_ON_CURVE;
+  }
+  if (fp_is_zero(out.x)) return LSG_BLST_POINT_NOT_IN_GROUP;
+  return LSG_BLST_SUCCESS;
+}
+
+// affine G1 -> 96-byte uncompressed (blst_p1_affine_serialize)
+LSG_INL void g1_serialize(uint8_t* out, const g1a_t& a, bool inf) {
+  if (inf) {
+    out[0] = 0x40;
+    for (int i = 1; i < 96; i++) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, fp_from_mont(a.x));
+  fp_to_be48(out + 48, fp_from_mont(a.y));
+}
+
+// affine G2 -> 192-byte uncompressed
+LSG_INL void g2_serialize(uint8_t* out, const g2a_t& a, bool inf) {
+  if (inf) {
+    out[0] = 0x40;
+    for (int i = 1; i < 192; i++) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, fp_from_mont(a.x.c1));
+  fp_to_be48(out + 48, fp_from_mont(a.x.c0));
+  fp_to_be48(out + 96, fp_from_mont(a.y.c1));
+  fp_to_be48(out + 144, fp_from_mont(a.y.c0));
+}

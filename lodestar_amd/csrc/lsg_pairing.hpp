@@ -1,0 +1,112 @@
+// Optimal-ate Miller loop and final exponentiation for gfx950.  Replaces blst's
+// miller_loop_n / final_exp used by Pairing.commit()/finalverify() under
+// @chainsafe/blst verifyMultipleAggregateSignatures and verify
+// (packages/beacon-node/src/chain/bls/maybeBatch.ts:18,37).
+// Operation-for-operation mirror of oracle/pairing.py (dbl_step, add_step,
+// f12_mul_line, miller_loop_fast, final_exp_fast), so per-pair Miller values are
+// bit-comparable with the oracle.
+#pragma once
+#include "lsg_curve.hpp"
+
+struct line_t {
+  fp2_t l00, l01, l11;
+};
+
+// T <- 2T; line = (3b'Z^2 - Y^2, 3X^2 xP, -2YZ yP)
+LSG_NOINL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
+  fp2_t t0 = fp2_sqr(T.Y);
+  fp2_t t1 = fp2_mul(T.Y, T.Z);
+  fp2_t t2 = fp2_mul_b3(fp2_sqr(T.Z));
+  fp2_t XX = fp2_sqr(T.X);
+  line_t L;
+  L.l00 = fp2_sub(t2, t0);
+  fp2_t XX3 = fp2_add(fp2_add(XX, XX), XX);
+  L.l01 = fp2_mul_fp(XX3, xP);
+  L.l11 = fp2_mul_fp(fp2_neg(fp2_add(t1, t1)), yP);
+  fp2_t Z3 = fp2_add(t0, t0);
+  Z3 = fp2_add(Z3, Z3);
+  Z3 = fp2_add(Z3, Z3);
+  fp2_t X3 = fp2_mul(t2, Z3);
+  fp2_t Y3 = fp2_add(t0, t2);
+  Z3 = fp2_mul(t1, Z3);
+  fp2_t u1 = fp2_add(t2, t2);
+  fp2_t u2 = fp2_add(u1, t2);
+  fp2_t s0 = fp2_sub(t0, u2);
+  Y3 = fp2_mul(s0, Y3);
+  Y3 = fp2_add(X3, Y3);
+  fp2_t v1 = fp2_mul(T.X, T.Y);
+  X3 = fp2_mul(s0, v1);
+  X3 = fp2_add(X3, X3);
+  T.X = X3;
+  T.Y = Y3;
+  T.Z = Z3;
+  return L;
+}
+
+// T <- T + Q; theta = Y - yQ Z, delta = X - xQ Z; line = (delta yQ - theta xQ, theta xP, -delta yP)
+LSG_NOINL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
+  fp2_t theta = fp2_sub(T.Y, fp2_mul(Q.y, T.Z));
+  fp2_t delta = fp2_sub(T.X, fp2_mul(Q.x, T.Z));
+  line_t L;
+  L.l00 = fp2_sub(fp2_mul(delta, Q.y), fp2_mul(theta, Q.x));
+  L.l01 = fp2_mul_fp(theta, xP);
+  L.l11 = fp2_mul_fp(fp2_neg(delta), yP);
+  fp2_t C = fp2_sqr(theta);
+  fp2_t D = fp2_sqr(delta);
+  fp2_t E = fp2_mul(D, delta);
+  fp2_t F = fp2_mul(T.Z, C);
+  fp2_t G = fp2_mul(T.X, D);
+  fp2_t H = fp2_sub(fp2_add(E, F), fp2_add(G, G));
+  fp2_t X3 = fp2_mul(delta, H);
+  fp2_t Y3 = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), fp2_mul(E, T.Y));
+  fp2_t Z3 = fp2_mul(E, T.Z);
+  T.X = X3;
+  T.Y = Y3;
+  T.Z = Z3;
+  return L;
+}
+
+// f_{|x|,Q}(P) conjugated (x < 0).  P affine G1, Q affine G2, both finite.
+LSG_NOINL fp12_t miller_loop(g1a_t P, g2a_t Q) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  g2p_t T = proj_from_aff(Q);
+  line_t L = ml_dbl_step(T, P.x, P.y);
+  fp12_t f;
+  f.c0 = fp6_make(L.l00, L.l01, fp2_zero());
+  f.c1 = fp6_make(fp2_zero(), L.l11, fp2_zero());
+  // bit 62 of |x| is 1
+  L = ml_add_step(T, Q, P.x, P.y);
+  f = fp12_mul_line(f, L.l00, L.l01, L.l11);
+  for (int b = 61; b >= 0; b--) {
+    f = fp12_sqr(f);
+    L = ml_dbl_step(T, P.x, P.y);
+    f = fp12_mul_line(f, L.l00, L.l01, L.l11);
+    if ((xa >> b) & 1u) {
+      L = ml_add_step(T, Q, P.x, P.y);
+      f = fp12_mul_line(f, L.l00, L.l01, L.l11);
+    }
+  }
+  return fp12_conj(f);
+}
+
+// g^x for g in the cyclotomic subgroup
+LSG_NOINL fp12_t fp12_exp_by_x(fp12_t g) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  fp12_t r = g;
+  for (int b = 62; b >= 0; b--) {
+    r = fp12_sqr(r);
+    if ((xa >> b) & 1u) r = fp12_mul(r, g);
+  }
+  return fp12_conj(r);
+}
+
+// f^(3 (p^12 - 1)/r)   -- oracle/pairing.py:final_exp_fast
+LSG_NOINL fp12_t final_exp(fp12_t f) {
+  fp12_t f1 = fp12_mul(fp12_conj(f), fp12_inv(f));
+  fp12_t g = fp12_mul(fp12_frob2(f1), f1);
+  fp12_t t0 = fp12_mul(fp12_exp_by_x(g), fp12_conj(g));
+  t0 = fp12_mul(fp12_exp_by_x(t0), fp12_conj(t0));
+  fp12_t t1 = fp12_mul(fp12_exp_by_x(t0), fp12_frob(t0));
+  fp12_t t2 = fp12_mul(fp12_mul(fp12_exp_by_x(fp12_exp_by_x(t1)), fp12_frob2(t1)), fp12_conj(t1));
+  return fp12_mul(t2, fp12_mul(fp12_sqr(g), g));
+}

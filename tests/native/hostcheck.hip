@@ -1,0 +1,120 @@
+// TEST INFRASTRUCTURE ONLY -- host (x86) build of the kernel math headers.
+//
+// Compiles lodestar_amd/csrc/lsg_*.hpp (all functions are __host__ __device__) for the
+// CPU so tests/test_hostcheck_math.py can compare every stage of the device arithmetic
+// with the oracle inside the build container, where no GPU exists.  It is never linked
+// into, loaded by or reachable from the product library (lodestar_amd/liblodestar_bls.so);
+// the product path runs only on the GPU.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "lsg_h2c.hpp"
+#include "lsg_pairing.hpp"
+
+static fp_t rd(const uint8_t* b) { return fp_to_mont(fp_from_be48(b)); }
+static void wr(uint8_t* b, const fp_t& a) { fp_to_be48(b, fp_from_mont(a)); }
+static fp2_t rd2(const uint8_t* b) { return fp2_make(rd(b), rd(b + 48)); }  // (c0, c1)
+static void wr2(uint8_t* b, const fp2_t& a) {
+  wr(b, a.c0);
+  wr(b + 48, a.c1);
+}
+static void wr12(uint8_t* b, const fp12_t& f) {
+  const fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; i++) wr2(b + 96 * i, *c[i]);
+}
+static fp12_t rd12(const uint8_t* b) {
+  fp12_t f;
+  fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; i++) *c[i] = rd2(b + 96 * i);
+  return f;
+}
+
+extern "C" {
+
+void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr(out, fp_mul(rd(a), rd(b))); }
+void hc_fp_inv(const uint8_t* a, uint8_t* out) { wr(out, fp_inv(rd(a))); }
+void hc_fp_from_be64(const uint8_t* a, uint8_t* out) { wr(out, fp_from_be64_mod(a)); }
+void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr2(out, fp2_mul(rd2(a), rd2(b))); }
+void hc_fp2_sqr(const uint8_t* a, uint8_t* out) { wr2(out, fp2_sqr(rd2(a))); }
+void hc_fp2_inv(const uint8_t* a, uint8_t* out) { wr2(out, fp2_inv(rd2(a))); }
+int hc_fp2_sqrt(const uint8_t* a, uint8_t* out) {
+  fp2_t r;
+  bool ok = fp2_sqrt(r, rd2(a));
+  wr2(out, r);
+  return ok;
+}
+void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { wr12(out, fp12_mul(rd12(a), rd12(b))); }
+void hc_fp12_sqr(const uint8_t* a, uint8_t* out) { wr12(out, fp12_sqr(rd12(a))); }
+void hc_fp12_inv(const uint8_t* a, uint8_t* out) { wr12(out, fp12_inv(rd12(a))); }
+void hc_fp12_frob(const uint8_t* a, uint8_t* out) { wr12(out, fp12_frob(rd12(a))); }
+void hc_fp12_frob2(const uint8_t* a, uint8_t* out) { wr12(out, fp12_frob2(rd12(a))); }
+void hc_final_exp(const uint8_t* a, uint8_t* out) { wr12(out, final_exp(rd12(a))); }
+
+int hc_g2_uncompress(const uint8_t* in, uint8_t* out192) {
+  g2a_t p;
+  bool inf;
+  int e = g2_uncompress(p, inf, in);
+  if (e == 0) g2_serialize(out192, p, inf);
+  return e;
+}
+int hc_g2_in_group(const uint8_t* in192) {
+  g2a_t p;
+  bool inf;
+  int e = g2_deserialize_uncompressed(p, inf, in192);
+  if (e != 0 && e != LSG_BLST_POINT_NOT_IN_GROUP) return -e;
+  if (inf) return 1;
+  return g2_in_group(proj_from_aff(p)) ? 1 : 0;
+}
+int hc_g1_deserialize(const uint8_t* in, int len, uint8_t* out96) {
+  g1a_t p;
+  bool inf;
+  int e = g1_deserialize(p, inf, in, len);
+  if (e == 0) g1_serialize(out96, p, inf);
+  return e;
+}
+void hc_expand_xmd(const uint8_t* msg, int mlen, const uint8_t* dst, int dlen, uint8_t* out256) {
+  expand_message_xmd_256(out256, msg, mlen, dst, dlen);
+}
+void hc_sswu(const uint8_t* u96, uint8_t* out192) {
+  g2a_t p = map_to_curve_sswu(rd2(u96));
+  g2_serialize(out192, p, false);
+}
+void hc_hash_to_g2(const uint8_t* msg, int mlen, const uint8_t* dst, int dlen, uint8_t* out192) {
+  uint8_t ub[256];
+  expand_message_xmd_256(ub, msg, mlen, dst, dlen);
+  fp2_t u0 = fp2_make(fp_from_be64_mod(ub), fp_from_be64_mod(ub + 64));
+  fp2_t u1 = fp2_make(fp_from_be64_mod(ub + 128), fp_from_be64_mod(ub + 192));
+  g2p_t q0 = iso_map3(map_to_curve_sswu(u0));
+  g2p_t q1 = iso_map3(map_to_curve_sswu(u1));
+  g2p_t r = clear_cofactor_g2(g2_add(q0, q1));
+  bool inf = proj_is_inf(r);
+  g2a_t a = inf ? g2a_t{fp2_zero(), fp2_zero()} : proj_to_aff(r);
+  g2_serialize(out192, a, inf);
+}
+void hc_g1_mul_u64(const uint8_t* in96, uint64_t k, uint8_t* out96) {
+  g1a_t p;
+  bool inf;
+  g1_deserialize(p, inf, in96, 96);
+  g1p_t r = proj_mul_u64(proj_from_aff(p), k);
+  bool rinf = proj_is_inf(r);
+  g1a_t a = rinf ? g1a_t{fp_zero(), fp_zero()} : proj_to_aff(r);
+  g1_serialize(out96, a, rinf);
+}
+void hc_g2_mul_u64(const uint8_t* in192, uint64_t k, uint8_t* out192) {
+  g2a_t p;
+  bool inf;
+  g2_deserialize_uncompressed(p, inf, in192);
+  g2p_t r = proj_mul_u64(proj_from_aff(p), k);
+  bool rinf = proj_is_inf(r);
+  g2a_t a = rinf ? g2a_t{fp2_zero(), fp2_zero()} : proj_to_aff(r);
+  g2_serialize(out192, a, rinf);
+}
+void hc_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  g1a_t p;
+  g2a_t q;
+  bool inf;
+  g1_deserialize(p, inf, p96, 96);
+  g2_deserialize_uncompressed(q, inf, q192);
+  wr12(out576, miller_loop(p, q));
+}
+}

@@ -1,0 +1,223 @@
+"""Stage-by-stage parity of the kernel math headers (lodestar_amd/csrc/lsg_*.hpp) with the
+oracle, using a host (x86) build of those same headers (tests/native/hostcheck.hip).
+This runs in the CPU container; the GPU parity tests (tests/test_gpu_parity.py) repeat
+the end-to-end checks through the real HIP kernels.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle.fields import (
+    P, f2_mul, f2_sqr, f2_inv, f2_sqrt, f12_mul, f12_sqr, f12_inv, f12_frob, f12_frob2, f12_coeffs,
+)
+from oracle.curves import (
+    E1, E2, G1_GEN, G2_GEN, g1_serialize, g2_serialize, g2_compress, in_g2, BlstError, g2_uncompress,
+)
+from oracle import hash_to_curve as h2c
+from oracle.pairing import miller_loop_fast, final_exp_fast
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "native", "libhostcheck.so")
+SRC = os.path.join(HERE, "native", "hostcheck.hip")
+
+
+def _build():
+    hdrs = [os.path.join(ROOT, "lodestar_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "lodestar_amd", "csrc"))]
+    newest = max(os.path.getmtime(p) for p in hdrs + [SRC])
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
+        return
+    subprocess.check_call(["hipcc", "-x", "hip", "--cuda-host-only", "-O2", "-std=c++17", "-fPIC", "-shared",
+                           "-I", os.path.join(ROOT, "lodestar_amd", "csrc"), SRC, "-o", LIB])
+
+
+@pytest.fixture(scope="module")
+def hc():
+    try:
+        _build()
+    except (OSError, subprocess.CalledProcessError) as e:  # pragma: no cover
+        pytest.skip(f"hipcc unavailable: {e}")
+    return ctypes.CDLL(LIB)
+
+
+def be(v):
+    return int(v).to_bytes(48, "big")
+
+
+def b2(a):
+    return be(a[0]) + be(a[1])
+
+
+def ub2(b):
+    return (int.from_bytes(b[:48], "big"), int.from_bytes(b[48:96], "big"))
+
+
+def b12(f):
+    return b"".join(b2(c) for c in f12_coeffs(f))
+
+
+def ub12(b):
+    c = [ub2(b[96 * i:96 * i + 96]) for i in range(6)]
+    return ((c[0], c[1], c[2]), (c[3], c[4], c[5]))
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+rng = random.Random(1234)
+
+
+def rfp():
+    return rng.randrange(P)
+
+
+def rf2():
+    return (rfp(), rfp())
+
+
+def rf12():
+    return tuple(tuple(rf2() for _ in range(3)) for _ in range(2))
+
+
+def test_fp_mul_inv(hc):
+    for _ in range(200):
+        a, b = rfp(), rfp()
+        o = buf(48)
+        hc.hc_fp_mul(be(a), be(b), o)
+        assert int.from_bytes(o.raw, "big") == a * b % P
+    for a in [0, 1, P - 1] + [rfp() for _ in range(20)]:
+        o = buf(48)
+        hc.hc_fp_inv(be(a), o)
+        assert int.from_bytes(o.raw, "big") == (pow(a, -1, P) if a else 0)
+
+
+def test_fp_from_be64(hc):
+    for _ in range(100):
+        v = rng.getrandbits(512)
+        o = buf(48)
+        hc.hc_fp_from_be64(v.to_bytes(64, "big"), o)
+        assert int.from_bytes(o.raw, "big") == v % P
+    for v in [0, (1 << 512) - 1, P, (1 << 384) - 1]:
+        o = buf(48)
+        hc.hc_fp_from_be64(v.to_bytes(64, "big"), o)
+        assert int.from_bytes(o.raw, "big") == v % P
+
+
+def test_fp2_ops(hc):
+    for _ in range(50):
+        a, b = rf2(), rf2()
+        o = buf(96)
+        hc.hc_fp2_mul(b2(a), b2(b), o)
+        assert ub2(o.raw) == f2_mul(a, b)
+        hc.hc_fp2_sqr(b2(a), o)
+        assert ub2(o.raw) == f2_sqr(a)
+        hc.hc_fp2_inv(b2(a), o)
+        assert ub2(o.raw) == f2_inv(a)
+
+
+def test_fp2_sqrt(hc):
+    cases = [rf2() for _ in range(60)] + [(0, 0), (4, 0), (P - 4, 0), (0, 5), (rfp(), 0), (0, rfp())]
+    for a in cases:
+        o = buf(96)
+        ok = hc.hc_fp2_sqrt(b2(a), o)
+        exp = f2_sqrt(a)
+        assert bool(ok) == (exp is not None), a
+        if ok:
+            r = ub2(o.raw)
+            assert f2_sqr(r) == (a[0] % P, a[1] % P)
+
+
+def test_fp12_ops(hc):
+    for _ in range(5):
+        a, b = rf12(), rf12()
+        o = buf(576)
+        hc.hc_fp12_mul(b12(a), b12(b), o)
+        assert ub12(o.raw) == f12_mul(a, b)
+        hc.hc_fp12_sqr(b12(a), o)
+        assert ub12(o.raw) == f12_sqr(a)
+        hc.hc_fp12_inv(b12(a), o)
+        assert ub12(o.raw) == f12_inv(a)
+        hc.hc_fp12_frob(b12(a), o)
+        assert ub12(o.raw) == f12_frob(a)
+        hc.hc_fp12_frob2(b12(a), o)
+        assert ub12(o.raw) == f12_frob2(a)
+
+
+def test_g2_uncompress_and_subgroup(hc):
+    import json
+    pts = json.load(open(os.path.join(HERE, "golden", "mainnet_g2_points.json")))
+    for hx in pts:
+        o = buf(192)
+        assert hc.hc_g2_uncompress(bytes.fromhex(hx), o) == 0
+        assert o.raw == g2_serialize(g2_uncompress(bytes.fromhex(hx)))
+        assert hc.hc_g2_in_group(o.raw) == 1
+    # random x: decompress where on curve; not in G2 w.h.p.
+    hits = 0
+    for _ in range(30):
+        x = rf2()
+        b = bytearray(be(x[1]) + be(x[0]))
+        b[0] |= 0x80
+        o = buf(192)
+        e = hc.hc_g2_uncompress(bytes(b), o)
+        try:
+            exp = g2_uncompress(bytes(b))
+            assert e == 0 and o.raw == g2_serialize(exp)
+            assert hc.hc_g2_in_group(o.raw) == int(in_g2(exp))
+            hits += 1
+        except BlstError as err:
+            assert e == err.code
+    assert hits > 5
+    bad = json.load(open(os.path.join(HERE, "golden", "mainnet_g2_points_bad.json")))
+    for item in bad:
+        o = buf(192)
+        assert hc.hc_g2_uncompress(bytes.fromhex(item["sig"]), o) == 2
+
+
+def test_hash_to_g2(hc):
+    msgs = [b"", b"abc", bytes(32), bytes(range(32)), os.urandom(32), b"lodestar" * 20]
+    for m in msgs:
+        o = buf(192)
+        hc.hc_hash_to_g2(m, len(m), h2c.DST_POP, len(h2c.DST_POP), o)
+        assert o.raw == g2_serialize(h2c.hash_to_g2(m)), m
+
+
+def test_expand_and_sswu(hc):
+    m = b"sswu"
+    o = buf(256)
+    hc.hc_expand_xmd(m, len(m), h2c.DST_POP, len(h2c.DST_POP), o)
+    assert o.raw == h2c.expand_message_xmd(m, h2c.DST_POP, 256)
+    for _ in range(10):
+        u = rf2()
+        o = buf(192)
+        hc.hc_sswu(b2(u), o)
+        assert o.raw == g2_serialize(h2c.map_to_curve_sswu(u))
+
+
+def test_scalar_mul(hc):
+    pk = E1.mul(G1_GEN, 0xABCDEF)
+    Q = E2.mul(G2_GEN, 12345)
+    for k in [1, 2, 3, (1 << 64) - 1, rng.getrandbits(64), rng.getrandbits(64) | (1 << 63)]:
+        hc.hc_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+        hc.hc_g2_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+        o = buf(96)
+        hc.hc_g1_mul_u64(g1_serialize(pk), k, o)
+        assert o.raw == g1_serialize(E1.mul(pk, k))
+        o = buf(192)
+        hc.hc_g2_mul_u64(g2_serialize(Q), k, o)
+        assert o.raw == g2_serialize(E2.mul(Q, k))
+
+
+def test_miller_loop_and_final_exp(hc):
+    pk = E1.mul(G1_GEN, 777)
+    Q = E2.mul(G2_GEN, 999)
+    o = buf(576)
+    hc.hc_miller(g1_serialize(pk), g2_serialize(Q), o)
+    f = miller_loop_fast(pk, Q)
+    assert ub12(o.raw) == f
+    o2 = buf(576)
+    hc.hc_final_exp(o.raw, o2)
+    assert ub12(o2.raw) == final_exp_fast(f)
