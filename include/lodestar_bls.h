@@ -1,0 +1,154 @@
+/*
+ * lodestar_bls.h -- C ABI of the MI355X (gfx950) BLS12-381 signature-set verifier.
+ *
+ * Drop-in boundary for Lodestar's IBlsVerifier hot path
+ * (/root/reference/packages/beacon-node/src/chain/bls/interface.ts:20-51).  It replaces
+ * the worker threads of BlsMultiThreadWorkerPool together with the crypto library they
+ * call (@chainsafe/bls@7.1.1 -> @chainsafe/blst@0.2.8 -> supranational blst):
+ *
+ *   lsg_verify_jobs        <- multithread/worker.ts:30-106 verifyManySignatureSets
+ *                             (+ maybeBatch.ts:16-39 verifySignatureSetsMaybeBatch,
+ *                                worker.ts:108-114 deserializeSet)
+ *   lsg_verify_sets        <- maybeBatch.ts:16-39 for one call (BlsSingleThreadVerifier,
+ *                             singleThread.ts:14-35; verifyOnMainThread, index.ts:155-168)
+ *   lsg_aggregate_pubkeys  <- utils.ts:11 PublicKey.aggregate (+ toBytes, index.ts:177)
+ *   lsg_hash_to_g2         <- blst Hash_to_G2 inside Pairing.mul_n_aggregate
+ *   lsg_sig_decode         <- maybeBatch.ts:23,36 Signature.fromBytes(bytes, affine, true)
+ *   lsg_batch_partial /    <- the per-GPU half of verifyMultipleSignatures for the
+ *   lsg_final_verify          node-sharded path: Miller-loop product
+ *                             per shard, all-gathered by the caller, one final exponentiation
+ *
+ * Plain pointers and sizes only; every call returns an int status (LSG_OK = 0) and never
+ * throws.  Verdicts and error codes follow blst's numbering (BLST_* below).  All compute
+ * runs in HIP kernels on the context's device; there is no CPU fallback -- lsg_init fails
+ * with LSG_ERR_NO_DEVICE when no gfx950 device is present.
+ */
+#ifndef LODESTAR_BLS_H
+#define LODESTAR_BLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- call status */
+#define LSG_OK 0
+#define LSG_ERR_INVALID_ARG 1
+#define LSG_ERR_NO_DEVICE 2
+#define LSG_ERR_DEVICE 3
+#define LSG_ERR_NOMEM 4
+#define LSG_ERR_CLOSED 5
+
+/* ---- blst error codes (blst.h BLST_ERROR) + @chainsafe/blst's size error */
+#define LSG_BLST_SUCCESS 0
+#define LSG_BLST_BAD_ENCODING 1
+#define LSG_BLST_POINT_NOT_ON_CURVE 2
+#define LSG_BLST_POINT_NOT_IN_GROUP 3
+#define LSG_BLST_AGGR_TYPE_MISMATCH 4
+#define LSG_BLST_VERIFY_FAIL 5
+#define LSG_BLST_PK_IS_INFINITY 6
+#define LSG_BLST_BAD_SCALAR 7
+#define LSG_BLST_INVALID_SIZE 10
+/* non-blst job errors */
+#define LSG_ERR_EMPTY_SET 100        /* maybeBatch.ts:29-31 "Empty signature set" */
+#define LSG_ERR_EMPTY_AGGREGATE 101  /* PublicKey.aggregate([]) "EMPTY_AGGREGATE_ARRAY" */
+
+/* ---- job verdicts (WorkResult<boolean>, multithread/types.ts:21-24) */
+#define LSG_INVALID 0 /* {code: success, result: false} */
+#define LSG_VALID 1   /* {code: success, result: true}  */
+#define LSG_ERROR 2   /* {code: error, error}           */
+
+/* ---- job flags (VerifySignatureOpts, interface.ts:3-18; priority/same-message are extensions) */
+#define LSG_JOB_BATCHABLE 1u
+#define LSG_JOB_PRIORITY 2u
+
+typedef struct lsg_ctx lsg_ctx;
+
+/* One signature set (ISignatureSet, state-transition/src/util/signatureSets.ts:10-22).
+ * Pubkeys are the set's n_pks keys back to back, each pk_len bytes (48 compressed or
+ * 96 uncompressed, ZCash encoding).  n_pks == 1 is a "single" set, > 1 an "aggregate"
+ * set whose keys are summed on the GPU.  sig_len other than 96/192 yields
+ * BLST_INVALID_SIZE for the set, exactly as Signature.fromBytes does. */
+typedef struct {
+  const uint8_t* pks;
+  uint32_t pk_len;
+  uint32_t n_pks;
+  const uint8_t* msg;
+  uint32_t msg_len;
+  const uint8_t* sig;
+  uint32_t sig_len;
+} lsg_set;
+
+/* One job = one BlsWorkReq (multithread/types.ts:14-17): the sets of one
+ * verifySignatureSets chunk (<= 128 sets) plus its options. */
+typedef struct {
+  const lsg_set* sets;
+  uint32_t n_sets;
+  uint32_t flags;
+} lsg_job;
+
+typedef struct {
+  int32_t status;   /* LSG_VALID / LSG_INVALID / LSG_ERROR */
+  int32_t err_code; /* BLST_* or LSG_ERR_EMPTY_* when status == LSG_ERROR */
+} lsg_job_result;
+
+/* BlsWorkResult counters (multithread/types.ts:26-38) */
+typedef struct {
+  uint32_t batch_retries;
+  uint32_t batch_sigs_success;
+  uint64_t start_ns;
+  uint64_t end_ns;
+  uint32_t n_final_exps; /* final exponentiations launched (batches + retries) */
+  uint32_t reserved;
+} lsg_stats;
+
+/* Context owning one device's streams and buffers.  device_ordinal < 0 -> device 0.
+ * Calls on one context are serialised internally; use one context per thread/device. */
+int lsg_init(int device_ordinal, lsg_ctx** out);
+int lsg_destroy(lsg_ctx* ctx);
+const char* lsg_last_error(lsg_ctx* ctx);
+int lsg_device_name(lsg_ctx* ctx, char* buf, size_t len);
+
+/* worker.ts:30-106 for one work package.  seed != 0 makes the RLC randomizers
+ * deterministic (tests); seed == 0 draws them from the OS CSPRNG.  results[n_jobs]. */
+int lsg_verify_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_job_result* results,
+                    lsg_stats* stats);
+
+/* maybeBatch.ts:16-39 over one list of sets (no retry): *result = one lsg_job_result. */
+int lsg_verify_sets(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_job_result* result);
+
+/* PublicKey.aggregate(pks).toBytes(uncompressed): out96 receives the 96-byte affine sum.
+ * *err_code = BLST_* for a bad input key, LSG_ERR_EMPTY_AGGREGATE for n == 0. */
+int lsg_aggregate_pubkeys(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96,
+                          int32_t* err_code);
+
+/* hash_to_G2(msg_i, DST) for n messages of msg_len bytes each -> n x 192-byte uncompressed points. */
+int lsg_hash_to_g2(lsg_ctx* ctx, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst,
+                   uint32_t dst_len, uint8_t* out192);
+
+/* Signature.fromBytes(sig, affine, validate=true) for n signatures of sig_len bytes:
+ * out192[i] = uncompressed affine point, err[i] = BLST_* (0 = ok). */
+int lsg_sig_decode(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, size_t n, uint8_t* out192, int32_t* err);
+
+/* Sharded batch: one shard's sets -> its un-exponentiated Miller product
+ * (576 bytes: 12 canonical big-endian Fp in tower order), per-set error codes.
+ * *any_error != 0 means the shard cannot be batched (caller falls back to retry). */
+int lsg_batch_partial(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
+                      int32_t* set_err, int32_t* any_error);
+/* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1). */
+int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
+
+/* Integer-VALU roofline probe: runs a throughput kernel of dependent-free 381-bit
+ * Montgomery multiplications; reports Fp-mul/s and v_mad_u64_u32/s (x300 per mul). */
+int lsg_probe_fp_mul_rate(lsg_ctx* ctx, double* fp_mul_per_s, double* mad_per_s);
+
+/* Per-kernel timing of the last lsg_verify_jobs/lsg_batch_partial call, from HIP events
+ * on the context's stream: names[i] / ms[i] for up to max entries; returns count. */
+int lsg_last_kernel_times(lsg_ctx* ctx, const char** names, double* ms, int max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LODESTAR_BLS_H */

@@ -1,0 +1,247 @@
+"""ctypes binding of the C ABI in include/lodestar_bls.h (lodestar_amd/liblodestar_bls.so).
+
+The library is built in-tree by ``lodestar_amd.build`` (hipcc --offload-arch=gfx950).
+There is no fallback: if the library or a gfx950 device is missing, every entry point
+raises ``NativeUnavailable``.
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblodestar_bls.so")
+
+LSG_OK = 0
+LSG_ERR_NO_DEVICE = 2
+
+LSG_INVALID = 0
+LSG_VALID = 1
+LSG_ERROR = 2
+
+LSG_JOB_BATCHABLE = 1
+LSG_JOB_PRIORITY = 2
+
+BLST_NAMES = {
+    0: "BLST_SUCCESS", 1: "BLST_BAD_ENCODING", 2: "BLST_POINT_NOT_ON_CURVE", 3: "BLST_POINT_NOT_IN_GROUP",
+    4: "BLST_AGGR_TYPE_MISMATCH", 5: "BLST_VERIFY_FAIL", 6: "BLST_PK_IS_INFINITY", 7: "BLST_BAD_SCALAR",
+    10: "BLST_INVALID_SIZE",
+}
+LSG_ERR_EMPTY_SET = 100
+LSG_ERR_EMPTY_AGGREGATE = 101
+
+
+def error_message(code):
+    """Error text in the form the reference's callers match on: the BLST code name is a
+    substring (multithread.test.ts:97 'BLST_INVALID_SIZE'; spec harness 'BLST_ERROR')."""
+    if code == LSG_ERR_EMPTY_SET:
+        return "Empty signature set"
+    if code == LSG_ERR_EMPTY_AGGREGATE:
+        return "EMPTY_AGGREGATE_ARRAY"
+    return "BLST_ERROR: " + BLST_NAMES.get(code, f"BLST_UNKNOWN_{code}")
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class LsgSet(ctypes.Structure):
+    _fields_ = [
+        ("pks", ctypes.c_void_p), ("pk_len", ctypes.c_uint32), ("n_pks", ctypes.c_uint32),
+        ("msg", ctypes.c_void_p), ("msg_len", ctypes.c_uint32),
+        ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_uint32),
+    ]
+
+
+class LsgJob(ctypes.Structure):
+    _fields_ = [("sets", ctypes.POINTER(LsgSet)), ("n_sets", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class LsgJobResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("err_code", ctypes.c_int32)]
+
+
+class LsgStats(ctypes.Structure):
+    _fields_ = [
+        ("batch_retries", ctypes.c_uint32), ("batch_sigs_success", ctypes.c_uint32),
+        ("start_ns", ctypes.c_uint64), ("end_ns", ctypes.c_uint64),
+        ("n_final_exps", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+EXPORTS = [
+    "lsg_init", "lsg_destroy", "lsg_last_error", "lsg_device_name", "lsg_verify_jobs", "lsg_verify_sets",
+    "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
+    "lsg_probe_fp_mul_rate", "lsg_last_kernel_times",
+]
+
+
+def load_library(path=LIB_PATH):
+    """Load the shared library and declare prototypes (works without a GPU)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path == LIB_PATH:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(f"{path} not built (run python -c 'import __graft_entry__; __graft_entry__.build()')")
+        lib = ctypes.CDLL(path)
+        vp, u32, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_size_t
+        pi32 = ctypes.POINTER(ctypes.c_int32)
+        lib.lsg_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        lib.lsg_destroy.argtypes = [vp]
+        lib.lsg_last_error.argtypes = [vp]
+        lib.lsg_last_error.restype = ctypes.c_char_p
+        lib.lsg_device_name.argtypes = [vp, ctypes.c_char_p, sz]
+        lib.lsg_verify_jobs.argtypes = [vp, ctypes.POINTER(LsgJob), sz, u64, ctypes.POINTER(LsgJobResult),
+                                        ctypes.POINTER(LsgStats)]
+        lib.lsg_verify_sets.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.POINTER(LsgJobResult)]
+        lib.lsg_aggregate_pubkeys.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
+        lib.lsg_hash_to_g2.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, u32, ctypes.c_char_p]
+        lib.lsg_sig_decode.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
+        lib.lsg_batch_partial.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.c_char_p, pi32, pi32]
+        lib.lsg_final_verify.argtypes = [vp, ctypes.c_char_p, sz, pi32]
+        lib.lsg_probe_fp_mul_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        lib.lsg_last_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                              ctypes.c_int]
+        for name in EXPORTS:
+            if name != "lsg_last_error":
+                getattr(lib, name).restype = ctypes.c_int
+        if path == LIB_PATH:
+            _lib = lib
+        return lib
+
+
+class SetBuffer:
+    """Keeps the bytes of a list of sets alive while the C call runs."""
+
+    def __init__(self, sets):
+        # sets: iterable of (pks: list[bytes], msg: bytes, sig: bytes)
+        self._keep = []
+        sets = list(sets)
+        self.arr = (LsgSet * max(len(sets), 1))()
+        for i, (pks, msg, sig) in enumerate(sets):
+            pk_len = len(pks[0]) if pks else 96
+            if any(len(p) != pk_len for p in pks):
+                raise ValueError("all pubkeys of one set must share one encoding length")
+            pkb = b"".join(pks)
+            for b in (pkb, msg, sig):
+                self._keep.append(b)
+            s = self.arr[i]
+            s.pks = ctypes.cast(ctypes.c_char_p(pkb), ctypes.c_void_p) if pkb else None
+            s.pk_len = pk_len
+            s.n_pks = len(pks)
+            s.msg = ctypes.cast(ctypes.c_char_p(msg), ctypes.c_void_p) if msg else None
+            s.msg_len = len(msg)
+            s.sig = ctypes.cast(ctypes.c_char_p(sig), ctypes.c_void_p) if sig else None
+            s.sig_len = len(sig)
+        self.n = len(sets)
+
+
+class Context:
+    """One device context (lsg_ctx).  Raises NativeUnavailable without a gfx950 GPU."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.lsg_init(int(device), ctypes.byref(h))
+        if rc != LSG_OK:
+            raise NativeUnavailable(f"lsg_init({device}) failed with status {rc} (no gfx950 device?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lsg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _check(self, rc, what):
+        if rc != LSG_OK:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.lsg_last_error(self.h).decode(errors='replace')}")
+
+    def device_name(self):
+        b = ctypes.create_string_buffer(256)
+        self._check(self.lib.lsg_device_name(self.h, b, 256), "lsg_device_name")
+        return b.value.decode()
+
+    def verify_jobs(self, jobs, seed=0):
+        """jobs: list of (sets, flags) with sets = list of (pks, msg, sig).
+        Returns (results list of (status, err_code), stats dict)."""
+        bufs = [SetBuffer(sets) for sets, _ in jobs]
+        arr = (LsgJob * max(len(jobs), 1))()
+        for i, ((sets, flags), b) in enumerate(zip(jobs, bufs)):
+            arr[i].sets = b.arr
+            arr[i].n_sets = b.n
+            arr[i].flags = flags
+        res = (LsgJobResult * max(len(jobs), 1))()
+        st = LsgStats()
+        self._check(self.lib.lsg_verify_jobs(self.h, arr, len(jobs), seed, res, ctypes.byref(st)), "lsg_verify_jobs")
+        out = [(res[i].status, res[i].err_code) for i in range(len(jobs))]
+        stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
+        return out, stats
+
+    def verify_sets(self, sets, seed=0):
+        b = SetBuffer(sets)
+        res = LsgJobResult()
+        self._check(self.lib.lsg_verify_sets(self.h, b.arr, b.n, seed, ctypes.byref(res)), "lsg_verify_sets")
+        return res.status, res.err_code
+
+    def aggregate_pubkeys(self, pks):
+        pk_len = len(pks[0]) if pks else 96
+        out = ctypes.create_string_buffer(96)
+        err = ctypes.c_int32()
+        self._check(self.lib.lsg_aggregate_pubkeys(self.h, b"".join(pks), pk_len, len(pks), out, ctypes.byref(err)),
+                    "lsg_aggregate_pubkeys")
+        return out.raw, err.value
+
+    def hash_to_g2(self, msgs, dst=b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"):
+        if not msgs:
+            return []
+        ml = len(msgs[0])
+        assert all(len(m) == ml for m in msgs)
+        out = ctypes.create_string_buffer(192 * len(msgs))
+        self._check(self.lib.lsg_hash_to_g2(self.h, b"".join(msgs), ml, len(msgs), dst, len(dst), out), "lsg_hash_to_g2")
+        return [out.raw[192 * i:192 * i + 192] for i in range(len(msgs))]
+
+    def sig_decode(self, sigs):
+        if not sigs:
+            return []
+        sl = len(sigs[0])
+        assert all(len(s) == sl for s in sigs)
+        out = ctypes.create_string_buffer(192 * len(sigs))
+        err = (ctypes.c_int32 * len(sigs))()
+        self._check(self.lib.lsg_sig_decode(self.h, b"".join(sigs), sl, len(sigs), out, err), "lsg_sig_decode")
+        return [(out.raw[192 * i:192 * i + 192], err[i]) for i in range(len(sigs))]
+
+    def batch_partial(self, sets, seed=0):
+        b = SetBuffer(sets)
+        out = ctypes.create_string_buffer(576)
+        errs = (ctypes.c_int32 * max(b.n, 1))()
+        anyerr = ctypes.c_int32()
+        self._check(self.lib.lsg_batch_partial(self.h, b.arr, b.n, seed, out, errs, ctypes.byref(anyerr)),
+                    "lsg_batch_partial")
+        return out.raw, [errs[i] for i in range(b.n)], bool(anyerr.value)
+
+    def final_verify(self, partials):
+        v = ctypes.c_int32()
+        self._check(self.lib.lsg_final_verify(self.h, b"".join(partials), len(partials), ctypes.byref(v)),
+                    "lsg_final_verify")
+        return bool(v.value)
+
+    def probe_fp_mul_rate(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.lsg_probe_fp_mul_rate(self.h, ctypes.byref(a), ctypes.byref(b)), "lsg_probe_fp_mul_rate")
+        return a.value, b.value
+
+    def last_kernel_times(self, max_entries=64):
+        names = (ctypes.c_char_p * max_entries)()
+        ms = (ctypes.c_double * max_entries)()
+        n = self.lib.lsg_last_kernel_times(self.h, names, ms, max_entries)
+        return [(names[i].decode(), ms[i]) for i in range(n)]

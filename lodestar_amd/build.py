@@ -1,0 +1,51 @@
+"""In-tree build of the gfx950 HIP library (lodestar_amd/liblodestar_bls.so).
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build container; the
+built .so travels to the GPU box with the repository snapshot.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "liblodestar_bls.so")
+SOURCES = ["lsg_bls.hip"]
+HEADERS = ["lsg_field.hpp", "lsg_curve.hpp", "lsg_h2c.hpp", "lsg_pairing.hpp", "lsg_constants.hpp"]
+
+
+def hipcc():
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_rebuild():
+    if not os.path.exists(OUT):
+        return True
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "lodestar_bls.h"),
+                                                                  os.path.abspath(__file__)]
+    return max(os.path.getmtime(d) for d in deps if os.path.exists(d)) > os.path.getmtime(OUT)
+
+
+def build(force=False, verbose=True):
+    gen = os.path.join(ROOT, "tools", "gen_constants.py")
+    const = os.path.join(CSRC, "lsg_constants.hpp")
+    if not os.path.exists(const) or os.path.getmtime(gen) > os.path.getmtime(const):
+        subprocess.check_call([sys.executable, gen, const])
+    if not force and not needs_rebuild():
+        return OUT
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", CSRC,
+           "-I", os.path.join(ROOT, "include")] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
+    if verbose:
+        print("[lodestar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -290,18 +290,19 @@ LSG_INL bool fp_canon_lt_p(const fp_t& a) {
   return br != 0;
 }
 
-// Status codes, numerically equal to blst's BLST_ERROR (+ wrapper's size error)
-enum {
-  LSG_BLST_SUCCESS = 0,
-  LSG_BLST_BAD_ENCODING = 1,
-  LSG_BLST_POINT_NOT_ON_CURVE = 2,
-  LSG_BLST_POINT_NOT_IN_GROUP = 3,
-  LSG_BLST_AGGR_TYPE_MISMATCH = 4,
-  LSG_BLST_VERIFY_FAIL = 5,
-  LSG_BLST_PK_IS_INFINITY = 6,
-  LSG_BLST_BAD_SCALAR = 7,
-  LSG_BLST_INVALID_SIZE = 10,
-};
+// Status codes, numerically equal to blst's BLST_ERROR (+ wrapper's size error); the
+// same values as include/lodestar_bls.h.
+#ifndef LSG_BLST_SUCCESS
+#define LSG_BLST_SUCCESS 0
+#define LSG_BLST_BAD_ENCODING 1
+#define LSG_BLST_POINT_NOT_ON_CURVE 2
+#define LSG_BLST_POINT_NOT_IN_GROUP 3
+#define LSG_BLST_AGGR_TYPE_MISMATCH 4
+#define LSG_BLST_VERIFY_FAIL 5
+#define LSG_BLST_PK_IS_INFINITY 6
+#define LSG_BLST_BAD_SCALAR 7
+#define LSG_BLST_INVALID_SIZE 10
+#endif
 
 // blst POINTonE2_Uncompress_Z (96 bytes).  Sets *inf for the infinity encoding.
 LSG_INL int g2_uncompress(g2a_t& out, bool& inf, const uint8_t* in) {

@@ -104,21 +104,24 @@ LSG_INL fp_t fp_neg(const fp_t& a) {
 }
 
 // Montgomery product a*b/R mod p, "no-carry" CIOS (valid since p[11] < 2^31 - 1).
-// Inputs: a < 2^384, b < p (a may be an unreduced 384-bit value: a*b < pR).
-LSG_NOINL fp_t fp_mul(fp_t a, fp_t b) {
+// Inputs: a, b < p.  The call boundary uses 12-wide vectors, which the AMDGPU calling
+// convention passes and returns in VGPRs (a struct return would go through scratch).
+typedef uint32_t lsg_u32x12 __attribute__((ext_vector_type(12)));
+
+LSG_NOINL lsg_u32x12 fp_mul_core(lsg_u32x12 a, lsg_u32x12 b) {
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; j++) t[j] = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) {
-    uint64_t s = (uint64_t)a.l[0] * b.l[i] + t[0];
+    uint64_t s = (uint64_t)a[0] * b[i] + t[0];
     t[0] = (uint32_t)s;
     uint64_t A = s >> 32;
     uint32_t m = t[0] * LSG_N0P;
     uint64_t C = ((uint64_t)m * LSG_P[0] + t[0]) >> 32;
 #pragma unroll
     for (int j = 1; j < 12; j++) {
-      s = (uint64_t)a.l[j] * b.l[i] + t[j] + A;
+      s = (uint64_t)a[j] * b[i] + t[j] + A;
       A = s >> 32;
       uint64_t s2 = (uint64_t)m * LSG_P[j] + (uint32_t)s + C;
       t[j - 1] = (uint32_t)s2;
@@ -126,10 +129,29 @@ LSG_NOINL fp_t fp_mul(fp_t a, fp_t b) {
     }
     t[11] = (uint32_t)(C + A);
   }
-  fp_t r;
+  // conditional final subtraction
+  uint32_t d[12];
+  uint32_t br = 0;
 #pragma unroll
-  for (int j = 0; j < 12; j++) r.l[j] = t[j];
-  return fp_reduce_once(r);
+  for (int j = 0; j < 12; j++) d[j] = __builtin_subc(t[j], LSG_P[j], br, &br);
+  lsg_u32x12 r;
+#pragma unroll
+  for (int j = 0; j < 12; j++) r[j] = br ? t[j] : d[j];
+  return r;
+}
+
+LSG_INL fp_t fp_mul(const fp_t& a, const fp_t& b) {
+  lsg_u32x12 x, y;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    x[i] = a.l[i];
+    y[i] = b.l[i];
+  }
+  lsg_u32x12 r = fp_mul_core(x, y);
+  fp_t o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o.l[i] = r[i];
+  return o;
 }
 
 LSG_INL fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
