@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Benchmark: BLS signature sets verified/sec on MI355X (BASELINE.json metric).
+
+Workload ("epoch firehose"): every GPU verifies a shard of 4096
+single-pubkey gossip-attestation sets per step (weak scaling: at 8 GPUs the node covers the
+~32k-set mainnet slot).  Keys are the interop keys sk_{v mod 1024}
+(packages/state-transition/src/util/interop.ts:19-22), messages sha256(b"lodestar-mi355x" ||
+b"firehose" || i), signatures sk*H(m) -- synthetic, generated on the GPU before timing.
+
+One step = the sharded hot path of SURVEY.md 8(e) on inputs already resident in HBM:
+  per GPU  lsg_batch_run: decode + subgroup-check signatures, decode pubkeys, hash_to_G2,
+           64-bit RLC scalars, per-set Miller loops, signature-sum Miller loop, Fp12 product
+  node     all_gather of the 576-byte Fp12 partials (RCCL over xGMI when N > 1)
+  rank 0.. lsg_final_verify: product of partials + one final exponentiation -> verdict
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+import argparse
+import hashlib
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+METRIC = "BLS signature sets verified/sec (whole node) at 1/2/4/8 MI355X; p50 batch latency"
+
+
+def interop_sk(i):
+    return int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER
+
+
+def make_shard(ctx, rank, n):
+    keys = 1024
+    sks = [interop_sk(i) for i in range(keys)]
+    pks = ctx.sk_to_pk(sks)
+    base = rank * n
+    msgs = [hashlib.sha256(b"lodestar-mi355x" + b"firehose" + (base + i).to_bytes(8, "little")).digest()
+            for i in range(n)]
+    sigs = ctx.sign([sks[(base + i) % keys] for i in range(n)], msgs)
+    return [([pks[(base + i) % keys]], msgs[i], sigs[i]) for i in range(n)]
+
+
+def cpu_baseline_oracle(sets, budget_s=12.0):
+    """Reference-semantics CPU path: the oracle (pure Python, 1 core) verifying 16-set RLC
+    batches of the same workload (worker.ts chunking), bounded to ~budget_s seconds."""
+    from oracle import verifier as ov
+    done = 0
+    t0 = time.time()
+    i = 0
+    while time.time() - t0 < budget_s and i < len(sets):
+        chunk = sets[i:i + 16]
+        ok = ov.verify_signature_sets_maybe_batch(
+            [{"publicKey": ov.public_key_from_bytes(p[0]), "message": m, "signature": s} for p, m, s in chunk])
+        assert ok
+        done += len(chunk)
+        i += 16
+    dt = time.time() - t0
+    return {"value": done / dt, "unit": "sets/s", "cores": 1, "kind": "port",
+            "sample": f"{done} sets of this workload in 16-set RLC batches (oracle/, pure Python, 1 thread) in {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sets-per-gpu", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from lodestar_amd._native import Context
+    ctx = Context(local)
+    n = args.sets_per_gpu
+    sets = make_shard(ctx, rank, n)
+    ctx.batch_stage(sets, seed=0x5EED + rank)
+
+    def gather(part):
+        if dist is None:
+            return [part]
+        import torch
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda(local)
+        out = torch.empty(world * 576, dtype=torch.uint8, device=t.device)
+        dist.all_gather_into_tensor(out, t)
+        b = out.cpu().numpy().tobytes()
+        return [b[576 * k:576 * k + 576] for k in range(world)]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def step():
+        part, anyerr = ctx.batch_run()
+        parts = gather(part)
+        ok = ctx.final_verify(parts)
+        if anyerr or not ok:
+            raise SystemExit(f"rank {rank}: verification failed (anyerr={anyerr}, verdict={ok})")
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    lat = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s0 = time.perf_counter()
+        step()
+        lat.append(time.perf_counter() - s0)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        te = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+
+    # kernel-level roofline for the dominant kernel of the last step (HIP events on ctx's stream)
+    ctx.batch_run()
+    ktimes = ctx.last_kernel_times()
+    opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
+    probe_fp, probe_mad = ctx.probe_fp_mul_rate()
+    peak_mad = float(os.environ.get("LSG_PEAK_MAD_PER_S", "2.827e13"))  # measured v_mad_u64_u32 peak (profiles/)
+    agg = {}
+    for name, ms in ktimes:
+        agg[name] = agg.get(name, 0.0) + ms
+    dom = max(agg, key=agg.get)
+    stage_of = {"k_miller_sets": "miller", "k_hash_map": "hash_map", "k_sig_scale": "sig_scale",
+                "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
+    roof = None
+    if dom in stage_of:
+        muls = opc["stage_fp_muls"][stage_of[dom]] * n
+        achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] * 1e-3) / 1e12
+        peak = peak_mad / 1e12
+        roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
+                "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
+    total_sets = n * world * args.steps
+    value = total_sets / elapsed
+    per_set_muls = opc["batched_single_set_fp_muls"]
+    node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_oracle(sets)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "firehose-32k shard (SURVEY 8d config D): single-pubkey gossip sets, RLC batch "
+                                   "per GPU, RCCL all-gather of Fp12 partials, one final exponentiation",
+                       "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
+                       "parallelism": f"shard{world}"},
+            "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
+            "roofline": roof,
+            "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
+            "kernel_ms": {k: round(v, 3) for k, v in agg.items()},
+            "probe_lane_fp_mul_per_s": probe_fp,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -137,8 +137,17 @@ int lsg_sig_decode(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, size_t n
  * *any_error != 0 means the shard cannot be batched (caller falls back to retry). */
 int lsg_batch_partial(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
                       int32_t* set_err, int32_t* any_error);
+/* The same in two halves: stage copies the shard's inputs (and randomizers) into device
+ * memory; run executes the kernels on the resident inputs (the benchmark times only run). */
+int lsg_batch_stage(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed);
+int lsg_batch_run(lsg_ctx* ctx, uint8_t* out576, int32_t* set_err, int32_t* any_error);
 /* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1). */
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
+
+/* Test/bench input generation (not on the verify path): sig_i = sk_i * H(m_i) compressed,
+ * pk_i = sk_i * G1 uncompressed; sks are 32-byte big-endian secret keys. */
+int lsg_sign(lsg_ctx* ctx, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96);
+int lsg_sk_to_pk(lsg_ctx* ctx, const uint8_t* sks32, size_t n, uint8_t* out96);
 
 /* Integer-VALU roofline probe: runs a throughput kernel of dependent-free 381-bit
  * Montgomery multiplications; reports Fp-mul/s and v_mad_u64_u32/s (x300 per mul). */

@@ -74,7 +74,8 @@ _lib_lock = threading.Lock()
 EXPORTS = [
     "lsg_init", "lsg_destroy", "lsg_last_error", "lsg_device_name", "lsg_verify_jobs", "lsg_verify_sets",
     "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
-    "lsg_probe_fp_mul_rate", "lsg_last_kernel_times",
+    "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
+    "lsg_batch_stage", "lsg_batch_run",
 ]
 
 
@@ -105,6 +106,10 @@ def load_library(path=LIB_PATH):
         lib.lsg_probe_fp_mul_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         lib.lsg_last_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                               ctypes.c_int]
+        lib.lsg_sign.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u32, sz, ctypes.c_char_p]
+        lib.lsg_sk_to_pk.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p]
+        lib.lsg_batch_stage.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64]
+        lib.lsg_batch_run.argtypes = [vp, ctypes.c_char_p, pi32, pi32]
         for name in EXPORTS:
             if name != "lsg_last_error":
                 getattr(lib, name).restype = ctypes.c_int
@@ -229,11 +234,41 @@ class Context:
                     "lsg_batch_partial")
         return out.raw, [errs[i] for i in range(b.n)], bool(anyerr.value)
 
+    def batch_stage(self, sets, seed=0):
+        self._staged = SetBuffer(sets)
+        self._check(self.lib.lsg_batch_stage(self.h, self._staged.arr, self._staged.n, seed), "lsg_batch_stage")
+        self._staged_n = self._staged.n
+
+    def batch_run(self):
+        out = ctypes.create_string_buffer(576)
+        errs = (ctypes.c_int32 * max(self._staged_n, 1))()
+        anyerr = ctypes.c_int32()
+        self._check(self.lib.lsg_batch_run(self.h, out, errs, ctypes.byref(anyerr)), "lsg_batch_run")
+        return out.raw, bool(anyerr.value)
+
     def final_verify(self, partials):
         v = ctypes.c_int32()
         self._check(self.lib.lsg_final_verify(self.h, b"".join(partials), len(partials), ctypes.byref(v)),
                     "lsg_final_verify")
         return bool(v.value)
+
+    def sign(self, sks, msgs):
+        """sks: list of ints (< r); msgs: equal-length bytes.  Returns compressed signatures."""
+        if not sks:
+            return []
+        ml = len(msgs[0])
+        out = ctypes.create_string_buffer(96 * len(sks))
+        skb = b"".join(int(k).to_bytes(32, "big") for k in sks)
+        self._check(self.lib.lsg_sign(self.h, skb, b"".join(msgs), ml, len(sks), out), "lsg_sign")
+        return [out.raw[96 * i:96 * i + 96] for i in range(len(sks))]
+
+    def sk_to_pk(self, sks):
+        if not sks:
+            return []
+        out = ctypes.create_string_buffer(96 * len(sks))
+        skb = b"".join(int(k).to_bytes(32, "big") for k in sks)
+        self._check(self.lib.lsg_sk_to_pk(self.h, skb, len(sks), out), "lsg_sk_to_pk")
+        return [out.raw[96 * i:96 * i + 96] for i in range(len(sks))]
 
     def probe_fp_mul_rate(self):
         a, b = ctypes.c_double(), ctypes.c_double()

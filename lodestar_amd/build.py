@@ -13,7 +13,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
 SOURCES = ["lsg_bls.hip"]
-HEADERS = ["lsg_field.hpp", "lsg_curve.hpp", "lsg_h2c.hpp", "lsg_pairing.hpp", "lsg_constants.hpp"]
+HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
+           "lsg_pairing.hpp", "lsg_constants.hpp"]
 
 
 def hipcc():

@@ -8,20 +8,24 @@
 //   packages/beacon-node/src/chain/bls/utils.ts:5-26               (pubkey aggregation)
 //   + the un-vendored @chainsafe/blst@0.2.8 arithmetic underneath.
 //
-// Device pipeline for one work package (all sets of all jobs at once, thread per item):
-//   k_sig_decode      96/192-byte signature -> affine G2 (flags, x<p, sqrt, sign)     [M2]
-//   k_sig_subgroup    psi(P) == [x]P                                                 [M2]
-//   k_pk_decode       48/96-byte pubkey -> affine G1 (on-curve only, worker.ts:110)   [H8]
-//   k_pk_agg_scale    sum of a set's pubkeys, times the set's 64-bit randomizer r_i  [M1,M4]
-//   k_hash_to_g2      H(m_i)                                                         [M3]
-//   k_sig_scale       [r_i] sig_i                                                    [M4]
-//   k_miller_sets     f_i = ML([r_i]PK_i, H(m_i))                                    [M5]
-// then per group (an RLC batch = one chunk of batchable jobs, or one job):
-//   k_group_sum       S_g = sum_{i in g} [r_i] sig_i
+// Execution model: every field element is limb-parallel over a 16-lane DPP row
+// (lsg_fp_lane.hpp), so one work item (a set, a pubkey, a group) is one row and a wave64
+// carries four items.  Per work package:
+//   k_expand_msg      expand_message_xmd (SHA-256), one thread per set          [M3]
+//   k_sig_decode      96/192-byte signature -> affine G2                         [M2]
+//   k_sig_subgroup    psi(P) == [x]P                                             [M2]
+//   k_pk_decode       48/96-byte pubkey -> projective G1 (on-curve only)         [H8]
+//   tree(G1 add)      per-set pubkey aggregation, pairwise over levels           [M1]
+//   k_pk_scale        P_i = [r_i] agg_i (affine)                                 [M4]
+//   k_hash_map        SSWU x2 -> 3-isogeny -> add -> clear_cofactor -> affine     [M3]
+//   k_sig_scale       [r_i] sig_i                                                [M4]
+//   k_miller_sets     f_i = ML(P_i, H(m_i))                                      [M5]
+// then per group (an RLC batch = a chunk of batchable jobs, or one job):
+//   tree(G2 add)      S_g = sum [r_i] sig_i
 //   k_miller_groups   f_g = ML(-G1, S_g)
-//   k_group_fe        FE(f_g * prod_{i in g} f_i) == 1                                [M6]
-// Per-set values stay resident between the batch attempt and the per-job retry, so a
-// failed batch costs only the group sums, one extra Miller loop and one FE per job.
+//   tree(Fp12 mul)    F_g = f_g prod f_i
+//   k_final_exp_check FE(F_g) == 1                                               [M6]
+// Per-set values stay resident between the batch attempt and the per-job retry.
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -35,77 +39,95 @@
 #include <vector>
 
 #include "../../include/lodestar_bls.h"
+#include "lsg_fp_lane.hpp"
 #include "lsg_h2c.hpp"
 #include "lsg_pairing.hpp"
 
-#define LSG_TPB 64
+#define LSG_TPB 256          // threads per block (16 lane-items)
+#define LSG_ITEMS_PER_BLOCK 16
 
-static __device__ __forceinline__ int gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
+static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
+#define LANE_ITEM(n)                        \
+  const size_t item = gtid() >> 4;          \
+  if (item >= (size_t)(n)) return;          \
+  const bool lead = (threadIdx.x & 15) == 0
 
 // ---------------------------------------------------------------------------- kernels
+// expand_message_xmd(msg_i, DST, 256): one thread per set (byte-serial SHA-256)
+__global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restrict__ msg,
+                                                    const uint32_t* __restrict__ msg_off,
+                                                    const uint32_t* __restrict__ msg_len,
+                                                    const uint8_t* __restrict__ dst, uint32_t dst_len,
+                                                    uint8_t* __restrict__ ub) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  uint8_t out[256];
+  expand_message_xmd_256(out, msg + msg_off[i], msg_len[i], dst, dst_len);
+  uint32_t* o = (uint32_t*)(ub + 256 * i);
+  for (int k = 0; k < 64; k++) {
+    uint32_t w;
+    __builtin_memcpy(&w, out + 4 * k, 4);
+    o[k] = w;
+  }
+}
+
 __global__ void __launch_bounds__(LSG_TPB) k_sig_decode(int n, const uint8_t* __restrict__ sig,
-                                                         const uint32_t* __restrict__ sig_len, g2a_t* __restrict__ out,
-                                                         uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
-  int i = gtid();
-  if (i >= n) return;
-  uint32_t len = sig_len[i];
+                                                         const uint32_t* __restrict__ sig_len,
+                                                         uint32_t* __restrict__ sig_aff, uint8_t* __restrict__ inf,
+                                                         int32_t* __restrict__ err) {
+  LANE_ITEM(n);
+  uint32_t len = sig_len[item];
   g2a_t p;
   p.x = fp2_zero();
   p.y = fp2_zero();
   bool is_inf = false;
   int e;
   if (len == 96)
-    e = g2_uncompress(p, is_inf, sig + 192 * (size_t)i);
+    e = g2_uncompress(p, is_inf, sig + 192 * item);
   else if (len == 192)
-    e = g2_deserialize_uncompressed(p, is_inf, sig + 192 * (size_t)i);
+    e = g2_deserialize_uncompressed(p, is_inf, sig + 192 * item);
   else
     e = LSG_BLST_INVALID_SIZE;
-  out[i] = p;
-  inf[i] = is_inf ? 1 : 0;
-  err[i] = e;
-}
-
-__global__ void __launch_bounds__(LSG_TPB) k_sig_subgroup(int n, const g2a_t* __restrict__ sig,
-                                                           const uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
-  int i = gtid();
-  if (i >= n) return;
-  if (err[i] != 0 || inf[i]) return;
-  if (!g2_in_group(proj_from_aff(sig[i]))) err[i] = LSG_BLST_POINT_NOT_IN_GROUP;
-}
-
-__global__ void __launch_bounds__(LSG_TPB) k_pk_decode(int n, const uint8_t* __restrict__ pk,
-                                                        const uint32_t* __restrict__ pk_len, g1a_t* __restrict__ out,
-                                                        uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
-  int i = gtid();
-  if (i >= n) return;
-  uint32_t len = pk_len[i];
-  g1a_t p;
-  p.x = fp_zero();
-  p.y = fp_zero();
-  bool is_inf = false;
-  int e = (len == 48 || len == 96) ? g1_deserialize(p, is_inf, pk + 96 * (size_t)i, (int)len) : LSG_BLST_INVALID_SIZE;
-  out[i] = p;
-  inf[i] = is_inf ? 1 : 0;
-  err[i] = e;
-}
-
-// P_i = [r_i] * sum(pks of set i) in affine; pinf[i] = aggregate is infinity.
-// r_i == 0 means "no scaling" (used by lsg_aggregate_pubkeys).
-__global__ void __launch_bounds__(LSG_TPB) k_pk_agg_scale(int n, const uint32_t* __restrict__ pk_off,
-                                                           const uint32_t* __restrict__ pk_cnt,
-                                                           const g1a_t* __restrict__ pk, const uint8_t* __restrict__ pk_inf,
-                                                           const uint64_t* __restrict__ rnd, g1a_t* __restrict__ out,
-                                                           uint8_t* __restrict__ pinf) {
-  int i = gtid();
-  if (i >= n) return;
-  g1p_t acc = proj_inf<fp_t>();
-  uint32_t o = pk_off[i], c = pk_cnt[i];
-  for (uint32_t k = 0; k < c; k++) {
-    if (!pk_inf[o + k]) acc = g1_add_mixed(acc, pk[o + k]);
+  lane_store(sig_aff, item, p);
+  if (lead) {
+    inf[item] = is_inf ? 1 : 0;
+    err[item] = e;
   }
-  uint64_t r = rnd[i];
-  if (r != 0 && !proj_is_inf(acc)) acc = proj_mul_u64(acc, r);
+}
+
+__global__ void __launch_bounds__(LSG_TPB) k_sig_subgroup(int n, const uint32_t* __restrict__ sig_aff,
+                                                           const uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
+  LANE_ITEM(n);
+  if (err[item] != 0 || inf[item]) return;
+  bool ok = g2_in_group(proj_from_aff(lane_load<g2a_t>(sig_aff, item)));
+  if (lead && !ok) err[item] = LSG_BLST_POINT_NOT_IN_GROUP;
+}
+
+// pubkey -> projective G1 (infinity and undecodable keys become (0:1:0))
+__global__ void __launch_bounds__(LSG_TPB) k_pk_decode(int n, const uint8_t* __restrict__ pk,
+                                                        const uint32_t* __restrict__ pk_len, uint32_t* __restrict__ pkp,
+                                                        int32_t* __restrict__ err) {
+  LANE_ITEM(n);
+  uint32_t len = pk_len[item];
+  g1a_t a;
+  a.x = fp_zero();
+  a.y = fp_zero();
+  bool is_inf = false;
+  int e = (len == 48 || len == 96) ? g1_deserialize(a, is_inf, pk + 96 * item, (int)len) : LSG_BLST_INVALID_SIZE;
+  g1p_t p = (e == 0 && !is_inf) ? proj_from_aff(a) : proj_inf<fp_t>();
+  lane_store(pkp, item, p);
+  if (lead) err[item] = e;
+}
+
+// P_i = [r_i] agg_i in affine (r_i == 0: no scaling); pinf = aggregate is infinity
+__global__ void __launch_bounds__(LSG_TPB) k_pk_scale(int n, const uint32_t* __restrict__ agg,
+                                                       const uint64_t* __restrict__ rnd, uint32_t* __restrict__ P,
+                                                       uint8_t* __restrict__ pinf) {
+  LANE_ITEM(n);
+  g1p_t acc = lane_load<g1p_t>(agg, item);
+  uint64_t r = rnd[item];
   bool is_inf = proj_is_inf(acc);
+  if (r != 0 && !is_inf) acc = proj_mul_u64(acc, r);
   g1a_t a;
   if (is_inf) {
     a.x = fp_zero();
@@ -113,21 +135,16 @@ __global__ void __launch_bounds__(LSG_TPB) k_pk_agg_scale(int n, const uint32_t*
   } else {
     a = proj_to_aff(acc);
   }
-  out[i] = a;
-  pinf[i] = is_inf ? 1 : 0;
+  lane_store(P, item, a);
+  if (lead) pinf[item] = is_inf ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_hash_to_g2(int n, const uint8_t* __restrict__ msg,
-                                                         const uint32_t* __restrict__ msg_off,
-                                                         const uint32_t* __restrict__ msg_len,
-                                                         const uint8_t* __restrict__ dst, uint32_t dst_len,
-                                                         g2a_t* __restrict__ out, uint8_t* __restrict__ hinf) {
-  int i = gtid();
-  if (i >= n) return;
-  uint8_t ub[256];
-  expand_message_xmd_256(ub, msg + msg_off[i], msg_len[i], dst, dst_len);
-  fp2_t u0 = fp2_make(fp_from_be64_mod(ub), fp_from_be64_mod(ub + 64));
-  fp2_t u1 = fp2_make(fp_from_be64_mod(ub + 128), fp_from_be64_mod(ub + 192));
+__global__ void __launch_bounds__(LSG_TPB) k_hash_map(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ H,
+                                                       uint8_t* __restrict__ hinf) {
+  LANE_ITEM(n);
+  const uint8_t* b = ub + 256 * item;
+  fp2_t u0 = fp2_make(fp_from_be64_mod(b), fp_from_be64_mod(b + 64));
+  fp2_t u1 = fp2_make(fp_from_be64_mod(b + 128), fp_from_be64_mod(b + 192));
   g2p_t q = g2_add(iso_map3(map_to_curve_sswu(u0)), iso_map3(map_to_curve_sswu(u1)));
   q = clear_cofactor_g2(q);
   bool is_inf = proj_is_inf(q);
@@ -138,136 +155,188 @@ __global__ void __launch_bounds__(LSG_TPB) k_hash_to_g2(int n, const uint8_t* __
   } else {
     a = proj_to_aff(q);
   }
-  out[i] = a;
-  hinf[i] = is_inf ? 1 : 0;
+  lane_store(H, item, a);
+  if (lead) hinf[item] = is_inf ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const g2a_t* __restrict__ sig,
+__global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const uint32_t* __restrict__ sig_aff,
                                                         const uint8_t* __restrict__ inf, const int32_t* __restrict__ err,
-                                                        const uint64_t* __restrict__ rnd, g2p_t* __restrict__ out) {
-  int i = gtid();
-  if (i >= n) return;
+                                                        const uint64_t* __restrict__ rnd, uint32_t* __restrict__ rs) {
+  LANE_ITEM(n);
   g2p_t r = proj_inf<fp2_t>();
-  if (err[i] == 0 && !inf[i]) r = proj_mul_u64(proj_from_aff(sig[i]), rnd[i]);
-  out[i] = r;
+  if (err[item] == 0 && !inf[item]) r = proj_mul_u64(proj_from_aff(lane_load<g2a_t>(sig_aff, item)), rnd[item]);
+  lane_store(rs, item, r);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_miller_sets(int n, const g1a_t* __restrict__ P,
-                                                          const uint8_t* __restrict__ pinf, const g2a_t* __restrict__ H,
+__global__ void __launch_bounds__(LSG_TPB) k_miller_sets(int n, const uint32_t* __restrict__ P,
+                                                          const uint8_t* __restrict__ pinf, const uint32_t* __restrict__ H,
                                                           const uint8_t* __restrict__ hinf,
-                                                          const int32_t* __restrict__ err, fp12_t* __restrict__ f) {
-  int i = gtid();
-  if (i >= n) return;
+                                                          const int32_t* __restrict__ err, uint32_t* __restrict__ f) {
+  LANE_ITEM(n);
   fp12_t r = fp12_one();
-  if (err[i] == 0 && !pinf[i] && !hinf[i]) r = miller_loop(P[i], H[i]);
-  f[i] = r;
+  if (err[item] == 0 && !pinf[item] && !hinf[item])
+    r = miller_loop(lane_load<g1a_t>(P, item), lane_load<g2a_t>(H, item));
+  lane_store(f, item, r);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_group_sum(int ng, const uint32_t* __restrict__ goff,
-                                                        const uint32_t* __restrict__ members,
-                                                        const g2p_t* __restrict__ rs, g2a_t* __restrict__ S,
-                                                        uint8_t* __restrict__ sinf) {
-  int g = gtid();
-  if (g >= ng) return;
-  g2p_t acc = proj_inf<fp2_t>();
-  for (uint32_t k = goff[g]; k < goff[g + 1]; k++) acc = g2_add(acc, rs[members[k]]);
-  bool is_inf = proj_is_inf(acc);
+// f_g = ML(-G1, S_g) = conj(ML(G1, S_g)) written at slot n_sets + g
+__global__ void __launch_bounds__(LSG_TPB) k_miller_groups(int ng, const uint32_t* __restrict__ S, size_t slot0,
+                                                            uint32_t* __restrict__ f) {
+  LANE_ITEM(ng);
+  g2p_t s = lane_load<g2p_t>(S, item);
+  fp12_t r = fp12_one();
+  if (!proj_is_inf(s)) {
+    g1a_t ng1;
+    ng1.x = fp_t(G1_GEN_X);
+    ng1.y = fp_t(G1_GEN_NEG_Y);
+    r = miller_loop(ng1, proj_to_aff(s));
+  }
+  lane_store(f, slot0 + item, r);
+}
+
+// one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy)
+template <int OP>
+__global__ void __launch_bounds__(LSG_TPB) k_tree_level(int n, const int32_t* __restrict__ ia,
+                                                         const int32_t* __restrict__ ib, const uint32_t* __restrict__ src,
+                                                         uint32_t* __restrict__ dst) {
+  LANE_ITEM(n);
+  int32_t a = ia[item], b = ib[item];
+  if (OP == 0) {
+    g1p_t x = lane_load<g1p_t>(src, a);
+    if (b >= 0) x = g1_add(x, lane_load<g1p_t>(src, b));
+    lane_store(dst, item, x);
+  } else if (OP == 1) {
+    g2p_t x = lane_load<g2p_t>(src, a);
+    if (b >= 0) x = g2_add(x, lane_load<g2p_t>(src, b));
+    lane_store(dst, item, x);
+  } else {
+    fp12_t x = lane_load<fp12_t>(src, a);
+    if (b >= 0) x = fp12_mul(x, lane_load<fp12_t>(src, b));
+    lane_store(dst, item, x);
+  }
+}
+
+__global__ void __launch_bounds__(LSG_TPB) k_final_exp_check(int ng, const uint32_t* __restrict__ F,
+                                                              int32_t* __restrict__ verdict) {
+  LANE_ITEM(ng);
+  bool one = fp12_is_one(final_exp(lane_load<fp12_t>(F, item)));
+  if (lead) verdict[item] = one ? 1 : 0;
+}
+
+LSG_DEVI fp12_t fp12_from_canon_bytes(const uint8_t* b) {
+  fp12_t f;
+  fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int j = 0; j < 6; j++) {
+    c[j]->c0 = fp_to_mont(fp_from_be48(b + 96 * j));
+    c[j]->c1 = fp_to_mont(fp_from_be48(b + 96 * j + 48));
+  }
+  return f;
+}
+
+// partials: canonical big-endian 576-byte Fp12 blobs -> lane form (one item each)
+__global__ void __launch_bounds__(LSG_TPB) k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs,
+                                                            uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  lane_store(out, item, fp12_from_canon_bytes(blobs + 576 * item));
+}
+
+__global__ void __launch_bounds__(LSG_TPB) k_fp12_to_canon(int n, const uint32_t* __restrict__ in,
+                                                            uint8_t* __restrict__ out) {
+  LANE_ITEM(n);
+  const fp12_t f = lane_load<fp12_t>(in, item);
+  const fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  uint8_t* o = out + 576 * item;
+  for (int j = 0; j < 6; j++) {
+    fp_to_be48(o + 96 * j, fp_from_mont(c[j]->c0));
+    fp_to_be48(o + 96 * j + 48, fp_from_mont(c[j]->c1));
+  }
+}
+
+__global__ void __launch_bounds__(LSG_TPB) k_g1p_to_bytes(int n, const uint32_t* __restrict__ pts,
+                                                           uint8_t* __restrict__ out) {
+  LANE_ITEM(n);
+  g1p_t p = lane_load<g1p_t>(pts, item);
+  bool inf = proj_is_inf(p);
+  g1a_t a;
+  if (inf) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  } else {
+    a = proj_to_aff(p);
+  }
+  g1_serialize(out + 96 * item, a, inf);
+}
+
+__global__ void __launch_bounds__(LSG_TPB) k_g2a_to_bytes(int n, const uint32_t* __restrict__ pts,
+                                                           const uint8_t* __restrict__ inf, uint8_t* __restrict__ out) {
+  LANE_ITEM(n);
+  g2_serialize(out + 192 * item, lane_load<g2a_t>(pts, item), inf[item] != 0);
+}
+
+// [k]P for a 256-bit big-endian scalar (test-data utilities only: signing, keygen)
+template <class F>
+__device__ proj_t<F> proj_mul_be256(const proj_t<F>& p, const uint8_t* k) {
+  proj_t<F> acc = proj_inf<F>();
+  for (int byte = 0; byte < 32; byte++) {
+    uint32_t v = k[byte];
+    for (int b = 7; b >= 0; b--) {
+      acc = gdbl(acc);
+      proj_t<F> s = gadd(acc, p);
+      bool bit = (v >> b) & 1u;
+      acc.X = fselect(bit, s.X, acc.X);
+      acc.Y = fselect(bit, s.Y, acc.Y);
+      acc.Z = fselect(bit, s.Z, acc.Z);
+    }
+  }
+  return acc;
+}
+
+// sig_i = [sk_i] H(m_i), ZCash-compressed (bench/test input generation; not on the verify path)
+__global__ void __launch_bounds__(LSG_TPB) k_sign(int n, const uint8_t* __restrict__ sks, const uint32_t* __restrict__ H,
+                                                   uint8_t* __restrict__ out96) {
+  LANE_ITEM(n);
+  g2p_t s = proj_mul_be256(proj_from_aff(lane_load<g2a_t>(H, item)), sks + 32 * item);
+  bool inf = proj_is_inf(s);
   g2a_t a;
-  if (is_inf) {
+  if (inf) {
     a.x = fp2_zero();
     a.y = fp2_zero();
   } else {
-    a = proj_to_aff(acc);
+    a = proj_to_aff(s);
   }
-  S[g] = a;
-  sinf[g] = is_inf ? 1 : 0;
+  g2_compress(out96 + 96 * item, a, inf);
 }
 
-// f_g = ML(-G1, S_g) = conj(ML(G1, S_g))
-__global__ void __launch_bounds__(LSG_TPB) k_miller_groups(int ng, const g2a_t* __restrict__ S,
-                                                            const uint8_t* __restrict__ sinf, fp12_t* __restrict__ f) {
-  int g = gtid();
-  if (g >= ng) return;
-  fp12_t r = fp12_one();
-  if (!sinf[g]) {
-    g1a_t ng1;
-    ng1.x = G1_GEN_X;
-    ng1.y = G1_GEN_NEG_Y;
-    r = miller_loop(ng1, S[g]);
+// pk_i = [sk_i] G1, uncompressed 96 bytes (bench/test input generation)
+__global__ void __launch_bounds__(LSG_TPB) k_sk_to_pk(int n, const uint8_t* __restrict__ sks,
+                                                       uint8_t* __restrict__ out96) {
+  LANE_ITEM(n);
+  g1a_t g;
+  g.x = fp_t(G1_GEN_X);
+  g.y = fp_t(G1_GEN_Y);
+  g1p_t s = proj_mul_be256(proj_from_aff(g), sks + 32 * item);
+  bool inf = proj_is_inf(s);
+  g1a_t a;
+  if (inf) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  } else {
+    a = proj_to_aff(s);
   }
-  f[g] = r;
+  g1_serialize(out96 + 96 * item, a, inf);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_group_product(int ng, const uint32_t* __restrict__ goff,
-                                                            const uint32_t* __restrict__ members,
-                                                            const fp12_t* __restrict__ fset,
-                                                            const fp12_t* __restrict__ fgrp, fp12_t* __restrict__ out) {
-  int g = gtid();
-  if (g >= ng) return;
-  fp12_t acc = fgrp[g];
-  for (uint32_t k = goff[g]; k < goff[g + 1]; k++) acc = fp12_mul(acc, fset[members[k]]);
-  out[g] = acc;
-}
-
-__global__ void __launch_bounds__(LSG_TPB) k_final_exp_check(int ng, const fp12_t* __restrict__ F,
-                                                              int32_t* __restrict__ verdict) {
-  int g = gtid();
-  if (g >= ng) return;
-  verdict[g] = fp12_is_one(final_exp(F[g])) ? 1 : 0;
-}
-
-// partials: canonical big-endian 576-byte Fp12 blobs -> product (Montgomery)
-__global__ void k_partials_product(int n, const uint8_t* __restrict__ blobs, fp12_t* __restrict__ out) {
-  if (gtid() != 0) return;
-  fp12_t acc = fp12_one();
-  for (int k = 0; k < n; k++) {
-    const uint8_t* b = blobs + 576 * (size_t)k;
-    fp12_t f;
-    fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-    for (int j = 0; j < 6; j++) {
-      c[j]->c0 = fp_to_mont(fp_from_be48(b + 96 * j));
-      c[j]->c1 = fp_to_mont(fp_from_be48(b + 96 * j + 48));
-    }
-    acc = fp12_mul(acc, f);
-  }
-  out[0] = acc;
-}
-
-__global__ void k_fp12_to_canon(const fp12_t* __restrict__ in, uint8_t* __restrict__ out) {
-  if (gtid() != 0) return;
-  const fp12_t f = in[0];
-  const fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-  for (int j = 0; j < 6; j++) {
-    fp_to_be48(out + 96 * j, fp_from_mont(c[j]->c0));
-    fp_to_be48(out + 96 * j + 48, fp_from_mont(c[j]->c1));
-  }
-}
-
-__global__ void __launch_bounds__(LSG_TPB) k_g1_to_bytes(int n, const g1a_t* __restrict__ a,
-                                                          const uint8_t* __restrict__ inf, uint8_t* __restrict__ out) {
-  int i = gtid();
-  if (i >= n) return;
-  g1_serialize(out + 96 * (size_t)i, a[i], inf[i] != 0);
-}
-
-__global__ void __launch_bounds__(LSG_TPB) k_g2_to_bytes(int n, const g2a_t* __restrict__ a,
-                                                          const uint8_t* __restrict__ inf, uint8_t* __restrict__ out) {
-  int i = gtid();
-  if (i >= n) return;
-  g2_serialize(out + 192 * (size_t)i, a[i], inf[i] != 0);
-}
-
-// roofline probe: 4 independent Montgomery chains per thread
-__global__ void __launch_bounds__(256) k_probe_fp_mul(int iters, fp_t* __restrict__ io) {
-  int i = gtid();
-  fp_t a = io[i], b = io[i + 1], c = io[i + 2], d = io[i + 3];
+// roofline probe: 4 independent limb-parallel Montgomery chains per row
+__global__ void __launch_bounds__(LSG_TPB) k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
+  LANE_ITEM(n);
+  fp_t a = lane_load<fp_t>(io, item), b = fp_t(FP_R2), c = fp_t(FP_R3), d = fp_t(FP_HALF);
   for (int k = 0; k < iters; k++) {
     a = fp_mul(a, b);
     b = fp_mul(b, c);
     c = fp_mul(c, d);
     d = fp_mul(d, a);
   }
-  io[i] = fp_add(fp_add(a, b), fp_add(c, d));
+  lane_store(io, item, fp_add(fp_add(a, b), fp_add(c, d)));
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -275,6 +344,14 @@ namespace {
 
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
+
+// u32 words per item for each lane-form type
+constexpr size_t W_G1A = lane_words<g1a_t>();
+constexpr size_t W_G1P = lane_words<g1p_t>();
+constexpr size_t W_G2A = lane_words<g2a_t>();
+constexpr size_t W_G2P = lane_words<g2p_t>();
+constexpr size_t W_F12 = lane_words<fp12_t>();
+constexpr size_t W_MAX = W_F12;
 
 uint64_t now_ns() {
   timespec ts;
@@ -306,14 +383,16 @@ struct lsg_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   std::string err;
-  // device buffers (grow-only)
-  DevBuf d_sig, d_siglen, d_msg, d_msgoff, d_msglen, d_pk, d_pklen, d_pkoff, d_pkcnt, d_rnd;
-  DevBuf d_sigaff, d_siginf, d_seterr, d_pkaff, d_pkinf, d_pkerr, d_P, d_pinf, d_H, d_hinf, d_rs, d_fset;
-  DevBuf d_goff, d_members, d_S, d_sinf, d_fgrp, d_F, d_verdict, d_dst, d_blob, d_probe;
-  // timing of the last call
+  // inputs
+  DevBuf d_sig, d_siglen, d_msg, d_msgoff, d_msglen, d_pk, d_pklen, d_rnd, d_dst;
+  // per-set / per-pk state
+  DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_fall;
+  // groups and reductions
+  DevBuf d_idx, d_tA, d_tB, d_S, d_F, d_verdict, d_blob, d_aux;
   std::vector<Timer> timers;
   size_t ntimers = 0;
-  std::vector<std::string> timer_names;
+  size_t n_sets = 0, n_pks = 0;
+  std::vector<uint32_t> pk_off, pk_cnt;  // host copy of the staged set -> pk ranges
 };
 
 namespace {
@@ -323,9 +402,9 @@ int fail(lsg_ctx* c, const char* what, hipError_t e) {
   return LSG_ERR_DEVICE;
 }
 
-#define LSG_HIP(c, call)                              \
-  do {                                                \
-    hipError_t _e = (call);                           \
+#define LSG_HIP(c, call)                               \
+  do {                                                 \
+    hipError_t _e = (call);                            \
     if (_e != hipSuccess) return fail((c), #call, _e); \
   } while (0)
 
@@ -335,7 +414,7 @@ int ensure(lsg_ctx* c, DevBuf& b, size_t bytes) {
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.cap = 0;
-  size_t cap = std::max(bytes, (size_t)4096);
+  size_t cap = std::max(bytes + bytes / 4, (size_t)4096);
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess) return fail(c, "hipMalloc", e);
   b.cap = cap;
@@ -347,7 +426,7 @@ T* P_(DevBuf& b) {
   return (T*)b.p;
 }
 
-int blocks(size_t n) { return (int)((n + LSG_TPB - 1) / LSG_TPB); }
+int lane_blocks(size_t items) { return (int)((items + LSG_ITEMS_PER_BLOCK - 1) / LSG_ITEMS_PER_BLOCK); }
 
 void timer_reset(lsg_ctx* c) { c->ntimers = 0; }
 
@@ -368,33 +447,31 @@ void timer_end(lsg_ctx* c) {
   c->ntimers++;
 }
 
-#define LAUNCH(c, name, grid, ...)                                        \
-  do {                                                                    \
-    timer_begin((c), #name);                                              \
-    hipLaunchKernelGGL(name, dim3(grid), dim3(LSG_TPB), 0, (c)->stream, __VA_ARGS__); \
-    timer_end((c));                                                       \
-    hipError_t _le = hipGetLastError();                                   \
-    if (_le != hipSuccess) return fail((c), #name, _le);                  \
+#define LAUNCH_T(c, name, kern, grid, tpb, ...)                                       \
+  do {                                                                                \
+    timer_begin((c), name);                                                           \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb), 0, (c)->stream, __VA_ARGS__);     \
+    timer_end((c));                                                                   \
+    hipError_t _le = hipGetLastError();                                               \
+    if (_le != hipSuccess) return fail((c), name, _le);                               \
   } while (0)
+#define LAUNCH(c, kern, items, ...) LAUNCH_T(c, #kern, kern, lane_blocks(items), LSG_TPB, __VA_ARGS__)
 
-// Flattened view of a package of sets, staged to the device.
-struct Staged {
-  size_t n_sets = 0, n_pks = 0;
-  std::vector<int32_t> host_err;  // per set (host-side size errors)
-};
-
-int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale, Staged& st) {
-  st.n_sets = n;
+// ---- stage a package of sets into device memory (one synchronous batch of copies)
+int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
   size_t npk = 0, msg_total = 0;
   for (size_t i = 0; i < n; i++) {
     npk += sets[i]->n_pks;
     msg_total += sets[i]->msg_len;
   }
-  st.n_pks = npk;
-  std::vector<uint8_t> sig(192 * std::max(n, (size_t)1), 0), msg(std::max(msg_total, (size_t)1)),
-      pk(96 * std::max(npk, (size_t)1), 0);
-  std::vector<uint32_t> siglen(n), msgoff(n), msglen(n), pklen(std::max(npk, (size_t)1)), pkoff(n), pkcnt(n);
-  std::vector<uint64_t> rnd(n);
+  c->n_sets = n;
+  c->n_pks = npk;
+  size_t nn = std::max(n, (size_t)1), np = std::max(npk, (size_t)1);
+  std::vector<uint8_t> sig(192 * nn, 0), msg(std::max(msg_total, (size_t)1)), pk(96 * np, 0);
+  std::vector<uint32_t> siglen(nn), msgoff(nn), msglen(nn), pklen(np);
+  std::vector<uint64_t> rnd(nn);
+  c->pk_off.assign(n, 0);
+  c->pk_cnt.assign(n, 0);
   size_t mo = 0, po = 0;
   uint64_t s = seed;
   FILE* ur = nullptr;
@@ -407,8 +484,8 @@ int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, 
     msglen[i] = q->msg_len;
     if (q->msg_len) memcpy(&msg[mo], q->msg, q->msg_len);
     mo += q->msg_len;
-    pkoff[i] = (uint32_t)po;
-    pkcnt[i] = q->n_pks;
+    c->pk_off[i] = (uint32_t)po;
+    c->pk_cnt[i] = q->n_pks;
     for (uint32_t k = 0; k < q->n_pks; k++) {
       pklen[po] = q->pk_len;
       if (q->pk_len == 48 || q->pk_len == 96) memcpy(&pk[96 * po], q->pks + (size_t)q->pk_len * k, q->pk_len);
@@ -428,94 +505,176 @@ int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, 
   }
   if (ur) fclose(ur);
   int rc;
-  size_t nn = std::max(n, (size_t)1), np = std::max(npk, (size_t)1);
   if ((rc = ensure(c, c->d_sig, sig.size())) || (rc = ensure(c, c->d_siglen, 4 * nn)) ||
       (rc = ensure(c, c->d_msg, msg.size())) || (rc = ensure(c, c->d_msgoff, 4 * nn)) ||
       (rc = ensure(c, c->d_msglen, 4 * nn)) || (rc = ensure(c, c->d_pk, pk.size())) ||
-      (rc = ensure(c, c->d_pklen, 4 * np)) || (rc = ensure(c, c->d_pkoff, 4 * nn)) ||
-      (rc = ensure(c, c->d_pkcnt, 4 * nn)) || (rc = ensure(c, c->d_rnd, 8 * nn)) ||
-      (rc = ensure(c, c->d_sigaff, sizeof(g2a_t) * nn)) || (rc = ensure(c, c->d_siginf, nn)) ||
-      (rc = ensure(c, c->d_seterr, 4 * nn)) || (rc = ensure(c, c->d_pkaff, sizeof(g1a_t) * np)) ||
-      (rc = ensure(c, c->d_pkinf, np)) || (rc = ensure(c, c->d_pkerr, 4 * np)) ||
-      (rc = ensure(c, c->d_P, sizeof(g1a_t) * nn)) || (rc = ensure(c, c->d_pinf, nn)) ||
-      (rc = ensure(c, c->d_H, sizeof(g2a_t) * nn)) || (rc = ensure(c, c->d_hinf, nn)) ||
-      (rc = ensure(c, c->d_rs, sizeof(g2p_t) * nn)) || (rc = ensure(c, c->d_fset, sizeof(fp12_t) * nn)) ||
-      (rc = ensure(c, c->d_dst, 256)))
+      (rc = ensure(c, c->d_pklen, 4 * np)) || (rc = ensure(c, c->d_rnd, 8 * nn)) || (rc = ensure(c, c->d_dst, 256)) ||
+      (rc = ensure(c, c->d_ub, 256 * nn)) || (rc = ensure(c, c->d_sigaff, 4 * W_G2A * nn)) ||
+      (rc = ensure(c, c->d_siginf, nn)) || (rc = ensure(c, c->d_seterr, 4 * nn)) ||
+      (rc = ensure(c, c->d_pkp, 4 * W_G1P * np)) || (rc = ensure(c, c->d_pkerr, 4 * np)) ||
+      (rc = ensure(c, c->d_agg, 4 * W_G1P * nn)) || (rc = ensure(c, c->d_P, 4 * W_G1A * nn)) ||
+      (rc = ensure(c, c->d_pinf, nn)) || (rc = ensure(c, c->d_H, 4 * W_G2A * nn)) || (rc = ensure(c, c->d_hinf, nn)) ||
+      (rc = ensure(c, c->d_rs, 4 * W_G2P * nn)))
     return rc;
   hipStream_t S = c->stream;
   LSG_HIP(c, hipMemcpyAsync(c->d_sig.p, sig.data(), sig.size(), hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_siglen.p, siglen.data(), 4 * n, hipMemcpyHostToDevice, S));
+  LSG_HIP(c, hipMemcpyAsync(c->d_siglen.p, siglen.data(), 4 * nn, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_msg.p, msg.data(), msg.size(), hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_msgoff.p, msgoff.data(), 4 * n, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_msglen.p, msglen.data(), 4 * n, hipMemcpyHostToDevice, S));
+  LSG_HIP(c, hipMemcpyAsync(c->d_msgoff.p, msgoff.data(), 4 * nn, hipMemcpyHostToDevice, S));
+  LSG_HIP(c, hipMemcpyAsync(c->d_msglen.p, msglen.data(), 4 * nn, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_pk.p, pk.data(), pk.size(), hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_pklen.p, pklen.data(), 4 * np, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_pkoff.p, pkoff.data(), 4 * n, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_pkcnt.p, pkcnt.data(), 4 * n, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_rnd.p, rnd.data(), 8 * n, hipMemcpyHostToDevice, S));
+  LSG_HIP(c, hipMemcpyAsync(c->d_rnd.p, rnd.data(), 8 * nn, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice, S));
-  // host copies must outlive the async copies: synchronize before the vectors die
-  LSG_HIP(c, hipStreamSynchronize(S));
+  LSG_HIP(c, hipStreamSynchronize(S));  // host vectors die at return
+  return LSG_OK;
+}
+
+// Segmented pairwise reduction of lane-form values: for each group, combine the slots
+// groups[g] of `src` (OP 0: G1 add, 1: G2 add, 2: Fp12 mul) into dense out[g].
+// All levels' index pairs are built on the host and uploaded once; each level is one
+// launch over all pairs of all groups (log2(max group size) + 1 launches).
+template <int OP>
+int tree_reduce(lsg_ctx* c, const char* name, const uint32_t* src, const std::vector<std::vector<int32_t>>& groups,
+                uint32_t* out) {
+  size_t ng = groups.size();
+  if (ng == 0) return LSG_OK;
+  size_t W = OP == 0 ? W_G1P : (OP == 1 ? W_G2P : W_F12);
+  std::vector<std::vector<int32_t>> cur = groups;
+  std::vector<int32_t> idx;             // all levels: [ia..., ib...] per level
+  std::vector<std::pair<size_t, size_t>> levels;  // (offset into idx, count)
+  size_t max_level = 0;
+  bool first = true;
+  for (;;) {
+    bool done = true;
+    for (auto& g : cur)
+      if (g.size() > 1) done = false;
+    size_t cnt = 0;
+    std::vector<int32_t> ia, ib;
+    std::vector<std::vector<int32_t>> nxt(ng);
+    if (done) {  // final gather into out[g]
+      for (size_t g = 0; g < ng; g++) {
+        ia.push_back(g < cur.size() && !cur[g].empty() ? cur[g][0] : -1);
+        ib.push_back(-1);
+      }
+      cnt = ng;
+    } else {
+      for (size_t g = 0; g < ng; g++) {
+        for (size_t k = 0; k < cur[g].size(); k += 2) {
+          ia.push_back(cur[g][k]);
+          ib.push_back(k + 1 < cur[g].size() ? cur[g][k + 1] : -1);
+          nxt[g].push_back((int32_t)cnt++);
+        }
+      }
+    }
+    levels.push_back({idx.size(), cnt});
+    idx.insert(idx.end(), ia.begin(), ia.end());
+    idx.insert(idx.end(), ib.begin(), ib.end());
+    max_level = std::max(max_level, cnt);
+    if (done) break;
+    cur.swap(nxt);
+    first = false;
+  }
+  (void)first;
+  int rc;
+  if ((rc = ensure(c, c->d_idx, 4 * idx.size())) || (rc = ensure(c, c->d_tA, 4 * W * max_level)) ||
+      (rc = ensure(c, c->d_tB, 4 * W * max_level)))
+    return rc;
+  LSG_HIP(c, hipMemcpyAsync(c->d_idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, c->stream));
+  const uint32_t* in = src;
+  uint32_t* bufs[2] = {P_<uint32_t>(c->d_tA), P_<uint32_t>(c->d_tB)};
+  for (size_t L = 0; L < levels.size(); L++) {
+    size_t off = levels[L].first, cnt = levels[L].second;
+    bool last = L + 1 == levels.size();
+    uint32_t* dst = last ? out : bufs[L & 1];
+    const int32_t* ia = P_<int32_t>(c->d_idx) + off;
+    LAUNCH_T(c, name, k_tree_level<OP>, lane_blocks(cnt), LSG_TPB, (int)cnt, ia, ia + cnt, in, dst);
+    in = dst;
+  }
+  // keep the host index vector alive until the copy has been consumed
+  LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
 }
 
 // Per-set stages (everything that does not depend on the grouping).
-int run_set_stages(lsg_ctx* c, const Staged& st) {
-  int n = (int)st.n_sets, np = (int)st.n_pks;
+int run_set_stages(lsg_ctx* c) {
+  int n = (int)c->n_sets, np = (int)c->n_pks;
   if (n == 0) return LSG_OK;
-  LAUNCH(c, k_sig_decode, blocks(n), n, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<g2a_t>(c->d_sigaff),
+  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
+           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), DST_POP_LEN, P_<uint8_t>(c->d_ub));
+  LAUNCH(c, k_sig_decode, n, n, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
          P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LAUNCH(c, k_sig_subgroup, blocks(n), n, P_<g2a_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
+  LAUNCH(c, k_sig_subgroup, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
   if (np > 0)
-    LAUNCH(c, k_pk_decode, blocks(np), np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<g1a_t>(c->d_pkaff),
-           P_<uint8_t>(c->d_pkinf), P_<int32_t>(c->d_pkerr));
-  LAUNCH(c, k_pk_agg_scale, blocks(n), n, P_<uint32_t>(c->d_pkoff), P_<uint32_t>(c->d_pkcnt), P_<g1a_t>(c->d_pkaff),
-         P_<uint8_t>(c->d_pkinf), P_<uint64_t>(c->d_rnd), P_<g1a_t>(c->d_P), P_<uint8_t>(c->d_pinf));
-  LAUNCH(c, k_hash_to_g2, blocks(n), n, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff), P_<uint32_t>(c->d_msglen),
-         P_<uint8_t>(c->d_dst), DST_POP_LEN, P_<g2a_t>(c->d_H), P_<uint8_t>(c->d_hinf));
-  LAUNCH(c, k_sig_scale, blocks(n), n, P_<g2a_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr),
-         P_<uint64_t>(c->d_rnd), P_<g2p_t>(c->d_rs));
-  LAUNCH(c, k_miller_sets, blocks(n), n, P_<g1a_t>(c->d_P), P_<uint8_t>(c->d_pinf), P_<g2a_t>(c->d_H),
-         P_<uint8_t>(c->d_hinf), P_<int32_t>(c->d_seterr), P_<fp12_t>(c->d_fset));
+    LAUNCH(c, k_pk_decode, np, np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<uint32_t>(c->d_pkp),
+           P_<int32_t>(c->d_pkerr));
+  std::vector<std::vector<int32_t>> sets_pks(n);
+  for (int i = 0; i < n; i++)
+    for (uint32_t k = 0; k < c->pk_cnt[i]; k++) sets_pks[i].push_back((int32_t)(c->pk_off[i] + k));
+  bool need_agg = np > 0;
+  if (need_agg) {
+    // sets with no keys reduce to nothing: give them the infinity slot of a 1-pk dummy? They are
+    // errors upstream (empty aggregate); map them to pk 0 and let the host treat them as errors.
+    for (int i = 0; i < n; i++)
+      if (sets_pks[i].empty()) sets_pks[i].push_back(0);
+    int rc = tree_reduce<0>(c, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), sets_pks, P_<uint32_t>(c->d_agg));
+    if (rc) return rc;
+  }
+  LAUNCH(c, k_pk_scale, n, n, P_<uint32_t>(c->d_agg), P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_P),
+         P_<uint8_t>(c->d_pinf));
+  LAUNCH(c, k_hash_map, n, n, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
+  LAUNCH(c, k_sig_scale, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr),
+         P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_rs));
   return LSG_OK;
 }
 
-// Evaluate groups of set indices: verdict[g] = FE(ML(-G1, S_g) prod f_i) == 1.
-// If out_F != null the un-exponentiated products are returned instead (no FE).
-int run_groups(lsg_ctx* c, const std::vector<std::vector<uint32_t>>& groups, std::vector<int32_t>& verdict,
-               fp12_t* out_F_host) {
-  int ng = (int)groups.size();
+int run_miller_sets(lsg_ctx* c, size_t slots) {
+  int n = (int)c->n_sets;
+  int rc = ensure(c, c->d_fall, 4 * W_F12 * std::max(slots, (size_t)1));
+  if (rc) return rc;
+  if (n == 0) return LSG_OK;
+  LAUNCH(c, k_miller_sets, n, n, P_<uint32_t>(c->d_P), P_<uint8_t>(c->d_pinf), P_<uint32_t>(c->d_H),
+         P_<uint8_t>(c->d_hinf), P_<int32_t>(c->d_seterr), P_<uint32_t>(c->d_fall));
+  return LSG_OK;
+}
+
+// Evaluate groups of set indices.  verdict[g] = FE(ML(-G1, S_g) prod f_i) == 1, or, with
+// out_blob != null (one group only), the un-exponentiated product in canonical bytes.
+int run_groups(lsg_ctx* c, const std::vector<std::vector<int32_t>>& groups, std::vector<int32_t>& verdict,
+               uint8_t* out_blob) {
+  size_t ng = groups.size();
   verdict.assign(ng, 0);
   if (ng == 0) return LSG_OK;
-  std::vector<uint32_t> goff(ng + 1), members;
-  for (int g = 0; g < ng; g++) {
-    goff[g] = (uint32_t)members.size();
-    members.insert(members.end(), groups[g].begin(), groups[g].end());
-  }
-  goff[ng] = (uint32_t)members.size();
+  size_t n = c->n_sets;
   int rc;
-  if ((rc = ensure(c, c->d_goff, 4 * (ng + 1))) || (rc = ensure(c, c->d_members, 4 * std::max(members.size(), (size_t)1))) ||
-      (rc = ensure(c, c->d_S, sizeof(g2a_t) * ng)) || (rc = ensure(c, c->d_sinf, ng)) ||
-      (rc = ensure(c, c->d_fgrp, sizeof(fp12_t) * ng)) || (rc = ensure(c, c->d_F, sizeof(fp12_t) * ng)) ||
+  // grow the Miller slot array to hold n + ng values, preserving the per-set f_i
+  size_t need = 4 * W_F12 * (n + ng);
+  if (c->d_fall.cap < need) {
+    DevBuf nb;
+    if ((rc = ensure(c, nb, need))) return rc;
+    if (n) LSG_HIP(c, hipMemcpyAsync(nb.p, c->d_fall.p, 4 * W_F12 * n, hipMemcpyDeviceToDevice, c->stream));
+    LSG_HIP(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(c->d_fall.p);
+    c->d_fall = nb;
+  }
+  if ((rc = ensure(c, c->d_S, 4 * W_G2P * ng)) || (rc = ensure(c, c->d_F, 4 * W_F12 * ng)) ||
       (rc = ensure(c, c->d_verdict, 4 * ng)))
     return rc;
-  hipStream_t S = c->stream;
-  LSG_HIP(c, hipMemcpyAsync(c->d_goff.p, goff.data(), 4 * (ng + 1), hipMemcpyHostToDevice, S));
-  if (!members.empty())
-    LSG_HIP(c, hipMemcpyAsync(c->d_members.p, members.data(), 4 * members.size(), hipMemcpyHostToDevice, S));
-  LAUNCH(c, k_group_sum, blocks(ng), ng, P_<uint32_t>(c->d_goff), P_<uint32_t>(c->d_members), P_<g2p_t>(c->d_rs),
-         P_<g2a_t>(c->d_S), P_<uint8_t>(c->d_sinf));
-  LAUNCH(c, k_miller_groups, blocks(ng), ng, P_<g2a_t>(c->d_S), P_<uint8_t>(c->d_sinf), P_<fp12_t>(c->d_fgrp));
-  LAUNCH(c, k_group_product, blocks(ng), ng, P_<uint32_t>(c->d_goff), P_<uint32_t>(c->d_members),
-         P_<fp12_t>(c->d_fset), P_<fp12_t>(c->d_fgrp), P_<fp12_t>(c->d_F));
-  if (out_F_host) {
-    LSG_HIP(c, hipMemcpyAsync(out_F_host, c->d_F.p, sizeof(fp12_t) * ng, hipMemcpyDeviceToHost, S));
-    LSG_HIP(c, hipStreamSynchronize(S));
+  if ((rc = tree_reduce<1>(c, "tree_g2_sigsum", P_<uint32_t>(c->d_rs), groups, P_<uint32_t>(c->d_S)))) return rc;
+  LAUNCH(c, k_miller_groups, ng, (int)ng, P_<uint32_t>(c->d_S), n, P_<uint32_t>(c->d_fall));
+  std::vector<std::vector<int32_t>> fg = groups;
+  for (size_t g = 0; g < ng; g++) fg[g].push_back((int32_t)(n + g));
+  if ((rc = tree_reduce<2>(c, "tree_fp12_product", P_<uint32_t>(c->d_fall), fg, P_<uint32_t>(c->d_F)))) return rc;
+  if (out_blob) {
+    if ((rc = ensure(c, c->d_blob, 576))) return rc;
+    LAUNCH(c, k_fp12_to_canon, 1, 1, P_<uint32_t>(c->d_F), P_<uint8_t>(c->d_blob));
+    LSG_HIP(c, hipMemcpyAsync(out_blob, c->d_blob.p, 576, hipMemcpyDeviceToHost, c->stream));
+    LSG_HIP(c, hipStreamSynchronize(c->stream));
     return LSG_OK;
   }
-  LAUNCH(c, k_final_exp_check, blocks(ng), ng, P_<fp12_t>(c->d_F), P_<int32_t>(c->d_verdict));
-  LSG_HIP(c, hipMemcpyAsync(verdict.data(), c->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
-  LSG_HIP(c, hipStreamSynchronize(S));
+  LAUNCH(c, k_final_exp_check, ng, (int)ng, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
+  LSG_HIP(c, hipMemcpyAsync(verdict.data(), c->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, c->stream));
+  LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
 }
 
@@ -525,8 +684,8 @@ struct SetStatus {
   std::vector<int32_t> pkerr;  // per pubkey
 };
 
-int read_status(lsg_ctx* c, const Staged& st, SetStatus& ss) {
-  size_t n = st.n_sets, np = st.n_pks;
+int read_status(lsg_ctx* c, SetStatus& ss) {
+  size_t n = c->n_sets, np = c->n_pks;
   ss.err.assign(n, 0);
   ss.pinf.assign(n, 0);
   ss.pkerr.assign(np, 0);
@@ -537,6 +696,9 @@ int read_status(lsg_ctx* c, const Staged& st, SetStatus& ss) {
   }
   if (np) LSG_HIP(c, hipMemcpyAsync(ss.pkerr.data(), c->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
   LSG_HIP(c, hipStreamSynchronize(S));
+  // a set without keys is an empty aggregate (PublicKey.aggregate([]) throws)
+  for (size_t i = 0; i < n; i++)
+    if (c->pk_cnt[i] == 0) ss.pinf[i] = 2;
   return LSG_OK;
 }
 
@@ -553,6 +715,12 @@ std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk
   return out;
 }
 
+int32_t set_error(const SetStatus& ss, size_t s) {
+  if (ss.err[s]) return ss.err[s];
+  if (ss.pinf[s] == 2) return LSG_ERR_EMPTY_AGGREGATE;
+  return ss.pinf[s] ? LSG_BLST_PK_IS_INFINITY : 0;
+}
+
 // Error a job's maybeBatch call would throw, in the reference's order:
 // Signature.fromBytes over all sets first (maybeBatch.ts:17-26 map), then
 // mul_n_aggregate rejecting an infinite public key (BLST_PK_IS_INFINITY).
@@ -561,7 +729,7 @@ int32_t job_error(const SetStatus& ss, size_t first, size_t count) {
   for (size_t k = 0; k < count; k++)
     if (ss.err[first + k]) return ss.err[first + k];
   for (size_t k = 0; k < count; k++)
-    if (ss.pinf[first + k]) return LSG_BLST_PK_IS_INFINITY;
+    if (ss.pinf[first + k]) return set_error(ss, first + k);
   return 0;
 }
 
@@ -594,11 +762,11 @@ int lsg_destroy(lsg_ctx* c) {
   if (!c) return LSG_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf* bufs[] = {&c->d_sig,  &c->d_siglen, &c->d_msg,    &c->d_msgoff, &c->d_msglen, &c->d_pk,    &c->d_pklen,
-                    &c->d_pkoff, &c->d_pkcnt, &c->d_rnd,    &c->d_sigaff, &c->d_siginf, &c->d_seterr, &c->d_pkaff,
-                    &c->d_pkinf, &c->d_pkerr, &c->d_P,      &c->d_pinf,   &c->d_H,      &c->d_hinf,  &c->d_rs,
-                    &c->d_fset,  &c->d_goff,  &c->d_members, &c->d_S,     &c->d_sinf,   &c->d_fgrp,  &c->d_F,
-                    &c->d_verdict, &c->d_dst, &c->d_blob,   &c->d_probe};
+  DevBuf* bufs[] = {&c->d_sig,  &c->d_siglen, &c->d_msg, &c->d_msgoff, &c->d_msglen, &c->d_pk,   &c->d_pklen,
+                    &c->d_rnd,  &c->d_dst,    &c->d_ub,  &c->d_sigaff, &c->d_siginf, &c->d_seterr, &c->d_pkp,
+                    &c->d_pkerr, &c->d_agg,   &c->d_P,   &c->d_pinf,   &c->d_H,      &c->d_hinf, &c->d_rs,
+                    &c->d_fall, &c->d_idx,    &c->d_tA,  &c->d_tB,     &c->d_S,      &c->d_F,    &c->d_verdict,
+                    &c->d_blob, &c->d_aux};
   for (DevBuf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (Timer& t : c->timers) {
@@ -629,7 +797,6 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
   memset(&stt, 0, sizeof(stt));
   stt.start_ns = now_ns();
   timer_reset(c);
-  // flatten
   std::vector<const lsg_set*> flat;
   std::vector<size_t> jfirst(n_jobs), jcount(n_jobs);
   for (size_t j = 0; j < n_jobs; j++) {
@@ -637,16 +804,16 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
     jcount[j] = jobs[j].n_sets;
     for (uint32_t k = 0; k < jobs[j].n_sets; k++) flat.push_back(&jobs[j].sets[k]);
   }
-  Staged st;
-  int rc = stage_sets(c, flat.data(), flat.size(), seed, true, st);
+  int rc = stage_sets(c, flat.data(), flat.size(), seed, true);
   if (rc) return rc;
-  if ((rc = run_set_stages(c, st))) return rc;
+  if ((rc = run_set_stages(c))) return rc;
+  if ((rc = run_miller_sets(c, flat.size()))) return rc;
   SetStatus ss;
-  if ((rc = read_status(c, st, ss))) return rc;
+  if ((rc = read_status(c, ss))) return rc;
   // worker.ts:108-114: deserializeSet runs before anything else; a bad pubkey throws
   // out of verifyManySignatureSets and rejects every job of the package.
   int32_t pkfail = 0;
-  for (size_t k = 0; k < st.n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
+  for (size_t k = 0; k < c->n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
   if (pkfail) {
     for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_ERROR, pkfail};
     stt.end_ns = now_ns();
@@ -658,31 +825,28 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
   for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_INVALID, 0};
 
   // Phase A: batchable chunks (worker.ts:51-86) + non-batchable jobs (worker.ts:88-96)
-  std::vector<std::vector<uint32_t>> groups;
-  std::vector<std::vector<size_t>> group_jobs;  // jobs covered by a group
+  std::vector<std::vector<int32_t>> groups;
+  std::vector<std::vector<size_t>> group_jobs;
   std::vector<bool> group_is_chunk;
-  std::vector<size_t> retry;  // jobs to verify individually after a failed chunk
+  std::vector<size_t> retry;
   auto job_group = [&](size_t j) {
-    std::vector<uint32_t> m;
-    for (size_t k = 0; k < jcount[j]; k++) m.push_back((uint32_t)(jfirst[j] + k));
+    std::vector<int32_t> m;
+    for (size_t k = 0; k < jcount[j]; k++) m.push_back((int32_t)(jfirst[j] + k));
     return m;
   };
   if (!batchable.empty()) {
     for (auto ch : chunkify(batchable.size(), 16)) {
-      std::vector<uint32_t> m;
+      std::vector<int32_t> m;
       bool throws = false;
-      size_t nsets = 0;
-      // the flattened chunk's maybeBatch call throws on the first bad set / pk infinity / empty
       for (size_t q = ch.first; q < ch.second; q++) {
         size_t j = batchable[q];
-        nsets += jcount[j];
         for (size_t k = 0; k < jcount[j]; k++) {
           size_t s = jfirst[j] + k;
-          if (ss.err[s] || ss.pinf[s]) throws = true;
-          m.push_back((uint32_t)s);
+          if (set_error(ss, s)) throws = true;
+          m.push_back((int32_t)s);
         }
       }
-      if (nsets == 0) throws = true;
+      if (m.empty()) throws = true;
       std::vector<size_t> js;
       for (size_t q = ch.first; q < ch.second; q++) js.push_back(batchable[q]);
       if (throws) {
@@ -723,9 +887,9 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
       results[group_jobs[g][0]] = {verdict[g] ? LSG_VALID : LSG_INVALID, 0};
     }
   }
-  // Phase B: per-job retry of failed chunks
+  // Phase B: per-job retry of failed chunks (worker.ts:74-96)
   if (!retry.empty()) {
-    std::vector<std::vector<uint32_t>> g2;
+    std::vector<std::vector<int32_t>> g2;
     std::vector<size_t> g2job;
     for (size_t j : retry) {
       int32_t e = job_error(ss, jfirst[j], jcount[j]);
@@ -771,16 +935,16 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
   s.pk_len = pk_len;
   s.n_pks = (uint32_t)n;
   const lsg_set* sp = &s;
-  Staged st;
-  int rc = stage_sets(c, &sp, 1, 0, false, st);
+  int rc = stage_sets(c, &sp, 1, 0, false);
   if (rc) return rc;
   int np = (int)n;
-  LAUNCH(c, k_pk_decode, blocks(np), np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<g1a_t>(c->d_pkaff),
-         P_<uint8_t>(c->d_pkinf), P_<int32_t>(c->d_pkerr));
-  LAUNCH(c, k_pk_agg_scale, 1, 1, P_<uint32_t>(c->d_pkoff), P_<uint32_t>(c->d_pkcnt), P_<g1a_t>(c->d_pkaff),
-         P_<uint8_t>(c->d_pkinf), P_<uint64_t>(c->d_rnd), P_<g1a_t>(c->d_P), P_<uint8_t>(c->d_pinf));
+  LAUNCH(c, k_pk_decode, np, np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<uint32_t>(c->d_pkp),
+         P_<int32_t>(c->d_pkerr));
+  std::vector<std::vector<int32_t>> g(1);
+  for (int k = 0; k < np; k++) g[0].push_back(k);
+  if ((rc = tree_reduce<0>(c, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), g, P_<uint32_t>(c->d_agg)))) return rc;
   if ((rc = ensure(c, c->d_blob, 192))) return rc;
-  LAUNCH(c, k_g1_to_bytes, 1, 1, P_<g1a_t>(c->d_P), P_<uint8_t>(c->d_pinf), P_<uint8_t>(c->d_blob));
+  LAUNCH(c, k_g1p_to_bytes, 1, 1, P_<uint32_t>(c->d_agg), P_<uint8_t>(c->d_blob));
   std::vector<int32_t> pkerr(n);
   LSG_HIP(c, hipMemcpyAsync(pkerr.data(), c->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
   LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96, hipMemcpyDeviceToHost, c->stream));
@@ -795,7 +959,7 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
 
 int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst,
                    uint32_t dst_len, uint8_t* out192) {
-  if (!c || !out192 || (n && msg_len && !msgs) || dst_len > 255 || (dst_len && !dst)) return LSG_ERR_INVALID_ARG;
+  if (!c || (n && msg_len && !msgs) || dst_len > 255 || (dst_len && !dst)) return LSG_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   LSG_HIP(c, hipSetDevice(c->device));
   timer_reset(c);
@@ -808,15 +972,19 @@ int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, 
     sets[i].msg_len = msg_len;
     sp[i] = &sets[i];
   }
-  Staged st;
-  int rc = stage_sets(c, sp.data(), n, 0, false, st);
+  int rc = stage_sets(c, sp.data(), n, 0, false);
   if (rc) return rc;
   LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, c->stream));
   int nn = (int)n;
-  LAUNCH(c, k_hash_to_g2, blocks(nn), nn, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff), P_<uint32_t>(c->d_msglen),
-         P_<uint8_t>(c->d_dst), dst_len, P_<g2a_t>(c->d_H), P_<uint8_t>(c->d_hinf));
+  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (nn + 63) / 64, 64, nn, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
+           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), dst_len, P_<uint8_t>(c->d_ub));
+  LAUNCH(c, k_hash_map, nn, nn, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
+  if (!out192) {  // internal use (lsg_sign): leave H in d_H
+    LSG_HIP(c, hipStreamSynchronize(c->stream));
+    return LSG_OK;
+  }
   if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
-  LAUNCH(c, k_g2_to_bytes, blocks(nn), nn, P_<g2a_t>(c->d_H), P_<uint8_t>(c->d_hinf), P_<uint8_t>(c->d_blob));
+  LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf), P_<uint8_t>(c->d_blob));
   LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->stream));
   LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
@@ -836,54 +1004,91 @@ int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, 
     sets[i].sig_len = sig_len;
     sp[i] = &sets[i];
   }
-  Staged st;
-  int rc = stage_sets(c, sp.data(), n, 0, false, st);
+  int rc = stage_sets(c, sp.data(), n, 0, false);
   if (rc) return rc;
   int nn = (int)n;
-  LAUNCH(c, k_sig_decode, blocks(nn), nn, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<g2a_t>(c->d_sigaff),
+  LAUNCH(c, k_sig_decode, nn, nn, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
          P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LAUNCH(c, k_sig_subgroup, blocks(nn), nn, P_<g2a_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
+  LAUNCH(c, k_sig_subgroup, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
   if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
-  LAUNCH(c, k_g2_to_bytes, blocks(nn), nn, P_<g2a_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<uint8_t>(c->d_blob));
+  LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<uint8_t>(c->d_blob));
   LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->stream));
   LSG_HIP(c, hipMemcpyAsync(err, c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
   LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
 }
 
-int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
-                      int32_t* set_err, int32_t* any_error) {
-  if (!c || !out576 || !any_error || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+int lsg_sign(lsg_ctx* c, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96) {
+  if (!c || !out96 || (n && (!sks32 || !msgs))) return LSG_ERR_INVALID_ARG;
+  int rc = lsg_hash_to_g2(c, msgs, msg_len, n, DST_POP, DST_POP_LEN, nullptr);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
+    return rc;
+  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  int nn = (int)n;
+  LAUNCH(c, k_sign, nn, nn, P_<uint8_t>(c->d_aux), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_blob));
+  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->stream));
+  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  return LSG_OK;
+}
+
+int lsg_sk_to_pk(lsg_ctx* c, const uint8_t* sks32, size_t n, uint8_t* out96) {
+  if (!c || !out96 || (n && !sks32)) return LSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  LSG_HIP(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
+    return rc;
+  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  int nn = (int)n;
+  LAUNCH(c, k_sk_to_pk, nn, nn, P_<uint8_t>(c->d_aux), P_<uint8_t>(c->d_blob));
+  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->stream));
+  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  return LSG_OK;
+}
+
+int lsg_batch_stage(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed) {
+  if (!c || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  LSG_HIP(c, hipSetDevice(c->device));
+  std::vector<const lsg_set*> sp(n_sets);
+  for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
+  return stage_sets(c, sp.data(), n_sets, seed, true);
+}
+
+int lsg_batch_run(lsg_ctx* c, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
+  if (!c || !out576 || !any_error) return LSG_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   LSG_HIP(c, hipSetDevice(c->device));
   timer_reset(c);
-  std::vector<const lsg_set*> sp(n_sets);
-  for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
-  Staged st;
-  int rc = stage_sets(c, sp.data(), n_sets, seed, true, st);
-  if (rc) return rc;
-  if ((rc = run_set_stages(c, st))) return rc;
+  size_t n_sets = c->n_sets;
+  int rc;
+  if ((rc = run_set_stages(c))) return rc;
+  if ((rc = run_miller_sets(c, n_sets + 1))) return rc;
   SetStatus ss;
-  if ((rc = read_status(c, st, ss))) return rc;
+  if ((rc = read_status(c, ss))) return rc;
   *any_error = 0;
+  std::vector<std::vector<int32_t>> groups(1);
   for (size_t i = 0; i < n_sets; i++) {
-    int32_t e = ss.err[i] ? ss.err[i] : (ss.pinf[i] ? LSG_BLST_PK_IS_INFINITY : 0);
+    int32_t e = set_error(ss, i);
     if (set_err) set_err[i] = e;
-    if (e) *any_error = 1;
+    if (e)
+      *any_error = 1;
+    else
+      groups[0].push_back((int32_t)i);
   }
-  for (size_t k = 0; k < st.n_pks; k++)
+  for (size_t k = 0; k < c->n_pks; k++)
     if (ss.pkerr[k]) *any_error = 1;
-  std::vector<std::vector<uint32_t>> groups(1);
-  for (size_t i = 0; i < n_sets; i++)
-    if (!(set_err ? set_err[i] : 0)) groups[0].push_back((uint32_t)i);
   std::vector<int32_t> verdict;
-  fp12_t F;
-  if ((rc = run_groups(c, groups, verdict, &F))) return rc;
-  if ((rc = ensure(c, c->d_blob, 576))) return rc;
-  LAUNCH(c, k_fp12_to_canon, 1, P_<fp12_t>(c->d_F), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out576, c->d_blob.p, 576, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
-  return LSG_OK;
+  return run_groups(c, groups, verdict, out576);
+}
+
+int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
+                      int32_t* set_err, int32_t* any_error) {
+  int rc = lsg_batch_stage(c, sets, n_sets, seed);
+  if (rc) return rc;
+  return lsg_batch_run(c, out576, set_err, any_error);
 }
 
 int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, int32_t* valid) {
@@ -892,12 +1097,20 @@ int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, 
   LSG_HIP(c, hipSetDevice(c->device));
   timer_reset(c);
   int rc;
-  if ((rc = ensure(c, c->d_blob, 576 * std::max(n_partials, (size_t)1))) || (rc = ensure(c, c->d_F, sizeof(fp12_t))) ||
-      (rc = ensure(c, c->d_verdict, 4)))
+  size_t np = std::max(n_partials, (size_t)1);
+  if ((rc = ensure(c, c->d_blob, 576 * np)) || (rc = ensure(c, c->d_aux, 4 * W_F12 * np)) ||
+      (rc = ensure(c, c->d_F, 4 * W_F12)) || (rc = ensure(c, c->d_verdict, 4)))
     return rc;
+  if (n_partials == 0) {
+    *valid = 0;
+    return LSG_OK;
+  }
   LSG_HIP(c, hipMemcpyAsync(c->d_blob.p, partials576, 576 * n_partials, hipMemcpyHostToDevice, c->stream));
-  LAUNCH(c, k_partials_product, 1, (int)n_partials, P_<uint8_t>(c->d_blob), P_<fp12_t>(c->d_F));
-  LAUNCH(c, k_final_exp_check, 1, 1, P_<fp12_t>(c->d_F), P_<int32_t>(c->d_verdict));
+  LAUNCH(c, k_blobs_to_fp12, n_partials, (int)n_partials, P_<uint8_t>(c->d_blob), P_<uint32_t>(c->d_aux));
+  std::vector<std::vector<int32_t>> g(1);
+  for (size_t k = 0; k < n_partials; k++) g[0].push_back((int32_t)k);
+  if ((rc = tree_reduce<2>(c, "tree_fp12_product", P_<uint32_t>(c->d_aux), g, P_<uint32_t>(c->d_F)))) return rc;
+  LAUNCH(c, k_final_exp_check, 1, 1, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
   LSG_HIP(c, hipMemcpyAsync(valid, c->d_verdict.p, 4, hipMemcpyDeviceToHost, c->stream));
   LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
@@ -909,29 +1122,29 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
   LSG_HIP(c, hipSetDevice(c->device));
   hipDeviceProp_t prop;
   LSG_HIP(c, hipGetDeviceProperties(&prop, c->device));
-  int threads = prop.multiProcessorCount * 1024;  // 16 waves per CU
+  int items = prop.multiProcessorCount * 128;  // 32 waves of 4 rows per CU
   int rc;
-  if ((rc = ensure(c, c->d_probe, sizeof(fp_t) * (threads + 4)))) return rc;
-  std::vector<fp_t> init(threads + 4);
-  for (size_t i = 0; i < init.size(); i++) {
-    init[i] = FP_ONE;
-    init[i].l[0] ^= (uint32_t)i;
-  }
-  LSG_HIP(c, hipMemcpy(c->d_probe.p, init.data(), sizeof(fp_t) * init.size(), hipMemcpyHostToDevice));
-  const int iters = 256;
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(threads / 256), dim3(256), 0, c->stream, 8, P_<fp_t>(c->d_probe));
+  if ((rc = ensure(c, c->d_aux, 4 * 16 * (size_t)items))) return rc;
+  std::vector<uint32_t> init(16 * (size_t)items, 0);
+  for (size_t i = 0; i < init.size(); i++)
+    if ((i & 15) < 11) init[i] = (uint32_t)(i * 2654435761u);
+  LSG_HIP(c, hipMemcpy(c->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
+  const int iters = 64;
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->stream, items, 2,
+                     P_<uint32_t>(c->d_aux));
   hipEvent_t a, b;
   LSG_HIP(c, hipEventCreate(&a));
   LSG_HIP(c, hipEventCreate(&b));
   LSG_HIP(c, hipEventRecord(a, c->stream));
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(threads / 256), dim3(256), 0, c->stream, iters, P_<fp_t>(c->d_probe));
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->stream, items, iters,
+                     P_<uint32_t>(c->d_aux));
   LSG_HIP(c, hipEventRecord(b, c->stream));
   LSG_HIP(c, hipEventSynchronize(b));
   float ms = 0;
   LSG_HIP(c, hipEventElapsedTime(&ms, a, b));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
-  double muls = (double)threads * iters * 4.0;
+  double muls = (double)items * iters * 4.0;
   *fp_mul_per_s = muls / (ms * 1e-3);
   *mad_per_s = *fp_mul_per_s * 300.0;
   return LSG_OK;

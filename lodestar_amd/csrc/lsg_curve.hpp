@@ -4,7 +4,7 @@
 // bls/utils.ts:11), Signature.fromBytes(..., validate) (maybeBatch.ts:23,36) and the
 // Pairing.mul_n_aggregate randomizer multiplications.
 #pragma once
-#include "lsg_field.hpp"
+#include "lsg_tower.hpp"
 
 // ---- overload set so one template serves G1 and G2
 LSG_INL fp_t fadd(const fp_t& a, const fp_t& b) { return fp_add(a, b); }
@@ -174,12 +174,12 @@ LSG_INL proj_t<F> proj_dbl(const proj_t<F>& p) {
 }
 
 // Non-inlined wrappers (keep call sites small: one G2 op expands to ~12 Fp2 muls)
-LSG_NOINL g1p_t g1_add(g1p_t p, g1p_t q) { return proj_add(p, q); }
-LSG_NOINL g1p_t g1_add_mixed(g1p_t p, g1a_t q) { return proj_add_mixed(p, q); }
-LSG_NOINL g1p_t g1_dbl(g1p_t p) { return proj_dbl(p); }
-LSG_NOINL g2p_t g2_add(g2p_t p, g2p_t q) { return proj_add(p, q); }
-LSG_NOINL g2p_t g2_add_mixed(g2p_t p, g2a_t q) { return proj_add_mixed(p, q); }
-LSG_NOINL g2p_t g2_dbl(g2p_t p) { return proj_dbl(p); }
+LSG_BIGFN g1p_t g1_add(g1p_t p, g1p_t q) { return proj_add(p, q); }
+LSG_BIGFN g1p_t g1_add_mixed(g1p_t p, g1a_t q) { return proj_add_mixed(p, q); }
+LSG_BIGFN g1p_t g1_dbl(g1p_t p) { return proj_dbl(p); }
+LSG_BIGFN g2p_t g2_add(g2p_t p, g2p_t q) { return proj_add(p, q); }
+LSG_BIGFN g2p_t g2_add_mixed(g2p_t p, g2a_t q) { return proj_add_mixed(p, q); }
+LSG_BIGFN g2p_t g2_dbl(g2p_t p) { return proj_dbl(p); }
 
 LSG_INL g1p_t gadd(const g1p_t& p, const g1p_t& q) { return g1_add(p, q); }
 LSG_INL g2p_t gadd(const g2p_t& p, const g2p_t& q) { return g2_add(p, q); }
@@ -246,7 +246,7 @@ LSG_INL g2p_t g2_psi2(const g2p_t& p) {
 }
 
 // Scott's G2 membership test: psi(P) == [x]P (x < 0)
-LSG_NOINL bool g2_in_group(g2p_t p) {
+LSG_BIGFN bool g2_in_group(g2p_t p) {
   if (proj_is_inf(p)) return true;
   g2p_t xp = proj_neg(proj_mul_xabs(p));
   return proj_eq(g2_psi(p), xp);
@@ -259,35 +259,6 @@ LSG_INL bool g1_on_curve_aff(const g1a_t& a) {
 LSG_INL bool g2_on_curve_aff(const g2a_t& a) {
   fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), FP2_B_G2);
   return fp2_eq(fp2_sqr(a.y), rhs);
-}
-
-// ------------------------------------------------------------------ byte <-> Fp
-// 48 big-endian bytes -> canonical limbs (top 3 flag bits masked off by the caller)
-LSG_INL fp_t fp_from_be48(const uint8_t* b) {
-  fp_t r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    const uint8_t* q = b + 44 - 4 * i;
-    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
-  }
-  return r;
-}
-LSG_INL void fp_to_be48(uint8_t* b, const fp_t& a) {
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint8_t* q = b + 44 - 4 * i;
-    q[0] = (uint8_t)(a.l[i] >> 24);
-    q[1] = (uint8_t)(a.l[i] >> 16);
-    q[2] = (uint8_t)(a.l[i] >> 8);
-    q[3] = (uint8_t)a.l[i];
-  }
-}
-// canonical value < p ?
-LSG_INL bool fp_canon_lt_p(const fp_t& a) {
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], LSG_P[i], br, &br);
-  return br != 0;
 }
 
 // Status codes, numerically equal to blst's BLST_ERROR (+ wrapper's size error); the
@@ -321,7 +292,7 @@ LSG_INL int g2_uncompress(g2a_t& out, bool& inf, const uint8_t* in) {
     return LSG_BLST_BAD_ENCODING;
   }
   fp_t x1 = fp_from_be48(in);
-  x1.l[11] &= 0x1fffffffu;
+  x1 = fp_mask_flags(x1);
   fp_t x0 = fp_from_be48(in + 48);
   if (!fp_canon_lt_p(x1) || !fp_canon_lt_p(x0)) return LSG_BLST_BAD_ENCODING;
   fp2_t x = fp2_make(fp_to_mont(x0), fp_to_mont(x1));
@@ -356,7 +327,7 @@ LSG_INL int g2_deserialize_uncompressed(g2a_t& out, bool& inf, const uint8_t* in
   fp_t v[4];
   for (int k = 0; k < 4; k++) {
     v[k] = fp_from_be48(in + 48 * k);
-    if (k == 0) v[k].l[11] &= 0x1fffffffu;
+    if (k == 0) v[k] = fp_mask_flags(v[k]);
     if (!fp_canon_lt_p(v[k])) return LSG_BLST_BAD_ENCODING;
   }
   out.x = fp2_make(fp_to_mont(v[1]), fp_to_mont(v[0]));
@@ -385,7 +356,7 @@ LSG_INL int g1_deserialize(g1a_t& out, bool& inf, const uint8_t* in, int len) {
   }
   if (!compressed && (in0 & 0x20)) return LSG_BLST_BAD_ENCODING;
   fp_t x = fp_from_be48(in);
-  x.l[11] &= 0x1fffffffu;
+  x = fp_mask_flags(x);
   if (!fp_canon_lt_p(x)) return LSG_BLST_BAD_ENCODING;
   out.x = fp_to_mont(x);
   if (compressed) {
@@ -427,4 +398,16 @@ LSG_INL void g2_serialize(uint8_t* out, const g2a_t& a, bool inf) {
   fp_to_be48(out + 48, fp_from_mont(a.x.c0));
   fp_to_be48(out + 96, fp_from_mont(a.y.c1));
   fp_to_be48(out + 144, fp_from_mont(a.y.c0));
+}
+
+// affine G2 -> 96-byte ZCash-compressed (blst_p2_affine_compress)
+LSG_INL void g2_compress(uint8_t* out, const g2a_t& a, bool inf) {
+  if (inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; i++) out[i] = 0;
+    return;
+  }
+  uint32_t flags = 0x80u | (fp2_lexi_largest(a.y) ? 0x20u : 0u);
+  fp_to_be48(out, fp_or_flags(fp_from_mont(a.x.c1), flags));
+  fp_to_be48(out + 48, fp_from_mont(a.x.c0));
 }

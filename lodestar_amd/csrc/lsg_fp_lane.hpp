@@ -1,0 +1,204 @@
+// Lane backend: limb-parallel 381-bit Montgomery arithmetic for gfx950.
+//
+// One Fp element lives in one 16-lane DPP row: lane j (0..11) holds 32-bit limb j, lanes
+// 12..15 hold 0.  A wave64 therefore carries four independent field elements (four
+// signature sets), so a 4096-set batch occupies 1024 waves -- one per SIMD -- instead of the
+// 64 waves a thread-per-set layout would give, and an Fp12 costs 12 VGPRs instead of 144.
+//
+// Montgomery multiplication is CIOS with the i-loop across time and the j-loop across lanes:
+//   b_i   : DPP row_newbcast:i          m : row_newbcast:0 of (column 0) * n0'
+//   a_j b_i, m p_j : one v_mad_u64_u32 each, per lane
+//   the /2^32 shift of CIOS is a DPP row_shl:1 (lane j <- lane j+1)
+// Carries are deferred in two 32-bit words per lane (ca from the a*b column, cb from the
+// m*p column) so that every v_mad_u64_u32 addend stays < 2^33 and nothing overflows.  The
+// final carry resolve and the conditional subtraction of p use a carry-lookahead on ballot
+// masks: with G = lanes that generate and P = lanes that propagate a carry (disjoint),
+// ((G|P) + G) ^ (G|P) ^ G is the carry INTO every lane, computed on the scalar unit for all
+// four rows of the wave at once (rows cannot interact: lanes 12..15 never generate or
+// propagate).
+#pragma once
+#include "lsg_constants.hpp"
+
+#define LSG_LANE_MODE 1
+// the generic layers built on this backend are device-only code
+#undef LSG_INL
+#define LSG_INL __device__ __forceinline__
+#undef LSG_NOINL
+#define LSG_NOINL __device__ __noinline__
+
+LSG_DEVI uint32_t lane16() { return __lane_id() & 15u; }
+LSG_DEVI uint32_t row_base() { return __lane_id() & 48u; }
+
+struct fp_t {
+  uint32_t v;
+  fp_t() = default;
+  LSG_DEVI fp_t(const fpc_t& c) {
+    uint32_t j = lane16();
+    v = j < 12 ? c.l[j] : 0u;
+  }
+  LSG_DEVI explicit fp_t(uint32_t x) : v(x) {}
+};
+
+// ---- DPP helpers (control codes must be immediates)
+template <int CTRL, bool BC>
+LSG_DEVI uint32_t dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, BC);
+}
+LSG_DEVI uint32_t row_bcast(uint32_t x, int i) {
+  switch (i) {
+    case 0: return dpp<0x150, false>(x);
+    case 1: return dpp<0x151, false>(x);
+    case 2: return dpp<0x152, false>(x);
+    case 3: return dpp<0x153, false>(x);
+    case 4: return dpp<0x154, false>(x);
+    case 5: return dpp<0x155, false>(x);
+    case 6: return dpp<0x156, false>(x);
+    case 7: return dpp<0x157, false>(x);
+    case 8: return dpp<0x158, false>(x);
+    case 9: return dpp<0x159, false>(x);
+    case 10: return dpp<0x15a, false>(x);
+    default: return dpp<0x15b, false>(x);
+  }
+}
+LSG_DEVI uint32_t row_shl1(uint32_t x) { return dpp<0x101, true>(x); }  // lane j <- lane j+1 (15 <- 0)
+LSG_DEVI uint32_t row_shr1(uint32_t x) { return dpp<0x111, true>(x); }  // lane j <- lane j-1 (0 <- 0)
+
+// carry-lookahead over the wave: bit k of the result = carry INTO lane k
+LSG_DEVI uint64_t carry_into(bool g, bool p) {
+  uint64_t G = __ballot(g);
+  uint64_t A = G | __ballot(p);
+  return (A + G) ^ A ^ G;
+}
+LSG_DEVI uint32_t lane_bit(uint64_t m) { return (uint32_t)(m >> __lane_id()) & 1u; }
+LSG_DEVI bool row_bit(uint64_t m, uint32_t k) { return ((m >> (row_base() + k)) & 1u) != 0; }
+LSG_DEVI bool row_none(bool pred) { return ((__ballot(pred) >> row_base()) & 0xffffull) == 0; }
+
+LSG_DEVI uint32_t p_limb() {
+  uint32_t j = lane16();
+  return j < 12 ? LSG_P[j] : 0u;
+}
+
+// z < 2p (normalized limbs) -> z mod p
+LSG_DEVI uint32_t lane_reduce_once(uint32_t z, uint32_t pj) {
+  uint32_t j = lane16();
+  uint64_t B = carry_into(z < pj, z == pj && j < 12);
+  uint32_t d = z - pj - lane_bit(B);
+  uint32_t r = row_bit(B, 12) ? z : d;  // borrow out of limb 11 <=> z < p
+  return j < 12 ? r : 0u;
+}
+
+LSG_DEVNOINL uint32_t lane_mont_mul(uint32_t a, uint32_t b) {
+  const uint32_t pj = p_limb();
+  uint32_t x = 0, ca = 0, cb = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint32_t bi = row_bcast(b, i);
+    uint64_t s = (uint64_t)a * bi + ((uint64_t)x + ca);
+    uint64_t t2 = (uint64_t)(uint32_t)s + cb;
+    uint32_t m = row_bcast((uint32_t)t2, 0) * LSG_N0P;
+    uint64_t u = (uint64_t)m * pj + t2;
+    x = row_shl1((uint32_t)u);
+    ca = (uint32_t)(s >> 32);
+    cb = (uint32_t)(u >> 32);
+  }
+  // resolve the deferred carries: value = sum_j (x_j + ca_j + cb_j) 2^(32 j) < 2p
+  uint64_t y = (uint64_t)x + ca + cb;
+  uint64_t z = (uint64_t)(uint32_t)y + row_shr1((uint32_t)(y >> 32));
+  uint32_t zl = (uint32_t)z;
+  zl += lane_bit(carry_into((z >> 32) != 0, zl == 0xffffffffu));
+  return lane_reduce_once(zl, pj);
+}
+
+LSG_DEVI uint32_t lane_add(uint32_t a, uint32_t b) {
+  uint64_t s = (uint64_t)a + b;
+  uint32_t z = (uint32_t)s;
+  z += lane_bit(carry_into((s >> 32) != 0, z == 0xffffffffu));
+  return lane_reduce_once(z, p_limb());
+}
+
+LSG_DEVI uint32_t lane_sub(uint32_t a, uint32_t b) {
+  uint32_t j = lane16();
+  uint64_t B = carry_into(a < b, a == b && j < 12);
+  uint32_t d = a - b - lane_bit(B);
+  bool neg = row_bit(B, 12);
+  uint64_t s = (uint64_t)d + p_limb();
+  uint32_t e = (uint32_t)s;
+  e += lane_bit(carry_into((s >> 32) != 0, e == 0xffffffffu && j < 12));
+  uint32_t r = neg ? e : d;
+  return j < 12 ? r : 0u;
+}
+
+// ------------------------------------------------------------------ Fp API
+LSG_DEVI fp_t fp_zero() { return fp_t(0u); }
+LSG_DEVI bool fp_is_zero(const fp_t& a) { return row_none(a.v != 0); }
+LSG_DEVI bool fp_eq(const fp_t& a, const fp_t& b) { return row_none(a.v != b.v); }
+LSG_DEVI fp_t fp_select(bool c, const fp_t& a, const fp_t& b) { return fp_t(c ? a.v : b.v); }
+LSG_DEVI fp_t fp_add(const fp_t& a, const fp_t& b) { return fp_t(lane_add(a.v, b.v)); }
+LSG_DEVI fp_t fp_sub(const fp_t& a, const fp_t& b) { return fp_t(lane_sub(a.v, b.v)); }
+LSG_DEVI fp_t fp_neg(const fp_t& a) { return fp_t(lane_sub(0u, a.v)); }
+LSG_DEVI fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_t(lane_mont_mul(a.v, b.v)); }
+
+// ---- canonical predicates and byte I/O (row-uniform results)
+LSG_DEVI bool fp_canon_gt_half(const fp_t& c) {
+  uint32_t j = lane16();
+  uint32_t h = j < 12 ? LSG_HALF_P_CANON[j] : 0u;
+  return row_bit(carry_into(h < c.v, h == c.v && j < 12), 12);  // borrow of HALF - c
+}
+LSG_DEVI bool fp_canon_lt_p(const fp_t& c) {
+  uint32_t j = lane16();
+  uint32_t pj = p_limb();
+  return row_bit(carry_into(c.v < pj, c.v == pj && j < 12), 12);  // borrow of c - p
+}
+LSG_DEVI uint32_t fp_canon_parity(const fp_t& c) { return row_bcast(c.v, 0) & 1u; }
+
+LSG_DEVI fp_t fp_from_be_bytes(const uint8_t* b, int nlimbs) {
+  uint32_t j = lane16();
+  uint32_t v = 0;
+  if ((int)j < nlimbs) {
+    const uint8_t* q = b + 4 * (nlimbs - 1 - (int)j);
+    v = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  return fp_t(v);
+}
+LSG_DEVI void fp_to_be48(uint8_t* b, const fp_t& a) {
+  uint32_t j = lane16();
+  if (j < 12) {
+    uint8_t* q = b + 44 - 4 * j;
+    q[0] = (uint8_t)(a.v >> 24);
+    q[1] = (uint8_t)(a.v >> 16);
+    q[2] = (uint8_t)(a.v >> 8);
+    q[3] = (uint8_t)a.v;
+  }
+}
+LSG_DEVI fp_t fp_mask_flags(const fp_t& a) { return fp_t(lane16() == 11 ? (a.v & 0x1fffffffu) : a.v); }
+// OR ZCash flag bits into the most significant byte (canonical value, for serialization)
+LSG_DEVI fp_t fp_or_flags(const fp_t& a, uint32_t flags) {
+  return fp_t(lane16() == 11 ? (a.v | (flags << 24)) : a.v);
+}
+
+// ---- item-major global storage of lane-form values: a value of type T (a struct of W
+// fp_t) for item i lives at mem[(i*W + k)*16 + lane], k = 0..W-1 (coalesced 64-byte rows).
+template <class T>
+LSG_DEVI T lane_load(const uint32_t* __restrict__ mem, size_t item) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  const uint32_t* p = mem + item * W * 16 + lane16();
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = p[k * 16];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+template <class T>
+LSG_DEVI void lane_store(uint32_t* __restrict__ mem, size_t item, const T& v) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+  uint32_t* p = mem + item * W * 16 + lane16();
+#pragma unroll
+  for (int k = 0; k < W; k++) p[k * 16] = w[k];
+}
+template <class T>
+constexpr size_t lane_words() {
+  return sizeof(T) / 4 * 16;  // u32 words per item in global memory
+}

@@ -20,7 +20,7 @@ LSG_CONST uint32_t SHA_K[64] = {
 
 LSG_INL uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-LSG_NOINL void sha256_compress(uint32_t* st, const uint32_t* blk) {
+LSG_BIGFN void sha256_compress(uint32_t* st, const uint32_t* blk) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) w[i] = blk[i];
@@ -155,22 +155,14 @@ LSG_INL void expand_message_xmd_256(uint8_t* out, const uint8_t* msg, uint32_t m
 //   N = hi * 2^384 + mid * 2^256 + lo,  hi, mid < 2^128, lo < 2^256
 //   mont(N) = mont_mul(lo, R^2) + mont_mul(mid, 2^256 R^2) + mont_mul(hi, R^3)
 LSG_INL fp_t fp_from_be64_mod(const uint8_t* b) {
-  fp_t lo = fp_zero(), mid = fp_zero(), hi = fp_zero();
-  for (int i = 0; i < 8; i++) {
-    const uint8_t* q = b + 60 - 4 * i;
-    lo.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
-  }
-  for (int i = 0; i < 4; i++) {
-    const uint8_t* q = b + 28 - 4 * i;
-    mid.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
-    const uint8_t* r = b + 12 - 4 * i;
-    hi.l[i] = ((uint32_t)r[0] << 24) | ((uint32_t)r[1] << 16) | ((uint32_t)r[2] << 8) | (uint32_t)r[3];
-  }
-  return fp_add(fp_add(fp_mul(lo, FP_R2), fp_mul(mid, FP_R2_SHL256)), fp_mul(hi, FP_R3));
+  fp_t lo = fp_from_be_bytes(b + 32, 8);
+  fp_t mid = fp_from_be_bytes(b + 16, 4);
+  fp_t hi = fp_from_be_bytes(b, 4);
+  return fp_add(fp_add(fp_mul(lo, fp_t(FP_R2)), fp_mul(mid, fp_t(FP_R2_SHL256))), fp_mul(hi, fp_t(FP_R3)));
 }
 
 // ------------------------------------------------------------------ SSWU on E2' (RFC 9380 6.6.2)
-LSG_NOINL g2a_t map_to_curve_sswu(fp2_t u) {
+LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) {
   fp2_t u2 = fp2_sqr(u);
   fp2_t zu2 = fp2_mul(SSWU_Z, u2);
   fp2_t tv1 = fp2_add(fp2_sqr(zu2), zu2);
@@ -195,7 +187,7 @@ LSG_NOINL g2a_t map_to_curve_sswu(fp2_t u) {
 }
 
 // 3-isogeny E2' -> E2, projective output (X, Y, Z) = (xn yd, y yn xd, xd yd)
-LSG_NOINL g2p_t iso_map3(g2a_t p) {
+LSG_BIGFN g2p_t iso_map3(g2a_t p) {
   const fp2_t& x = p.x;
   fp2_t xn = fp2_add(fp2_mul(fp2_add(fp2_mul(fp2_add(fp2_mul(ISO_XNUM_3, x), ISO_XNUM_2), x), ISO_XNUM_1), x),
                      ISO_XNUM_0);
@@ -212,7 +204,7 @@ LSG_NOINL g2p_t iso_map3(g2a_t p) {
 }
 
 // h_eff * P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)   (RFC 9380 appendix G.3)
-LSG_NOINL g2p_t clear_cofactor_g2(g2p_t p) {
+LSG_BIGFN g2p_t clear_cofactor_g2(g2p_t p) {
   g2p_t t1 = proj_neg(proj_mul_xabs(p));  // [x]P
   g2p_t t2 = g2_psi(p);
   g2p_t t3 = g2_psi2(g2_dbl(p));

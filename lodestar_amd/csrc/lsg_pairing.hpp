@@ -13,7 +13,7 @@ struct line_t {
 };
 
 // T <- 2T; line = (3b'Z^2 - Y^2, 3X^2 xP, -2YZ yP)
-LSG_NOINL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
+LSG_BIGFN line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
   fp2_t t0 = fp2_sqr(T.Y);
   fp2_t t1 = fp2_mul(T.Y, T.Z);
   fp2_t t2 = fp2_mul_b3(fp2_sqr(T.Z));
@@ -44,7 +44,7 @@ LSG_NOINL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
 }
 
 // T <- T + Q; theta = Y - yQ Z, delta = X - xQ Z; line = (delta yQ - theta xQ, theta xP, -delta yP)
-LSG_NOINL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
+LSG_BIGFN line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
   fp2_t theta = fp2_sub(T.Y, fp2_mul(Q.y, T.Z));
   fp2_t delta = fp2_sub(T.X, fp2_mul(Q.x, T.Z));
   line_t L;
@@ -67,7 +67,7 @@ LSG_NOINL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
 }
 
 // f_{|x|,Q}(P) conjugated (x < 0).  P affine G1, Q affine G2, both finite.
-LSG_NOINL fp12_t miller_loop(g1a_t P, g2a_t Q) {
+LSG_BIGFN fp12_t miller_loop(g1a_t P, g2a_t Q) {
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
   g2p_t T = proj_from_aff(Q);
   line_t L = ml_dbl_step(T, P.x, P.y);
@@ -90,7 +90,7 @@ LSG_NOINL fp12_t miller_loop(g1a_t P, g2a_t Q) {
 }
 
 // g^x for g in the cyclotomic subgroup
-LSG_NOINL fp12_t fp12_exp_by_x(fp12_t g) {
+LSG_BIGFN fp12_t fp12_exp_by_x(fp12_t g) {
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
   fp12_t r = g;
   for (int b = 62; b >= 0; b--) {
@@ -101,7 +101,7 @@ LSG_NOINL fp12_t fp12_exp_by_x(fp12_t g) {
 }
 
 // f^(3 (p^12 - 1)/r)   -- oracle/pairing.py:final_exp_fast
-LSG_NOINL fp12_t final_exp(fp12_t f) {
+LSG_BIGFN fp12_t final_exp(fp12_t f) {
   fp12_t f1 = fp12_mul(fp12_conj(f), fp12_inv(f));
   fp12_t g = fp12_mul(fp12_frob2(f1), f1);
   fp12_t t0 = fp12_mul(fp12_exp_by_x(g), fp12_conj(g));

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#define LSG_COUNT_MULS 1
+#include "lsg_fp_elem.hpp"
 #include "lsg_h2c.hpp"
 #include "lsg_pairing.hpp"
 
@@ -28,6 +30,8 @@ static fp12_t rd12(const uint8_t* b) {
   for (int i = 0; i < 6; i++) *c[i] = rd2(b + 96 * i);
   return f;
 }
+
+unsigned long long lsg_mul_count = 0;
 
 extern "C" {
 
@@ -116,5 +120,51 @@ void hc_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
   g1_deserialize(p, inf, p96, 96);
   g2_deserialize_uncompressed(q, inf, q192);
   wr12(out576, miller_loop(p, q));
+}
+
+// Fp-multiplication counts of each device stage for one representative set (bench/opcount.json).
+// counts[]: sig_decode, sig_subgroup, pk_decode, pk_scale, hash_map, sig_scale, miller,
+//           g2_add, fp12_mul, final_exp, g1_add
+void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32, uint64_t r, unsigned long long* counts) {
+  g2a_t s;
+  g1a_t pk;
+  bool inf;
+  lsg_mul_count = 0;
+  g2_uncompress(s, inf, sig96);
+  counts[0] = lsg_mul_count;
+  lsg_mul_count = 0;
+  (void)g2_in_group(proj_from_aff(s));
+  counts[1] = lsg_mul_count;
+  lsg_mul_count = 0;
+  g1_deserialize(pk, inf, pk96, 96);
+  counts[2] = lsg_mul_count;
+  lsg_mul_count = 0;
+  g1a_t P = proj_to_aff(proj_mul_u64(proj_from_aff(pk), r));
+  counts[3] = lsg_mul_count;
+  uint8_t ub[256];
+  expand_message_xmd_256(ub, msg32, 32, (const uint8_t*)"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_", 43);
+  lsg_mul_count = 0;
+  fp2_t u0 = fp2_make(fp_from_be64_mod(ub), fp_from_be64_mod(ub + 64));
+  fp2_t u1 = fp2_make(fp_from_be64_mod(ub + 128), fp_from_be64_mod(ub + 192));
+  g2a_t H = proj_to_aff(clear_cofactor_g2(g2_add(iso_map3(map_to_curve_sswu(u0)), iso_map3(map_to_curve_sswu(u1)))));
+  counts[4] = lsg_mul_count;
+  lsg_mul_count = 0;
+  g2p_t rs = proj_mul_u64(proj_from_aff(s), r);
+  counts[5] = lsg_mul_count;
+  lsg_mul_count = 0;
+  fp12_t f = miller_loop(P, H);
+  counts[6] = lsg_mul_count;
+  lsg_mul_count = 0;
+  (void)g2_add(rs, rs);
+  counts[7] = lsg_mul_count;
+  lsg_mul_count = 0;
+  (void)fp12_mul(f, f);
+  counts[8] = lsg_mul_count;
+  lsg_mul_count = 0;
+  (void)final_exp(f);
+  counts[9] = lsg_mul_count;
+  lsg_mul_count = 0;
+  (void)g1_add(proj_from_aff(pk), proj_from_aff(pk));
+  counts[10] = lsg_mul_count;
 }
 }

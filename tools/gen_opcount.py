@@ -1,0 +1,44 @@
+"""Freezes bench/opcount.json: exact Fp-multiplication counts of every device stage, measured
+by running the generic math headers (the code the GPU kernels instantiate) through the
+instrumented host build tests/native/hostcheck.hip on one representative set.  One Fp
+multiplication = 300 32x32->64 multiply-accumulates (2*12^2 + 12, CIOS), SURVEY.md 8(d)."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from tests import blsdata as bd  # noqa: E402
+
+NAMES = ["sig_decode", "sig_subgroup", "pk_decode", "pk_scale", "hash_map", "sig_scale", "miller",
+         "g2_add", "fp12_mul", "final_exp", "g1_add"]
+
+
+def main():
+    lib = ctypes.CDLL(os.path.join(ROOT, "tests", "native", "libhostcheck.so"))
+    lib.hc_opcount.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64,
+                               ctypes.POINTER(ctypes.c_ulonglong)]
+    pks, m, sig = bd.single_set(1, tag="opcount")
+    counts = (ctypes.c_ulonglong * len(NAMES))()
+    lib.hc_opcount(sig, pks[0], m, 0xF00DCAFE12345678, counts)
+    c = {n: int(counts[i]) for i, n in enumerate(NAMES)}
+    per_set = (c["sig_decode"] + c["sig_subgroup"] + c["pk_decode"] + c["pk_scale"] + c["hash_map"] + c["sig_scale"]
+               + c["miller"] + c["g2_add"] + c["fp12_mul"])
+    per_batch = c["miller"] + c["fp12_mul"] + c["final_exp"]  # group sig term + product + FE
+    out = {
+        "unit": "Fp multiplications (381-bit Montgomery); 1 = 300 v_mad_u64_u32",
+        "mads_per_fp_mul": 300,
+        "stage_fp_muls": c,
+        "batched_single_set_fp_muls": per_set,
+        "per_batch_fp_muls": per_batch,
+        "aggregate_extra_per_pubkey_fp_muls": c["g1_add"],
+        "survey_estimate_blst_equivalent": {"batched_single_set": 16000, "per_batch": 15000, "per_pubkey": 11},
+        "source": "tools/gen_opcount.py over tests/native/hostcheck.hip (LSG_COUNT_MULS)",
+    }
+    json.dump(out, open(os.path.join(ROOT, "bench", "opcount.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
