@@ -48,6 +48,7 @@
 
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 #define LANE_ITEM(n)                        \
+  lsg_lane_setup();                         \
   const size_t item = gtid() >> 4;          \
   if (item >= (size_t)(n)) return;          \
   const bool lead = (threadIdx.x & 15) == 0
@@ -378,9 +379,19 @@ struct Timer {
 
 }  // namespace
 
+struct TreeSlot {
+  DevBuf idx, tA, tB;
+  std::vector<int32_t> host;  // index pairs of the last reduction (alive until the call syncs)
+};
+
+// Three streams: S0 = hash_to_G2 -> Miller loops -> products -> FE, S1 = pubkeys,
+// S2 = signatures (decode, subgroup, RLC scaling, sums, sig Miller loop).  Stage order is
+// encoded with events; one synchronisation per phase.
 struct lsg_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t st[3] = {nullptr, nullptr, nullptr};
+  int cur = 0;
+  hipEvent_t ev_pk = nullptr, ev_sig = nullptr, ev_grp = nullptr;
   std::mutex mu;
   std::string err;
   // inputs
@@ -388,11 +399,13 @@ struct lsg_ctx {
   // per-set / per-pk state
   DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_fall;
   // groups and reductions
-  DevBuf d_idx, d_tA, d_tB, d_S, d_F, d_verdict, d_blob, d_aux;
+  DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
+  TreeSlot tree[3];
   std::vector<Timer> timers;
   size_t ntimers = 0;
   size_t n_sets = 0, n_pks = 0;
   std::vector<uint32_t> pk_off, pk_cnt;  // host copy of the staged set -> pk ranges
+  std::vector<std::vector<int32_t>> sets_pks;
 };
 
 namespace {
@@ -428,7 +441,12 @@ T* P_(DevBuf& b) {
 
 int lane_blocks(size_t items) { return (int)((items + LSG_ITEMS_PER_BLOCK - 1) / LSG_ITEMS_PER_BLOCK); }
 
-void timer_reset(lsg_ctx* c) { c->ntimers = 0; }
+inline hipStream_t S_(lsg_ctx* c) { return c->st[c->cur]; }
+
+void timer_reset(lsg_ctx* c) {
+  c->ntimers = 0;
+  c->cur = 0;
+}
 
 void timer_begin(lsg_ctx* c, const char* name) {
   if (c->ntimers >= c->timers.size()) {
@@ -439,23 +457,28 @@ void timer_begin(lsg_ctx* c, const char* name) {
   }
   Timer& t = c->timers[c->ntimers];
   t.name = name;
-  (void)hipEventRecord(t.a, c->stream);
+  (void)hipEventRecord(t.a, S_(c));
 }
 
 void timer_end(lsg_ctx* c) {
-  (void)hipEventRecord(c->timers[c->ntimers].b, c->stream);
+  (void)hipEventRecord(c->timers[c->ntimers].b, S_(c));
   c->ntimers++;
 }
 
 #define LAUNCH_T(c, name, kern, grid, tpb, ...)                                       \
   do {                                                                                \
     timer_begin((c), name);                                                           \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb), 0, (c)->stream, __VA_ARGS__);     \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb), 0, S_(c), __VA_ARGS__);           \
     timer_end((c));                                                                   \
     hipError_t _le = hipGetLastError();                                               \
     if (_le != hipSuccess) return fail((c), name, _le);                               \
   } while (0)
 #define LAUNCH(c, kern, items, ...) LAUNCH_T(c, #kern, kern, lane_blocks(items), LSG_TPB, __VA_ARGS__)
+
+int sync_all(lsg_ctx* c) {
+  for (int k = 0; k < 3; k++) LSG_HIP(c, hipStreamSynchronize(c->st[k]));
+  return LSG_OK;
+}
 
 // ---- stage a package of sets into device memory (one synchronous batch of copies)
 int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
@@ -504,6 +527,13 @@ int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, 
     rnd[i] = r;
   }
   if (ur) fclose(ur);
+  // per-set pubkey index lists for the aggregation tree (a set without keys points at
+  // pk 0 and is reported as an empty aggregate by read_status)
+  c->sets_pks.assign(n, {});
+  for (size_t i = 0; i < n; i++) {
+    for (uint32_t k = 0; k < c->pk_cnt[i]; k++) c->sets_pks[i].push_back((int32_t)(c->pk_off[i] + k));
+    if (c->sets_pks[i].empty()) c->sets_pks[i].push_back(0);
+  }
   int rc;
   if ((rc = ensure(c, c->d_sig, sig.size())) || (rc = ensure(c, c->d_siglen, 4 * nn)) ||
       (rc = ensure(c, c->d_msg, msg.size())) || (rc = ensure(c, c->d_msgoff, 4 * nn)) ||
@@ -516,7 +546,7 @@ int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, 
       (rc = ensure(c, c->d_pinf, nn)) || (rc = ensure(c, c->d_H, 4 * W_G2A * nn)) || (rc = ensure(c, c->d_hinf, nn)) ||
       (rc = ensure(c, c->d_rs, 4 * W_G2P * nn)))
     return rc;
-  hipStream_t S = c->stream;
+  hipStream_t S = c->st[0];
   LSG_HIP(c, hipMemcpyAsync(c->d_sig.p, sig.data(), sig.size(), hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_siglen.p, siglen.data(), 4 * nn, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_msg.p, msg.data(), msg.size(), hipMemcpyHostToDevice, S));
@@ -526,25 +556,27 @@ int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, 
   LSG_HIP(c, hipMemcpyAsync(c->d_pklen.p, pklen.data(), 4 * np, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_rnd.p, rnd.data(), 8 * nn, hipMemcpyHostToDevice, S));
   LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipStreamSynchronize(S));  // host vectors die at return
+  LSG_HIP(c, hipStreamSynchronize(S));  // host vectors die at return; other streams see the data
   return LSG_OK;
 }
 
-// Segmented pairwise reduction of lane-form values: for each group, combine the slots
-// groups[g] of `src` (OP 0: G1 add, 1: G2 add, 2: Fp12 mul) into dense out[g].
-// All levels' index pairs are built on the host and uploaded once; each level is one
-// launch over all pairs of all groups (log2(max group size) + 1 launches).
+// Segmented pairwise reduction of lane-form values on the current stream: for each group,
+// combine the slots groups[g] of `src` (OP 0: G1 add, 1: G2 add, 2: Fp12 mul) into dense
+// out[g].  All levels' index pairs are built on the host and uploaded once; each level is
+// one launch over all pairs of all groups.  `slot` selects private scratch so that trees on
+// different streams can run concurrently.
 template <int OP>
-int tree_reduce(lsg_ctx* c, const char* name, const uint32_t* src, const std::vector<std::vector<int32_t>>& groups,
-                uint32_t* out) {
+int tree_reduce(lsg_ctx* c, int slot, const char* name, const uint32_t* src,
+                const std::vector<std::vector<int32_t>>& groups, uint32_t* out) {
   size_t ng = groups.size();
   if (ng == 0) return LSG_OK;
+  TreeSlot& T = c->tree[slot];
   size_t W = OP == 0 ? W_G1P : (OP == 1 ? W_G2P : W_F12);
   std::vector<std::vector<int32_t>> cur = groups;
-  std::vector<int32_t> idx;             // all levels: [ia..., ib...] per level
+  std::vector<int32_t>& idx = T.host;
+  idx.clear();
   std::vector<std::pair<size_t, size_t>> levels;  // (offset into idx, count)
   size_t max_level = 0;
-  bool first = true;
   for (;;) {
     bool done = true;
     for (auto& g : cur)
@@ -554,7 +586,7 @@ int tree_reduce(lsg_ctx* c, const char* name, const uint32_t* src, const std::ve
     std::vector<std::vector<int32_t>> nxt(ng);
     if (done) {  // final gather into out[g]
       for (size_t g = 0; g < ng; g++) {
-        ia.push_back(g < cur.size() && !cur[g].empty() ? cur[g][0] : -1);
+        ia.push_back(!cur[g].empty() ? cur[g][0] : -1);
         ib.push_back(-1);
       }
       cnt = ng;
@@ -573,132 +605,128 @@ int tree_reduce(lsg_ctx* c, const char* name, const uint32_t* src, const std::ve
     max_level = std::max(max_level, cnt);
     if (done) break;
     cur.swap(nxt);
-    first = false;
   }
-  (void)first;
   int rc;
-  if ((rc = ensure(c, c->d_idx, 4 * idx.size())) || (rc = ensure(c, c->d_tA, 4 * W * max_level)) ||
-      (rc = ensure(c, c->d_tB, 4 * W * max_level)))
+  if ((rc = ensure(c, T.idx, 4 * idx.size())) || (rc = ensure(c, T.tA, 4 * W * max_level)) ||
+      (rc = ensure(c, T.tB, 4 * W * max_level)))
     return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, c->stream));
+  LSG_HIP(c, hipMemcpyAsync(T.idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, S_(c)));
   const uint32_t* in = src;
-  uint32_t* bufs[2] = {P_<uint32_t>(c->d_tA), P_<uint32_t>(c->d_tB)};
+  uint32_t* bufs[2] = {P_<uint32_t>(T.tA), P_<uint32_t>(T.tB)};
   for (size_t L = 0; L < levels.size(); L++) {
     size_t off = levels[L].first, cnt = levels[L].second;
     bool last = L + 1 == levels.size();
     uint32_t* dst = last ? out : bufs[L & 1];
-    const int32_t* ia = P_<int32_t>(c->d_idx) + off;
+    const int32_t* ia = P_<int32_t>(T.idx) + off;
     LAUNCH_T(c, name, k_tree_level<OP>, lane_blocks(cnt), LSG_TPB, (int)cnt, ia, ia + cnt, in, dst);
     in = dst;
   }
-  // keep the host index vector alive until the copy has been consumed
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
   return LSG_OK;
 }
 
-// Per-set stages (everything that does not depend on the grouping).
-int run_set_stages(lsg_ctx* c) {
+// Per-set stages on three streams (no host synchronisation):
+//   S1: pubkeys -> aggregation tree -> [r_i] scaling            (event ev_pk)
+//   S2: signature decode -> subgroup check (event ev_sig) -> [r_i] scaling
+//   S0: expand_message -> hash_to_G2 -> wait ev_pk -> Miller loops f_i
+// f_i is written to d_fall[0..n); the caller sized d_fall for n + groups slots.
+int launch_set_stages(lsg_ctx* c) {
   int n = (int)c->n_sets, np = (int)c->n_pks;
   if (n == 0) return LSG_OK;
-  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
-           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), DST_POP_LEN, P_<uint8_t>(c->d_ub));
-  LAUNCH(c, k_sig_decode, n, n, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
-         P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LAUNCH(c, k_sig_subgroup, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  if (np > 0)
+  // S1: pubkeys
+  c->cur = 1;
+  if (np > 0) {
     LAUNCH(c, k_pk_decode, np, np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<uint32_t>(c->d_pkp),
            P_<int32_t>(c->d_pkerr));
-  std::vector<std::vector<int32_t>> sets_pks(n);
-  for (int i = 0; i < n; i++)
-    for (uint32_t k = 0; k < c->pk_cnt[i]; k++) sets_pks[i].push_back((int32_t)(c->pk_off[i] + k));
-  bool need_agg = np > 0;
-  if (need_agg) {
-    // sets with no keys reduce to nothing: give them the infinity slot of a 1-pk dummy? They are
-    // errors upstream (empty aggregate); map them to pk 0 and let the host treat them as errors.
-    for (int i = 0; i < n; i++)
-      if (sets_pks[i].empty()) sets_pks[i].push_back(0);
-    int rc = tree_reduce<0>(c, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), sets_pks, P_<uint32_t>(c->d_agg));
+    int rc = tree_reduce<0>(c, 1, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), c->sets_pks, P_<uint32_t>(c->d_agg));
     if (rc) return rc;
   }
   LAUNCH(c, k_pk_scale, n, n, P_<uint32_t>(c->d_agg), P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_P),
          P_<uint8_t>(c->d_pinf));
-  LAUNCH(c, k_hash_map, n, n, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
+  LSG_HIP(c, hipEventRecord(c->ev_pk, c->st[1]));
+  // S2: signatures
+  c->cur = 2;
+  LAUNCH(c, k_sig_decode, n, n, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
+         P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
+  LAUNCH(c, k_sig_subgroup, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
+  LSG_HIP(c, hipEventRecord(c->ev_sig, c->st[2]));  // signature errors known
   LAUNCH(c, k_sig_scale, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr),
          P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_rs));
-  return LSG_OK;
-}
-
-int run_miller_sets(lsg_ctx* c, size_t slots) {
-  int n = (int)c->n_sets;
-  int rc = ensure(c, c->d_fall, 4 * W_F12 * std::max(slots, (size_t)1));
-  if (rc) return rc;
-  if (n == 0) return LSG_OK;
+  // S0: messages, then the per-set Miller loops once pubkeys are scaled and signature
+  // errors are known (k_miller_sets reads d_seterr)
+  c->cur = 0;
+  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
+           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), DST_POP_LEN, P_<uint8_t>(c->d_ub));
+  LAUNCH(c, k_hash_map, n, n, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
+  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_pk, 0));
+  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_sig, 0));
   LAUNCH(c, k_miller_sets, n, n, P_<uint32_t>(c->d_P), P_<uint8_t>(c->d_pinf), P_<uint32_t>(c->d_H),
          P_<uint8_t>(c->d_hinf), P_<int32_t>(c->d_seterr), P_<uint32_t>(c->d_fall));
   return LSG_OK;
 }
 
-// Evaluate groups of set indices.  verdict[g] = FE(ML(-G1, S_g) prod f_i) == 1, or, with
-// out_blob != null (one group only), the un-exponentiated product in canonical bytes.
-int run_groups(lsg_ctx* c, const std::vector<std::vector<int32_t>>& groups, std::vector<int32_t>& verdict,
-               uint8_t* out_blob) {
+int size_miller_slots(lsg_ctx* c, size_t groups) {
+  return ensure(c, c->d_fall, 4 * W_F12 * std::max(c->n_sets + groups, (size_t)1));
+}
+
+// Group stages (no host synchronisation): S2 sums [r_i] sig_i per group and runs the
+// signature Miller loop; S0 multiplies each group's f_i with it and, if fe, runs the final
+// exponentiation into d_verdict (else leaves the products in d_F).  Sets with errors
+// contribute identities (f_i = 1, [r_i] sig_i = O), so groups may include them.
+int launch_groups(lsg_ctx* c, const std::vector<std::vector<int32_t>>& groups, bool fe) {
   size_t ng = groups.size();
-  verdict.assign(ng, 0);
   if (ng == 0) return LSG_OK;
   size_t n = c->n_sets;
   int rc;
-  // grow the Miller slot array to hold n + ng values, preserving the per-set f_i
-  size_t need = 4 * W_F12 * (n + ng);
-  if (c->d_fall.cap < need) {
-    DevBuf nb;
-    if ((rc = ensure(c, nb, need))) return rc;
-    if (n) LSG_HIP(c, hipMemcpyAsync(nb.p, c->d_fall.p, 4 * W_F12 * n, hipMemcpyDeviceToDevice, c->stream));
-    LSG_HIP(c, hipStreamSynchronize(c->stream));
-    (void)hipFree(c->d_fall.p);
-    c->d_fall = nb;
+  if (c->d_fall.cap < 4 * W_F12 * (n + ng)) {
+    c->err = "internal: Miller slot array too small";
+    return LSG_ERR_INVALID_ARG;
   }
   if ((rc = ensure(c, c->d_S, 4 * W_G2P * ng)) || (rc = ensure(c, c->d_F, 4 * W_F12 * ng)) ||
       (rc = ensure(c, c->d_verdict, 4 * ng)))
     return rc;
-  if ((rc = tree_reduce<1>(c, "tree_g2_sigsum", P_<uint32_t>(c->d_rs), groups, P_<uint32_t>(c->d_S)))) return rc;
+  c->cur = 2;
+  if ((rc = tree_reduce<1>(c, 2, "tree_g2_sigsum", P_<uint32_t>(c->d_rs), groups, P_<uint32_t>(c->d_S)))) return rc;
   LAUNCH(c, k_miller_groups, ng, (int)ng, P_<uint32_t>(c->d_S), n, P_<uint32_t>(c->d_fall));
+  LSG_HIP(c, hipEventRecord(c->ev_grp, c->st[2]));
+  c->cur = 0;
+  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_grp, 0));
   std::vector<std::vector<int32_t>> fg = groups;
   for (size_t g = 0; g < ng; g++) fg[g].push_back((int32_t)(n + g));
-  if ((rc = tree_reduce<2>(c, "tree_fp12_product", P_<uint32_t>(c->d_fall), fg, P_<uint32_t>(c->d_F)))) return rc;
-  if (out_blob) {
-    if ((rc = ensure(c, c->d_blob, 576))) return rc;
-    LAUNCH(c, k_fp12_to_canon, 1, 1, P_<uint32_t>(c->d_F), P_<uint8_t>(c->d_blob));
-    LSG_HIP(c, hipMemcpyAsync(out_blob, c->d_blob.p, 576, hipMemcpyDeviceToHost, c->stream));
-    LSG_HIP(c, hipStreamSynchronize(c->stream));
-    return LSG_OK;
-  }
-  LAUNCH(c, k_final_exp_check, ng, (int)ng, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
-  LSG_HIP(c, hipMemcpyAsync(verdict.data(), c->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  if ((rc = tree_reduce<2>(c, 0, "tree_fp12_product", P_<uint32_t>(c->d_fall), fg, P_<uint32_t>(c->d_F)))) return rc;
+  if (fe) LAUNCH(c, k_final_exp_check, ng, (int)ng, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
   return LSG_OK;
 }
 
 struct SetStatus {
   std::vector<int32_t> err;    // per set: BLST code (0 ok)
-  std::vector<uint8_t> pinf;   // per set: aggregated pk is infinity
+  std::vector<uint8_t> pinf;   // per set: aggregated pk is infinity (2: no keys at all)
   std::vector<int32_t> pkerr;  // per pubkey
 };
 
-int read_status(lsg_ctx* c, SetStatus& ss) {
+// Copies per-set status (and optionally ng verdicts) to the host on S0 and waits for all
+// streams; S0 has already waited on S1/S2 through events.
+int finish(lsg_ctx* c, SetStatus* ss, std::vector<int32_t>* verdict, size_t ng) {
   size_t n = c->n_sets, np = c->n_pks;
-  ss.err.assign(n, 0);
-  ss.pinf.assign(n, 0);
-  ss.pkerr.assign(np, 0);
-  hipStream_t S = c->stream;
-  if (n) {
-    LSG_HIP(c, hipMemcpyAsync(ss.err.data(), c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, S));
-    LSG_HIP(c, hipMemcpyAsync(ss.pinf.data(), c->d_pinf.p, n, hipMemcpyDeviceToHost, S));
+  hipStream_t S = c->st[0];
+  if (ss) {
+    ss->err.assign(n, 0);
+    ss->pinf.assign(n, 0);
+    ss->pkerr.assign(np, 0);
+    if (n) {
+      LSG_HIP(c, hipMemcpyAsync(ss->err.data(), c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, S));
+      LSG_HIP(c, hipMemcpyAsync(ss->pinf.data(), c->d_pinf.p, n, hipMemcpyDeviceToHost, S));
+    }
+    if (np) LSG_HIP(c, hipMemcpyAsync(ss->pkerr.data(), c->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
   }
-  if (np) LSG_HIP(c, hipMemcpyAsync(ss.pkerr.data(), c->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
-  LSG_HIP(c, hipStreamSynchronize(S));
-  // a set without keys is an empty aggregate (PublicKey.aggregate([]) throws)
-  for (size_t i = 0; i < n; i++)
-    if (c->pk_cnt[i] == 0) ss.pinf[i] = 2;
+  if (verdict) {
+    verdict->assign(ng, 0);
+    if (ng) LSG_HIP(c, hipMemcpyAsync(verdict->data(), c->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
+  }
+  int rc = sync_all(c);
+  if (rc) return rc;
+  if (ss)
+    for (size_t i = 0; i < n; i++)
+      if (c->pk_cnt[i] == 0) ss->pinf[i] = 2;  // PublicKey.aggregate([]) throws
   return LSG_OK;
 }
 
@@ -750,8 +778,13 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LSG_ERR_NO_DEVICE;
   lsg_ctx* c = new lsg_ctx();
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  bool ok = hipSetDevice(dev) == hipSuccess;
+  for (int k = 0; k < 3 && ok; k++) ok = hipStreamCreateWithFlags(&c->st[k], hipStreamNonBlocking) == hipSuccess;
+  hipEvent_t* evs[] = {&c->ev_pk, &c->ev_sig, &c->ev_grp};
+  for (hipEvent_t* e : evs)
+    if (ok) ok = hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    lsg_destroy(c);
     return LSG_ERR_DEVICE;
   }
   *out = c;
@@ -761,19 +794,29 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
 int lsg_destroy(lsg_ctx* c) {
   if (!c) return LSG_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
-  DevBuf* bufs[] = {&c->d_sig,  &c->d_siglen, &c->d_msg, &c->d_msgoff, &c->d_msglen, &c->d_pk,   &c->d_pklen,
-                    &c->d_rnd,  &c->d_dst,    &c->d_ub,  &c->d_sigaff, &c->d_siginf, &c->d_seterr, &c->d_pkp,
-                    &c->d_pkerr, &c->d_agg,   &c->d_P,   &c->d_pinf,   &c->d_H,      &c->d_hinf, &c->d_rs,
-                    &c->d_fall, &c->d_idx,    &c->d_tA,  &c->d_tB,     &c->d_S,      &c->d_F,    &c->d_verdict,
-                    &c->d_blob, &c->d_aux};
+  for (int k = 0; k < 3; k++)
+    if (c->st[k]) (void)hipStreamSynchronize(c->st[k]);
+  DevBuf* bufs[] = {&c->d_sig,   &c->d_siglen, &c->d_msg,    &c->d_msgoff, &c->d_msglen, &c->d_pk,
+                    &c->d_pklen, &c->d_rnd,    &c->d_dst,    &c->d_ub,     &c->d_sigaff, &c->d_siginf,
+                    &c->d_seterr, &c->d_pkp,   &c->d_pkerr,  &c->d_agg,    &c->d_P,      &c->d_pinf,
+                    &c->d_H,     &c->d_hinf,   &c->d_rs,     &c->d_fall,   &c->d_S,      &c->d_F,
+                    &c->d_verdict, &c->d_blob, &c->d_aux};
   for (DevBuf* b : bufs)
     if (b->p) (void)hipFree(b->p);
+  for (TreeSlot& t : c->tree) {
+    DevBuf* tb[] = {&t.idx, &t.tA, &t.tB};
+    for (DevBuf* b : tb)
+      if (b->p) (void)hipFree(b->p);
+  }
   for (Timer& t : c->timers) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
-  (void)hipStreamDestroy(c->stream);
+  hipEvent_t evs[] = {c->ev_pk, c->ev_sig, c->ev_grp};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < 3; k++)
+    if (c->st[k]) (void)hipStreamDestroy(c->st[k]);
   delete c;
   return LSG_OK;
 }
@@ -788,6 +831,11 @@ int lsg_device_name(lsg_ctx* c, char* buf, size_t len) {
   return LSG_OK;
 }
 
+// Phase A is launched speculatively: every batchable chunk and every non-batchable job gets
+// its group (sum of [r_i] sig_i, Miller product, final exponentiation) before the per-set
+// status is known, so the whole package costs one host synchronisation.  Sets that fail
+// to decode contribute identities; the host then discards the verdicts of groups that the
+// reference would have thrown on (worker.ts:51-96) and re-runs those jobs one by one.
 int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_job_result* results,
                     lsg_stats* stats) {
   if (!c || (n_jobs && (!jobs || !results))) return LSG_ERR_INVALID_ARG;
@@ -804,12 +852,56 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
     jcount[j] = jobs[j].n_sets;
     for (uint32_t k = 0; k < jobs[j].n_sets; k++) flat.push_back(&jobs[j].sets[k]);
   }
+  for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_INVALID, 0};
+  std::vector<size_t> batchable, nonbatch;
+  for (size_t j = 0; j < n_jobs; j++) (jobs[j].flags & LSG_JOB_BATCHABLE ? batchable : nonbatch).push_back(j);
+  auto job_group = [&](size_t j) {
+    std::vector<int32_t> m;
+    for (size_t k = 0; k < jcount[j]; k++) m.push_back((int32_t)(jfirst[j] + k));
+    return m;
+  };
+  // Phase A groups: batchable chunks (worker.ts:51-86) + non-batchable jobs (worker.ts:88-96)
+  std::vector<std::vector<int32_t>> groups;
+  std::vector<std::vector<size_t>> group_jobs;
+  std::vector<bool> group_is_chunk;
+  std::vector<std::vector<size_t>> empty_chunks;  // chunks without sets: always throw
+  if (!batchable.empty()) {
+    for (auto ch : chunkify(batchable.size(), 16)) {
+      std::vector<int32_t> m;
+      std::vector<size_t> js;
+      for (size_t q = ch.first; q < ch.second; q++) {
+        size_t j = batchable[q];
+        js.push_back(j);
+        std::vector<int32_t> jm = job_group(j);
+        m.insert(m.end(), jm.begin(), jm.end());
+      }
+      if (m.empty()) {
+        empty_chunks.push_back(js);
+        continue;
+      }
+      groups.push_back(m);
+      group_jobs.push_back(js);
+      group_is_chunk.push_back(true);
+    }
+  }
+  for (size_t j : nonbatch) {
+    if (jcount[j] == 0) {
+      results[j] = {LSG_ERROR, LSG_ERR_EMPTY_SET};
+      continue;
+    }
+    groups.push_back(job_group(j));
+    group_jobs.push_back({j});
+    group_is_chunk.push_back(false);
+  }
   int rc = stage_sets(c, flat.data(), flat.size(), seed, true);
   if (rc) return rc;
-  if ((rc = run_set_stages(c))) return rc;
-  if ((rc = run_miller_sets(c, flat.size()))) return rc;
+  if ((rc = size_miller_slots(c, std::max(groups.size(), n_jobs)))) return rc;
+  if ((rc = launch_set_stages(c))) return rc;
+  if ((rc = launch_groups(c, groups, true))) return rc;
   SetStatus ss;
-  if ((rc = read_status(c, ss))) return rc;
+  std::vector<int32_t> verdict;
+  if ((rc = finish(c, &ss, &verdict, groups.size()))) return rc;
+  stt.n_final_exps += (uint32_t)groups.size();
   // worker.ts:108-114: deserializeSet runs before anything else; a bad pubkey throws
   // out of verifyManySignatureSets and rejects every job of the package.
   int32_t pkfail = 0;
@@ -820,61 +912,17 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
     if (stats) *stats = stt;
     return LSG_OK;
   }
-  std::vector<size_t> batchable, nonbatch;
-  for (size_t j = 0; j < n_jobs; j++) (jobs[j].flags & LSG_JOB_BATCHABLE ? batchable : nonbatch).push_back(j);
-  for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_INVALID, 0};
-
-  // Phase A: batchable chunks (worker.ts:51-86) + non-batchable jobs (worker.ts:88-96)
-  std::vector<std::vector<int32_t>> groups;
-  std::vector<std::vector<size_t>> group_jobs;
-  std::vector<bool> group_is_chunk;
   std::vector<size_t> retry;
-  auto job_group = [&](size_t j) {
-    std::vector<int32_t> m;
-    for (size_t k = 0; k < jcount[j]; k++) m.push_back((int32_t)(jfirst[j] + k));
-    return m;
-  };
-  if (!batchable.empty()) {
-    for (auto ch : chunkify(batchable.size(), 16)) {
-      std::vector<int32_t> m;
-      bool throws = false;
-      for (size_t q = ch.first; q < ch.second; q++) {
-        size_t j = batchable[q];
-        for (size_t k = 0; k < jcount[j]; k++) {
-          size_t s = jfirst[j] + k;
-          if (set_error(ss, s)) throws = true;
-          m.push_back((int32_t)s);
-        }
-      }
-      if (m.empty()) throws = true;
-      std::vector<size_t> js;
-      for (size_t q = ch.first; q < ch.second; q++) js.push_back(batchable[q]);
-      if (throws) {
-        stt.batch_retries++;
-        retry.insert(retry.end(), js.begin(), js.end());
-      } else {
-        groups.push_back(m);
-        group_jobs.push_back(js);
-        group_is_chunk.push_back(true);
-      }
-    }
+  for (auto& js : empty_chunks) {
+    stt.batch_retries++;
+    retry.insert(retry.end(), js.begin(), js.end());
   }
-  for (size_t j : nonbatch) {
-    int32_t e = job_error(ss, jfirst[j], jcount[j]);
-    if (e) {
-      results[j] = {LSG_ERROR, e};
-    } else {
-      groups.push_back(job_group(j));
-      group_jobs.push_back({j});
-      group_is_chunk.push_back(false);
-    }
-  }
-  std::vector<int32_t> verdict;
-  if ((rc = run_groups(c, groups, verdict, nullptr))) return rc;
-  stt.n_final_exps += (uint32_t)groups.size();
   for (size_t g = 0; g < groups.size(); g++) {
     if (group_is_chunk[g]) {
-      if (verdict[g]) {
+      bool throws = false;
+      for (int32_t s : groups[g])
+        if (set_error(ss, (size_t)s)) throws = true;
+      if (!throws && verdict[g]) {
         for (size_t j : group_jobs[g]) {
           results[j] = {LSG_VALID, 0};
           stt.batch_sigs_success += (uint32_t)jcount[j];
@@ -884,7 +932,9 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
         retry.insert(retry.end(), group_jobs[g].begin(), group_jobs[g].end());
       }
     } else {
-      results[group_jobs[g][0]] = {verdict[g] ? LSG_VALID : LSG_INVALID, 0};
+      size_t j = group_jobs[g][0];
+      int32_t e = job_error(ss, jfirst[j], jcount[j]);
+      results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{verdict[g] ? LSG_VALID : LSG_INVALID, 0};
     }
   }
   // Phase B: per-job retry of failed chunks (worker.ts:74-96)
@@ -900,7 +950,8 @@ int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
         g2job.push_back(j);
       }
     }
-    if ((rc = run_groups(c, g2, verdict, nullptr))) return rc;
+    if ((rc = launch_groups(c, g2, true))) return rc;
+    if ((rc = finish(c, nullptr, &verdict, g2.size()))) return rc;
     stt.n_final_exps += (uint32_t)g2.size();
     for (size_t g = 0; g < g2.size(); g++) results[g2job[g]] = {verdict[g] ? LSG_VALID : LSG_INVALID, 0};
   }
@@ -942,13 +993,13 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
          P_<int32_t>(c->d_pkerr));
   std::vector<std::vector<int32_t>> g(1);
   for (int k = 0; k < np; k++) g[0].push_back(k);
-  if ((rc = tree_reduce<0>(c, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), g, P_<uint32_t>(c->d_agg)))) return rc;
+  if ((rc = tree_reduce<0>(c, 1, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), g, P_<uint32_t>(c->d_agg)))) return rc;
   if ((rc = ensure(c, c->d_blob, 192))) return rc;
   LAUNCH(c, k_g1p_to_bytes, 1, 1, P_<uint32_t>(c->d_agg), P_<uint8_t>(c->d_blob));
   std::vector<int32_t> pkerr(n);
-  LSG_HIP(c, hipMemcpyAsync(pkerr.data(), c->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(pkerr.data(), c->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   for (size_t k = 0; k < n; k++)
     if (pkerr[k]) {
       *err_code = pkerr[k];
@@ -974,19 +1025,19 @@ int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, 
   }
   int rc = stage_sets(c, sp.data(), n, 0, false);
   if (rc) return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, c->stream));
+  LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, c->st[0]));
   int nn = (int)n;
   LAUNCH_T(c, "k_expand_msg", k_expand_msg, (nn + 63) / 64, 64, nn, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
            P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), dst_len, P_<uint8_t>(c->d_ub));
   LAUNCH(c, k_hash_map, nn, nn, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
   if (!out192) {  // internal use (lsg_sign): leave H in d_H
-    LSG_HIP(c, hipStreamSynchronize(c->stream));
+    LSG_HIP(c, hipStreamSynchronize(c->st[0]));
     return LSG_OK;
   }
   if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
   LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   return LSG_OK;
 }
 
@@ -1012,9 +1063,9 @@ int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, 
   LAUNCH(c, k_sig_subgroup, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
   if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
   LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipMemcpyAsync(err, c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipMemcpyAsync(err, c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   return LSG_OK;
 }
 
@@ -1025,11 +1076,11 @@ int lsg_sign(lsg_ctx* c, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
     return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->st[0]));
   int nn = (int)n;
   LAUNCH(c, k_sign, nn, nn, P_<uint8_t>(c->d_aux), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   return LSG_OK;
 }
 
@@ -1040,11 +1091,11 @@ int lsg_sk_to_pk(lsg_ctx* c, const uint8_t* sks32, size_t n, uint8_t* out96) {
   int rc;
   if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
     return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->st[0]));
   int nn = (int)n;
   LAUNCH(c, k_sk_to_pk, nn, nn, P_<uint8_t>(c->d_aux), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   return LSG_OK;
 }
 
@@ -1064,24 +1115,27 @@ int lsg_batch_run(lsg_ctx* c, uint8_t* out576, int32_t* set_err, int32_t* any_er
   timer_reset(c);
   size_t n_sets = c->n_sets;
   int rc;
-  if ((rc = run_set_stages(c))) return rc;
-  if ((rc = run_miller_sets(c, n_sets + 1))) return rc;
-  SetStatus ss;
-  if ((rc = read_status(c, ss))) return rc;
-  *any_error = 0;
   std::vector<std::vector<int32_t>> groups(1);
+  for (size_t i = 0; i < n_sets; i++) groups[0].push_back((int32_t)i);
+  if ((rc = size_miller_slots(c, 1))) return rc;
+  if ((rc = ensure(c, c->d_blob, 576))) return rc;
+  if ((rc = launch_set_stages(c))) return rc;
+  // errored sets contribute identities, so the partial covers exactly the valid sets (an
+  // empty package gives the identity)
+  if ((rc = launch_groups(c, groups, false))) return rc;
+  LAUNCH(c, k_fp12_to_canon, 1, 1, P_<uint32_t>(c->d_F), P_<uint8_t>(c->d_blob));
+  LSG_HIP(c, hipMemcpyAsync(out576, c->d_blob.p, 576, hipMemcpyDeviceToHost, c->st[0]));
+  SetStatus ss;
+  if ((rc = finish(c, &ss, nullptr, 0))) return rc;
+  *any_error = 0;
   for (size_t i = 0; i < n_sets; i++) {
     int32_t e = set_error(ss, i);
     if (set_err) set_err[i] = e;
-    if (e)
-      *any_error = 1;
-    else
-      groups[0].push_back((int32_t)i);
+    if (e) *any_error = 1;
   }
   for (size_t k = 0; k < c->n_pks; k++)
     if (ss.pkerr[k]) *any_error = 1;
-  std::vector<int32_t> verdict;
-  return run_groups(c, groups, verdict, out576);
+  return LSG_OK;
 }
 
 int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
@@ -1105,14 +1159,14 @@ int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, 
     *valid = 0;
     return LSG_OK;
   }
-  LSG_HIP(c, hipMemcpyAsync(c->d_blob.p, partials576, 576 * n_partials, hipMemcpyHostToDevice, c->stream));
+  LSG_HIP(c, hipMemcpyAsync(c->d_blob.p, partials576, 576 * n_partials, hipMemcpyHostToDevice, c->st[0]));
   LAUNCH(c, k_blobs_to_fp12, n_partials, (int)n_partials, P_<uint8_t>(c->d_blob), P_<uint32_t>(c->d_aux));
   std::vector<std::vector<int32_t>> g(1);
   for (size_t k = 0; k < n_partials; k++) g[0].push_back((int32_t)k);
-  if ((rc = tree_reduce<2>(c, "tree_fp12_product", P_<uint32_t>(c->d_aux), g, P_<uint32_t>(c->d_F)))) return rc;
+  if ((rc = tree_reduce<2>(c, 0, "tree_fp12_product", P_<uint32_t>(c->d_aux), g, P_<uint32_t>(c->d_F)))) return rc;
   LAUNCH(c, k_final_exp_check, 1, 1, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
-  LSG_HIP(c, hipMemcpyAsync(valid, c->d_verdict.p, 4, hipMemcpyDeviceToHost, c->stream));
-  LSG_HIP(c, hipStreamSynchronize(c->stream));
+  LSG_HIP(c, hipMemcpyAsync(valid, c->d_verdict.p, 4, hipMemcpyDeviceToHost, c->st[0]));
+  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
   return LSG_OK;
 }
 
@@ -1130,15 +1184,15 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
     if ((i & 15) < 11) init[i] = (uint32_t)(i * 2654435761u);
   LSG_HIP(c, hipMemcpy(c->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
   const int iters = 64;
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->stream, items, 2,
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->st[0], items, 2,
                      P_<uint32_t>(c->d_aux));
   hipEvent_t a, b;
   LSG_HIP(c, hipEventCreate(&a));
   LSG_HIP(c, hipEventCreate(&b));
-  LSG_HIP(c, hipEventRecord(a, c->stream));
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->stream, items, iters,
+  LSG_HIP(c, hipEventRecord(a, c->st[0]));
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->st[0], items, iters,
                      P_<uint32_t>(c->d_aux));
-  LSG_HIP(c, hipEventRecord(b, c->stream));
+  LSG_HIP(c, hipEventRecord(b, c->st[0]));
   LSG_HIP(c, hipEventSynchronize(b));
   float ms = 0;
   LSG_HIP(c, hipEventElapsedTime(&ms, a, b));
@@ -1152,7 +1206,7 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
 
 int lsg_last_kernel_times(lsg_ctx* c, const char** names, double* ms, int max) {
   if (!c) return 0;
-  (void)hipStreamSynchronize(c->stream);
+  for (int k = 0; k < 3; k++) (void)hipStreamSynchronize(c->st[k]);
   int n = 0;
   for (size_t i = 0; i < c->ntimers && n < max; i++) {
     float t = 0;

@@ -90,6 +90,20 @@ LSG_NOINL fp_t fp_mul(fp_t a, fp_t b) {
   return fp_reduce_once(r);
 }
 
+LSG_INL void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+  r0 = fp_mul(a0, b0);
+  r1 = fp_mul(a1, b1);
+}
+LSG_INL void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
+  for (int k = 0; k < 9; k++) r[k] = fp_mul(a[k], b[k]);
+}
+LSG_INL void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
+                     const fp_t& a2, const fp_t& b2) {
+  r0 = fp_mul(a0, b0);
+  r1 = fp_mul(a1, b1);
+  r2 = fp_mul(a2, b2);
+}
+
 // ---- canonical (non-Montgomery) predicates and byte I/O
 LSG_INL bool fp_canon_gt_half(const fp_t& c) {
   uint32_t br = 0;

@@ -42,7 +42,7 @@ struct fp_t {
 // ---- DPP helpers (control codes must be immediates)
 template <int CTRL, bool BC>
 LSG_DEVI uint32_t dpp(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, BC);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, BC);
 }
 LSG_DEVI uint32_t row_bcast(uint32_t x, int i) {
   switch (i) {
@@ -73,10 +73,19 @@ LSG_DEVI uint32_t lane_bit(uint64_t m) { return (uint32_t)(m >> __lane_id()) & 1
 LSG_DEVI bool row_bit(uint64_t m, uint32_t k) { return ((m >> (row_base() + k)) & 1u) != 0; }
 LSG_DEVI bool row_none(bool pred) { return ((__ballot(pred) >> row_base()) & 0xffffull) == 0; }
 
-LSG_DEVI uint32_t p_limb() {
+// The modulus limb p_j is needed by every add/sub/reduce: a global-memory load there put
+// ~500 cycles of latency on each field addition.  Every lane kernel calls lsg_lane_setup()
+// first; each wave writes the 16 limbs itself (identical values), and LDS operations of one
+// wave complete in order, so no barrier is needed before p_limb() reads them.
+__shared__ uint32_t lsg_lds_p[16];
+LSG_DEVI void lsg_lane_setup() {
   uint32_t j = lane16();
-  return j < 12 ? LSG_P[j] : 0u;
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) v = (j == (uint32_t)k) ? LSG_P[k] : v;  // literals, no memory
+  lsg_lds_p[j] = v;
 }
+LSG_DEVI uint32_t p_limb() { return lsg_lds_p[lane16()]; }
 
 // z < 2p (normalized limbs) -> z mod p
 LSG_DEVI uint32_t lane_reduce_once(uint32_t z, uint32_t pj) {
@@ -87,26 +96,85 @@ LSG_DEVI uint32_t lane_reduce_once(uint32_t z, uint32_t pj) {
   return j < 12 ? r : 0u;
 }
 
-LSG_DEVNOINL uint32_t lane_mont_mul(uint32_t a, uint32_t b) {
+// N independent Montgomery products, interleaved so that one wave keeps N dependency
+// chains in flight (the per-row chain is latency-bound: mad -> add -> DPP -> mul -> mad -> DPP).
+template <int N>
+LSG_DEVI void lane_mont_mul_n(const uint32_t* a, const uint32_t* b, uint32_t* r) {
   const uint32_t pj = p_limb();
-  uint32_t x = 0, ca = 0, cb = 0;
+  uint32_t x[N], ca[N], cb[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = ca[k] = cb[k] = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) {
-    uint32_t bi = row_bcast(b, i);
-    uint64_t s = (uint64_t)a * bi + ((uint64_t)x + ca);
-    uint64_t t2 = (uint64_t)(uint32_t)s + cb;
-    uint32_t m = row_bcast((uint32_t)t2, 0) * LSG_N0P;
-    uint64_t u = (uint64_t)m * pj + t2;
-    x = row_shl1((uint32_t)u);
-    ca = (uint32_t)(s >> 32);
-    cb = (uint32_t)(u >> 32);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      uint32_t bi = row_bcast(b[k], i);
+      // 33-bit addends built with a 32-bit add + carry bit (v_add_co / v_addc), no zero-extends
+      uint32_t tl = x[k] + ca[k];
+      uint32_t th = tl < ca[k];
+      uint64_t s = (uint64_t)a[k] * bi + (((uint64_t)th << 32) | tl);
+      uint32_t sl = (uint32_t)s;
+      uint32_t t2l = sl + cb[k];
+      uint32_t t2h = t2l < cb[k];
+      uint32_t m = row_bcast(t2l, 0) * LSG_N0P;
+      uint64_t u = (uint64_t)m * pj + (((uint64_t)t2h << 32) | t2l);
+      x[k] = row_shl1((uint32_t)u);
+      ca[k] = (uint32_t)(s >> 32);
+      cb[k] = (uint32_t)(u >> 32);
+    }
   }
   // resolve the deferred carries: value = sum_j (x_j + ca_j + cb_j) 2^(32 j) < 2p
-  uint64_t y = (uint64_t)x + ca + cb;
-  uint64_t z = (uint64_t)(uint32_t)y + row_shr1((uint32_t)(y >> 32));
-  uint32_t zl = (uint32_t)z;
-  zl += lane_bit(carry_into((z >> 32) != 0, zl == 0xffffffffu));
-  return lane_reduce_once(zl, pj);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    uint64_t y = (uint64_t)x[k] + ca[k] + cb[k];
+    uint64_t z = (uint64_t)(uint32_t)y + row_shr1((uint32_t)(y >> 32));
+    uint32_t zl = (uint32_t)z;
+    zl += lane_bit(carry_into((z >> 32) != 0, zl == 0xffffffffu));
+    r[k] = lane_reduce_once(zl, pj);
+  }
+}
+
+typedef uint32_t lsg_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t lsg_u32x4 __attribute__((ext_vector_type(4)));
+
+LSG_DEVNOINL uint32_t lane_mont_mul(uint32_t a, uint32_t b) {
+  uint32_t r;
+  lane_mont_mul_n<1>(&a, &b, &r);
+  return r;
+}
+LSG_DEVNOINL lsg_u32x2 lane_mont_mul2(lsg_u32x2 a, lsg_u32x2 b) {
+  uint32_t aa[2] = {a.x, a.y}, bb[2] = {b.x, b.y}, r[2];
+  lane_mont_mul_n<2>(aa, bb, r);
+  lsg_u32x2 o;
+  o.x = r[0];
+  o.y = r[1];
+  return o;
+}
+LSG_DEVNOINL lsg_u32x4 lane_mont_mul3(lsg_u32x4 a, lsg_u32x4 b) {
+  uint32_t aa[3] = {a.x, a.y, a.z}, bb[3] = {b.x, b.y, b.z}, r[3];
+  lane_mont_mul_n<3>(aa, bb, r);
+  lsg_u32x4 o;
+  o.x = r[0];
+  o.y = r[1];
+  o.z = r[2];
+  o.w = 0;
+  return o;
+}
+
+typedef uint32_t lsg_u32x16 __attribute__((ext_vector_type(16)));
+// nine independent products (three Fp2 Karatsuba products) per call
+LSG_DEVNOINL lsg_u32x16 lane_mont_mul9(lsg_u32x16 a, lsg_u32x16 b) {
+  uint32_t aa[9], bb[9], r[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    aa[k] = a[k];
+    bb[k] = b[k];
+  }
+  lane_mont_mul_n<9>(aa, bb, r);
+  lsg_u32x16 o;
+#pragma unroll
+  for (int k = 0; k < 16; k++) o[k] = k < 9 ? r[k] : 0u;
+  return o;
 }
 
 LSG_DEVI uint32_t lane_add(uint32_t a, uint32_t b) {
@@ -137,6 +205,44 @@ LSG_DEVI fp_t fp_add(const fp_t& a, const fp_t& b) { return fp_t(lane_add(a.v, b
 LSG_DEVI fp_t fp_sub(const fp_t& a, const fp_t& b) { return fp_t(lane_sub(a.v, b.v)); }
 LSG_DEVI fp_t fp_neg(const fp_t& a) { return fp_t(lane_sub(0u, a.v)); }
 LSG_DEVI fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_t(lane_mont_mul(a.v, b.v)); }
+LSG_DEVI void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
+  lsg_u32x16 x, y;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    x[k] = k < 9 ? a[k].v : 0u;
+    y[k] = k < 9 ? b[k].v : 0u;
+  }
+  lsg_u32x16 o = lane_mont_mul9(x, y);
+#pragma unroll
+  for (int k = 0; k < 9; k++) r[k] = fp_t(o[k]);
+}
+// two / three independent products with interleaved chains
+LSG_DEVI void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+  lsg_u32x2 a, b;
+  a.x = a0.v;
+  a.y = a1.v;
+  b.x = b0.v;
+  b.y = b1.v;
+  lsg_u32x2 r = lane_mont_mul2(a, b);
+  r0 = fp_t(r.x);
+  r1 = fp_t(r.y);
+}
+LSG_DEVI void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
+                      const fp_t& a2, const fp_t& b2) {
+  lsg_u32x4 a, b;
+  a.x = a0.v;
+  a.y = a1.v;
+  a.z = a2.v;
+  a.w = 0;
+  b.x = b0.v;
+  b.y = b1.v;
+  b.z = b2.v;
+  b.w = 0;
+  lsg_u32x4 r = lane_mont_mul3(a, b);
+  r0 = fp_t(r.x);
+  r1 = fp_t(r.y);
+  r2 = fp_t(r.z);
+}
 
 // ---- canonical predicates and byte I/O (row-uniform results)
 LSG_DEVI bool fp_canon_gt_half(const fp_t& c) {

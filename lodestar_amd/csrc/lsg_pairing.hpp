@@ -94,7 +94,7 @@ LSG_BIGFN fp12_t fp12_exp_by_x(fp12_t g) {
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
   fp12_t r = g;
   for (int b = 62; b >= 0; b--) {
-    r = fp12_sqr(r);
+    r = fp12_cyclotomic_sqr(r);
     if ((xa >> b) & 1u) r = fp12_mul(r, g);
   }
   return fp12_conj(r);

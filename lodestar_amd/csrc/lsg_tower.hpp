@@ -78,25 +78,81 @@ LSG_INL fp2_t fp2_conj(const fp2_t& a) { return fp2_t(a.c0, fp_neg(a.c1)); }
 
 // Karatsuba: 3 Fp multiplications
 LSG_INL fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
-  fp_t t0 = fp_mul(a.c0, b.c0);
-  fp_t t1 = fp_mul(a.c1, b.c1);
-  fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  fp_t t0, t1, t2;
+  fp_mul3(t0, t1, t2, a.c0, b.c0, a.c1, b.c1, fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return fp2_t(fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1));
 }
 
 // (a0 + a1)(a0 - a1), 2 a0 a1
 LSG_INL fp2_t fp2_sqr(const fp2_t& a) {
-  fp_t t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  fp_t t1 = fp_mul(a.c0, a.c1);
+  fp_t t0, t1;
+  fp_mul2(t0, t1, fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1), a.c0, a.c1);
   return fp2_t(t0, fp_dbl(t1));
 }
 
-LSG_INL fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& k) { return fp2_t(fp_mul(a.c0, k), fp_mul(a.c1, k)); }
+LSG_INL fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& k) {
+  fp_t r0, r1;
+  fp_mul2(r0, r1, a.c0, k, a.c1, k);
+  return fp2_t(r0, r1);
+}
+
+// ---- batched products: independent Montgomery chains interleaved 9 at a time
+// (fp_mul9 is one call with nine dependency chains in flight; the tail uses mul3/mul2/mul)
+template <int N>
+LSG_INL void fp_mul_list(fp_t* r, const fp_t* x, const fp_t* y) {
+#pragma unroll
+  for (int g = 0; g + 9 <= N; g += 9) fp_mul9(r + g, x + g, y + g);
+  constexpr int T = N % 9, B = N - T;
+#pragma unroll
+  for (int g = B; g + 3 <= N; g += 3) fp_mul3(r[g], r[g + 1], r[g + 2], x[g], y[g], x[g + 1], y[g + 1], x[g + 2], y[g + 2]);
+  constexpr int B2 = B + (T / 3) * 3;
+  if (N - B2 == 2) fp_mul2(r[B2], r[B2 + 1], x[B2], y[B2], x[B2 + 1], y[B2 + 1]);
+  if (N - B2 == 1) r[B2] = fp_mul(x[B2], y[B2]);
+}
+
+// K independent Fp2 products a[k] * b[k] (Karatsuba, 3K Fp products)
+template <int K>
+LSG_INL void fp2_mul_n(fp2_t* r, const fp2_t* a, const fp2_t* b) {
+  fp_t x[3 * K], y[3 * K], z[3 * K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    x[3 * k] = a[k].c0;
+    y[3 * k] = b[k].c0;
+    x[3 * k + 1] = a[k].c1;
+    y[3 * k + 1] = b[k].c1;
+    x[3 * k + 2] = fp_add(a[k].c0, a[k].c1);
+    y[3 * k + 2] = fp_add(b[k].c0, b[k].c1);
+  }
+  fp_mul_list<3 * K>(z, x, y);
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    r[k] = fp2_t(fp_sub(z[3 * k], z[3 * k + 1]), fp_sub(fp_sub(z[3 * k + 2], z[3 * k]), z[3 * k + 1]));
+}
+
+// K independent Fp2 squarings (2K Fp products)
+template <int K>
+LSG_INL void fp2_sqr_n(fp2_t* r, const fp2_t* a) {
+  fp_t x[2 * K], y[2 * K], z[2 * K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    x[2 * k] = fp_add(a[k].c0, a[k].c1);
+    y[2 * k] = fp_sub(a[k].c0, a[k].c1);
+    x[2 * k + 1] = a[k].c0;
+    y[2 * k + 1] = a[k].c1;
+  }
+  fp_mul_list<2 * K>(z, x, y);
+#pragma unroll
+  for (int k = 0; k < K; k++) r[k] = fp2_t(z[2 * k], fp_dbl(z[2 * k + 1]));
+}
 
 // (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u
 LSG_INL fp2_t fp2_mul_xi(const fp2_t& a) { return fp2_t(fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)); }
 
-LSG_INL fp_t fp2_norm(const fp2_t& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+LSG_INL fp_t fp2_norm(const fp2_t& a) {
+  fp_t s0, s1;
+  fp_mul2(s0, s1, a.c0, a.c0, a.c1, a.c1);
+  return fp_add(s0, s1);
+}
 
 LSG_INL fp2_t fp2_inv(const fp2_t& a) {
   fp_t ni = fp_inv(fp2_norm(a));
@@ -163,15 +219,38 @@ LSG_INL fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) {
 }
 LSG_INL fp6_t fp6_neg(const fp6_t& a) { return fp6_make(fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)); }
 
-// schoolbook as oracle/fields.py:f6_mul
+// Karatsuba Fp6 product in two halves so that several Fp6 products can share batched
+// Fp2 multiplications: prep writes the 6 Fp2 operand pairs, fin combines the 6 products.
+// Same value as oracle/fields.py:f6_mul.
+LSG_INL void fp6_mul_prep(fp2_t* A, fp2_t* B, const fp6_t& a, const fp6_t& b) {
+  A[0] = a.c0;
+  B[0] = b.c0;
+  A[1] = a.c1;
+  B[1] = b.c1;
+  A[2] = a.c2;
+  B[2] = b.c2;
+  A[3] = fp2_add(a.c1, a.c2);
+  B[3] = fp2_add(b.c1, b.c2);
+  A[4] = fp2_add(a.c0, a.c1);
+  B[4] = fp2_add(b.c0, b.c1);
+  A[5] = fp2_add(a.c0, a.c2);
+  B[5] = fp2_add(b.c0, b.c2);
+}
+LSG_INL fp6_t fp6_mul_fin(const fp2_t* V) {
+  fp2_t c0 = fp2_add(V[0], fp2_mul_xi(fp2_sub(fp2_sub(V[3], V[1]), V[2])));
+  fp2_t c1 = fp2_add(fp2_sub(fp2_sub(V[4], V[0]), V[1]), fp2_mul_xi(V[2]));
+  fp2_t c2 = fp2_add(fp2_sub(fp2_sub(V[5], V[0]), V[2]), V[1]);
+  fp6_t r;
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+  return r;
+}
 LSG_BIGFN fp6_t fp6_mul(fp6_t a, fp6_t b) {
-  fp2_t t0 = fp2_mul(a.c0, b.c0);
-  fp2_t t1 = fp2_mul(a.c1, b.c1);
-  fp2_t t2 = fp2_mul(a.c2, b.c2);
-  fp2_t c0 = fp2_add(t0, fp2_mul_xi(fp2_add(fp2_mul(a.c1, b.c2), fp2_mul(a.c2, b.c1))));
-  fp2_t c1 = fp2_add(fp2_add(fp2_mul(a.c0, b.c1), fp2_mul(a.c1, b.c0)), fp2_mul_xi(t2));
-  fp2_t c2 = fp2_add(fp2_add(fp2_mul(a.c0, b.c2), t1), fp2_mul(a.c2, b.c0));
-  return fp6_make(c0, c1, c2);
+  fp2_t A[6], B[6], V[6];
+  fp6_mul_prep(A, B, a, b);
+  fp2_mul_n<6>(V, A, B);
+  return fp6_mul_fin(V);
 }
 
 LSG_INL fp6_t fp6_mul_v(const fp6_t& a) { return fp6_make(fp2_mul_xi(a.c2), a.c0, a.c1); }
@@ -214,29 +293,105 @@ LSG_INL bool fp12_is_one(const fp12_t& a) {
 }
 LSG_INL fp12_t fp12_conj(const fp12_t& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
+// Karatsuba over Fp6: the three Fp6 products (18 Fp2 products) are issued as one batch
 LSG_BIGFN fp12_t fp12_mul(fp12_t a, fp12_t b) {
-  fp6_t t0 = fp6_mul(a.c0, b.c0);
-  fp6_t t1 = fp6_mul(a.c1, b.c1);
-  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
-  fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
-  return fp12_make(c0, c1);
+  fp2_t A[18], B[18], V[18];
+  fp6_mul_prep(A, B, a.c0, b.c0);
+  fp6_mul_prep(A + 6, B + 6, a.c1, b.c1);
+  fp6_mul_prep(A + 12, B + 12, fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1));
+  fp2_mul_n<18>(V, A, B);
+  fp6_t t0 = fp6_mul_fin(V), t1 = fp6_mul_fin(V + 6), t2 = fp6_mul_fin(V + 12);
+  return fp12_make(fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_sub(t2, t0), t1));
 }
 
-// (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w
+// (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w; both Fp6 products in one batch
 LSG_BIGFN fp12_t fp12_sqr(fp12_t a) {
-  fp6_t t = fp6_mul(a.c0, a.c1);
-  fp6_t c0 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1))), t), fp6_mul_v(t));
-  return fp12_make(c0, fp6_add(t, t));
+  fp2_t A[12], B[12], V[12];
+  fp6_mul_prep(A, B, a.c0, a.c1);
+  fp6_mul_prep(A + 6, B + 6, fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp2_mul_n<12>(V, A, B);
+  fp6_t t = fp6_mul_fin(V), u = fp6_mul_fin(V + 6);
+  return fp12_make(fp6_sub(fp6_sub(u, t), fp6_mul_v(t)), fp6_add(t, t));
+}
+
+// (a + b t)^2 in Fp4 = Fp2[t]/(t^2 - xi)  -- oracle/pairing.py:_fp4_square
+LSG_INL void fp4_square(fp2_t& c0, fp2_t& c1, const fp2_t& a, const fp2_t& b) {
+  fp2_t t0 = fp2_sqr(a);
+  fp2_t t1 = fp2_sqr(b);
+  c0 = fp2_add(fp2_mul_xi(t1), t0);
+  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+
+// Granger-Scott squaring for f in the cyclotomic subgroup -- oracle/pairing.py:f12_cyclotomic_sqr
+// (the three Fp4 squarings = 9 Fp2 squarings issued as one batch)
+LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
+  fp2_t z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fp2_t S[9], Q[9];
+  S[0] = z0;
+  S[1] = z1;
+  S[2] = fp2_add(z0, z1);
+  S[3] = z2;
+  S[4] = z3;
+  S[5] = fp2_add(z2, z3);
+  S[6] = z4;
+  S[7] = z5;
+  S[8] = fp2_add(z4, z5);
+  fp2_sqr_n<9>(Q, S);
+  // fp4_square(a, b): c0 = xi b^2 + a^2, c1 = (a + b)^2 - a^2 - b^2
+  fp2_t t0 = fp2_add(fp2_mul_xi(Q[1]), Q[0]);
+  fp2_t t1 = fp2_sub(fp2_sub(Q[2], Q[0]), Q[1]);
+  fp2_t u0 = fp2_add(fp2_mul_xi(Q[4]), Q[3]);
+  fp2_t u1 = fp2_sub(fp2_sub(Q[5], Q[3]), Q[4]);
+  fp2_t t2 = fp2_add(fp2_mul_xi(Q[7]), Q[6]);
+  fp2_t t3 = fp2_sub(fp2_sub(Q[8], Q[6]), Q[7]);
+  z0 = fp2_sub(t0, z0);
+  z0 = fp2_add(fp2_add(z0, z0), t0);
+  z1 = fp2_add(t1, z1);
+  z1 = fp2_add(fp2_add(z1, z1), t1);
+  t0 = u0;
+  t1 = u1;
+  z4 = fp2_sub(t0, z4);
+  z4 = fp2_add(fp2_add(z4, z4), t0);
+  z5 = fp2_add(t1, z5);
+  z5 = fp2_add(fp2_add(z5, z5), t1);
+  t0 = fp2_mul_xi(t3);
+  z2 = fp2_add(t0, z2);
+  z2 = fp2_add(fp2_add(z2, z2), t0);
+  z3 = fp2_sub(t2, z3);
+  z3 = fp2_add(fp2_add(z3, z3), t2);
+  return fp12_make(fp6_make(z0, z4, z3), fp6_make(z2, z1, z5));
 }
 
 // f * ((l00 + l01 v) + (l11 v) w)   -- oracle/pairing.py:f12_mul_line
+// fp6_mul_01(f0, l00, l01), fp6_mul_01(f0 + f1, l00, l01 + l11) and fp6_mul_1(f1, l11):
+// 13 independent Fp2 products issued as one batch.
 LSG_BIGFN fp12_t fp12_mul_line(fp12_t f, fp2_t l00, fp2_t l01, fp2_t l11) {
-  fp6_t t0 = fp6_mul_01(f.c0, l00, l01);
-  fp6_t t1 = fp6_mul_1(f.c1, l11);
+  const fp6_t& a = f.c0;
+  const fp6_t& c = f.c1;
   fp6_t s = fp6_add(f.c0, f.c1);
-  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(s, l00, fp2_add(l01, l11)), t0), t1);
-  fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
-  return fp12_make(c0, c1);
+  fp2_t m = fp2_add(l01, l11);
+  fp2_t A[13], B[13], V[13];
+  // fp6_mul_01(a, l00, l01): a0 b0, a1 b1, a2 b1, (a0+a1)(b0+b1), a2 b0
+  A[0] = a.c0; B[0] = l00;
+  A[1] = a.c1; B[1] = l01;
+  A[2] = a.c2; B[2] = l01;
+  A[3] = fp2_add(a.c0, a.c1); B[3] = fp2_add(l00, l01);
+  A[4] = a.c2; B[4] = l00;
+  // fp6_mul_01(s, l00, m)
+  A[5] = s.c0; B[5] = l00;
+  A[6] = s.c1; B[6] = m;
+  A[7] = s.c2; B[7] = m;
+  A[8] = fp2_add(s.c0, s.c1); B[8] = fp2_add(l00, m);
+  A[9] = s.c2; B[9] = l00;
+  // fp6_mul_1(c, l11): c2 b1, c0 b1, c1 b1
+  A[10] = c.c2; B[10] = l11;
+  A[11] = c.c0; B[11] = l11;
+  A[12] = c.c1; B[12] = l11;
+  fp2_mul_n<13>(V, A, B);
+  fp6_t t0 = fp6_make(fp2_add(fp2_mul_xi(V[2]), V[0]), fp2_sub(fp2_sub(V[3], V[0]), V[1]), fp2_add(V[4], V[1]));
+  fp6_t u = fp6_make(fp2_add(fp2_mul_xi(V[7]), V[5]), fp2_sub(fp2_sub(V[8], V[5]), V[6]), fp2_add(V[9], V[6]));
+  fp6_t t1 = fp6_make(fp2_mul_xi(V[10]), V[11], V[12]);
+  return fp12_make(fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_sub(u, t0), t1));
 }
 
 LSG_BIGFN fp12_t fp12_inv(fp12_t a) {

@@ -244,3 +244,37 @@ def multi_miller_loop(pairs):
 def pairing_check(pairs):
     """prod e(P_i, Q_i) == 1 ?"""
     return f12_is_one(final_exp_fast(multi_miller_loop(pairs)))
+
+
+# ---------------------------------------------------------------- cyclotomic squaring
+def _fp4_square(a, b):
+    """(a + b t)^2 in Fp4 = Fp2[t]/(t^2 - xi): returns (c0, c1)."""
+    from .fields import f2_mul_xi
+    t0 = f2_sqr(a)
+    t1 = f2_sqr(b)
+    c0 = f2_add(f2_mul_xi(t1), t0)
+    t2 = f2_sub(f2_sub(f2_sqr(f2_add(a, b)), t0), t1)
+    return c0, t2
+
+
+def f12_cyclotomic_sqr(f):
+    """Granger-Scott squaring, valid for f in the cyclotomic subgroup (after the easy part);
+    the GPU's fp12_cyclotomic_sqr (lodestar_amd/csrc/lsg_tower.hpp) mirrors it."""
+    (z0, z4, z3), (z2, z1, z5) = f
+    t0, t1 = _fp4_square(z0, z1)
+    z0 = f2_sub(t0, z0)
+    z0 = f2_add(f2_add(z0, z0), t0)
+    z1 = f2_add(t1, z1)
+    z1 = f2_add(f2_add(z1, z1), t1)
+    t0, t1 = _fp4_square(z2, z3)
+    t2, t3 = _fp4_square(z4, z5)
+    z4 = f2_sub(t0, z4)
+    z4 = f2_add(f2_add(z4, z4), t0)
+    z5 = f2_add(t1, z5)
+    z5 = f2_add(f2_add(z5, z5), t1)
+    t0 = f2_mul_xi(t3)
+    z2 = f2_add(t0, z2)
+    z2 = f2_add(f2_add(z2, z2), t0)
+    z3 = f2_sub(t2, z3)
+    z3 = f2_add(f2_add(z3, z3), t2)
+    return ((z0, z4, z3), (z2, z1, z5))
