@@ -8,13 +8,18 @@ single-pubkey gossip-attestation sets per step (weak scaling: at 8 GPUs the node
 b"firehose" || i), signatures sk*H(m) -- synthetic, generated on the GPU before timing.
 
 One step = the sharded hot path of SURVEY.md 8(e) on inputs already resident in HBM:
-  per GPU  lsg_batch_run: decode + subgroup-check signatures, decode pubkeys, hash_to_G2,
-           64-bit RLC scalars, per-set Miller loops, signature-sum Miller loop, Fp12 product
+  per GPU  lsg_batch_submit/wait: decode + subgroup-check signatures, decode pubkeys,
+           hash_to_G2, 64-bit RLC scalars, per-set Miller loops, signature-sum Miller loop,
+           Fp12 product
   node     all_gather of the 576-byte Fp12 partials (RCCL over xGMI when N > 1)
-  rank 0.. lsg_final_verify: product of partials + one final exponentiation -> verdict
+  rank 0.. lsg_final_submit/wait: product of partials + one final exponentiation -> verdict
+Steps are pipelined as a firehose verifier runs them: two batches in flight (the library's two
+pipeline slots) and the final exponentiation of batch k on its own stream while batch k+1
+computes.  Every batch is verified (verdict checked) inside the timed region.
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
 """
 import argparse
+import collections
 import hashlib
 import json
 import os
@@ -23,6 +28,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# 2 pipeline slots x 2 streams + the final-exponentiation stream (+ RCCL's): give each its
+# own hardware queue instead of HIP's default 4 shared ones
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -86,7 +94,7 @@ def main():
     ctx = Context(local)
     n = args.sets_per_gpu
     sets = make_shard(ctx, rank, n)
-    ctx.batch_stage(sets, seed=0x5EED + rank)
+    staged = ctx.stage(sets, seed=0x5EED + rank)
 
     def gather(part):
         if dist is None:
@@ -102,22 +110,42 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def step():
-        part, anyerr = ctx.batch_run()
-        parts = gather(part)
-        ok = ctx.final_verify(parts)
+    def check(anyerr, ok):
         if anyerr or not ok:
             raise SystemExit(f"rank {rank}: verification failed (anyerr={anyerr}, verdict={ok})")
 
-    for _ in range(args.warmup):
-        step()
+    def run(k_steps, depth=2, capture=False):
+        """k_steps batches, `depth` in flight; returns per-batch submit->verdict latencies and
+        (if capture) the per-kernel HIP-event times of the last batch and its final exp."""
+        lat, times = [], []
+        pend_b, pend_f = collections.deque(), collections.deque()
+        submitted = 0
+        while submitted < k_steps and len(pend_b) < depth:
+            pend_b.append((ctx.batch_submit(staged), time.perf_counter()))
+            submitted += 1
+        while pend_b:
+            tb, t_sub = pend_b.popleft()
+            part, _errs, anyerr = ctx.batch_wait(tb)
+            check(anyerr, True)
+            if capture and not pend_b and submitted == k_steps:
+                times += ctx.last_kernel_times()
+            tf = ctx.final_submit(gather(part))
+            pend_f.append((tf, t_sub, anyerr))
+            if submitted < k_steps:
+                pend_b.append((ctx.batch_submit(staged), time.perf_counter()))
+                submitted += 1
+            while pend_f and (len(pend_f) > 1 or not pend_b):
+                tf0, t0, ae = pend_f.popleft()
+                check(ae, ctx.final_wait(tf0))
+                lat.append(time.perf_counter() - t0)
+        if capture:
+            times += ctx.last_kernel_times()
+        return lat, times
+
+    run(args.warmup)
     barrier()
-    lat = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        s0 = time.perf_counter()
-        step()
-        lat.append(time.perf_counter() - s0)
+    lat, ktimes = run(args.steps, capture=True)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -125,27 +153,27 @@ def main():
         te = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
+    # unloaded latency: one batch at a time
+    lat1, _ = run(3, depth=1)
 
-    # kernel-level roofline for the dominant kernel of the last step (HIP events on ctx's stream)
-    ctx.batch_run()
-    ktimes = ctx.last_kernel_times()
+    # kernel-level roofline for the dominant kernel, from HIP events recorded on the streams
+    # the kernels ran on during the last timed batch
     opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
     probe_fp, probe_mad = ctx.probe_fp_mul_rate()
     peak_mad = float(os.environ.get("LSG_PEAK_MAD_PER_S", "2.827e13"))  # measured v_mad_u64_u32 peak (profiles/)
     agg = {}
     for name, ms in ktimes:
         agg[name] = agg.get(name, 0.0) + ms
-    dom = max(agg, key=agg.get)
     stage_of = {"k_miller_sets": "miller", "k_hash_map": "hash_map", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
-    roof = None
-    if dom in stage_of:
-        muls = opc["stage_fp_muls"][stage_of[dom]] * n
-        achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] * 1e-3) / 1e12
-        peak = peak_mad / 1e12
-        roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
-                "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
+    per_set = {k: v for k, v in agg.items() if k in stage_of}
+    dom = max(per_set, key=per_set.get)
+    muls = opc["stage_fp_muls"][stage_of[dom]] * n
+    achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] * 1e-3) / 1e12
+    peak = peak_mad / 1e12
+    roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
+            "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4), "traffic": None,
+            "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
     total_sets = n * world * args.steps
     value = total_sets / elapsed
     per_set_muls = opc["batched_single_set_fp_muls"]
@@ -163,6 +191,8 @@ def main():
                        "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
                        "parallelism": f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
+            "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
+            "pipeline_depth": 2,
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},
@@ -170,6 +200,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    staged.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -14,8 +14,10 @@
  *   lsg_aggregate_pubkeys  <- utils.ts:11 PublicKey.aggregate (+ toBytes, index.ts:177)
  *   lsg_hash_to_g2         <- blst Hash_to_G2 inside Pairing.mul_n_aggregate
  *   lsg_sig_decode         <- maybeBatch.ts:23,36 Signature.fromBytes(bytes, affine, true)
- *   lsg_batch_partial /    <- the per-GPU half of verifyMultipleSignatures for the
- *   lsg_final_verify          node-sharded path: Miller-loop product
+ *   lsg_submit_jobs /      <- the asynchronous lsg_submit / lsg_wait pair of SURVEY.md 8b:
+ *   lsg_wait_jobs             one BlsWorkReq[] package in flight per pipeline slot
+ *   lsg_batch_* /          <- the per-GPU half of verifyMultipleSignatures for the
+ *   lsg_final_*               node-sharded path: Miller-loop product
  *                             per shard, all-gathered by the caller, one final exponentiation
  *
  * Plain pointers and sizes only; every call returns an int status (LSG_OK = 0) and never
@@ -40,6 +42,7 @@ extern "C" {
 #define LSG_ERR_DEVICE 3
 #define LSG_ERR_NOMEM 4
 #define LSG_ERR_CLOSED 5
+#define LSG_ERR_BUSY 6 /* every pipeline slot holds an outstanding ticket (canAcceptWork false) */
 
 /* ---- blst error codes (blst.h BLST_ERROR) + @chainsafe/blst's size error */
 #define LSG_BLST_SUCCESS 0
@@ -65,6 +68,8 @@ extern "C" {
 #define LSG_JOB_PRIORITY 2u
 
 typedef struct lsg_ctx lsg_ctx;
+typedef struct lsg_staged lsg_staged; /* device-resident package of sets */
+typedef uint64_t lsg_ticket;          /* handle of an in-flight submission */
 
 /* One signature set (ISignatureSet, state-transition/src/util/signatureSets.ts:10-22).
  * Pubkeys are the set's n_pks keys back to back, each pk_len bytes (48 compressed or
@@ -105,14 +110,25 @@ typedef struct {
 } lsg_stats;
 
 /* Context owning one device's streams and buffers.  device_ordinal < 0 -> device 0.
- * Calls on one context are serialised internally; use one context per thread/device. */
+ * A context has two pipeline slots (each: a main and a side HIP stream plus its own
+ * device state) and a final-exponentiation stream, so up to two packages are in flight
+ * while earlier final exponentiations finish.  Calls are serialised by an internal mutex. */
 int lsg_init(int device_ordinal, lsg_ctx** out);
 int lsg_destroy(lsg_ctx* ctx);
 const char* lsg_last_error(lsg_ctx* ctx);
 int lsg_device_name(lsg_ctx* ctx, char* buf, size_t len);
 
-/* worker.ts:30-106 for one work package.  seed != 0 makes the RLC randomizers
- * deterministic (tests); seed == 0 draws them from the OS CSPRNG.  results[n_jobs]. */
+/* worker.ts:30-106 for one work package (BlsWorkReq[] -> BlsWorkResult), asynchronous:
+ * submit copies the jobs into pinned staging memory, launches every stage and returns a
+ * ticket (LSG_ERR_BUSY when both slots are outstanding: back-pressure as in
+ * canAcceptWork, multithread/index.ts:143-149); wait blocks on that ticket, applies the
+ * batch/retry verdict rules and runs the per-job retries.  seed != 0 makes the RLC
+ * randomizers deterministic (tests); seed == 0 draws them from the OS CSPRNG. */
+int lsg_submit_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket);
+int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n_jobs] */, lsg_stats* stats);
+/* *done = 1 once the ticket's device work has finished (any ticket kind). */
+int lsg_poll(lsg_ctx* ctx, lsg_ticket ticket, int32_t* done);
+/* submit + wait */
 int lsg_verify_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_job_result* results,
                     lsg_stats* stats);
 
@@ -133,16 +149,23 @@ int lsg_hash_to_g2(lsg_ctx* ctx, const uint8_t* msgs, uint32_t msg_len, size_t n
 int lsg_sig_decode(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, size_t n, uint8_t* out192, int32_t* err);
 
 /* Sharded batch: one shard's sets -> its un-exponentiated Miller product
- * (576 bytes: 12 canonical big-endian Fp in tower order), per-set error codes.
- * *any_error != 0 means the shard cannot be batched (caller falls back to retry). */
+ * (576 bytes: 12 canonical big-endian Fp in tower order) over the sets that decode, and
+ * per-set error codes.  *any_error != 0 means the shard cannot be batched (the caller
+ * falls back to per-job verification). */
 int lsg_batch_partial(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
                       int32_t* set_err, int32_t* any_error);
-/* The same in two halves: stage copies the shard's inputs (and randomizers) into device
- * memory; run executes the kernels on the resident inputs (the benchmark times only run). */
-int lsg_batch_stage(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed);
-int lsg_batch_run(lsg_ctx* ctx, uint8_t* out576, int32_t* set_err, int32_t* any_error);
-/* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1). */
+/* The same split for pipelining: stage copies a package (and its randomizers) into device
+ * memory once; submit runs the kernels on the resident package (which must outlive the
+ * ticket) and wait returns the partial.  The benchmark times submit..wait only. */
+int lsg_stage(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_staged** out);
+int lsg_staged_free(lsg_ctx* ctx, lsg_staged* staged);
+int lsg_batch_submit(lsg_ctx* ctx, const lsg_staged* staged, lsg_ticket* ticket);
+int lsg_batch_wait(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* set_err, int32_t* any_error);
+/* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1).  The
+ * submit/wait pair runs on the context's final stream, overlapping later batches. */
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
+int lsg_final_submit(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket);
+int lsg_final_wait(lsg_ctx* ctx, lsg_ticket ticket, int32_t* valid);
 
 /* Test/bench input generation (not on the verify path): sig_i = sk_i * H(m_i) compressed,
  * pk_i = sk_i * G1 uncompressed; sks are 32-byte big-endian secret keys. */
@@ -153,8 +176,9 @@ int lsg_sk_to_pk(lsg_ctx* ctx, const uint8_t* sks32, size_t n, uint8_t* out96);
  * Montgomery multiplications; reports Fp-mul/s and v_mad_u64_u32/s (x300 per mul). */
 int lsg_probe_fp_mul_rate(lsg_ctx* ctx, double* fp_mul_per_s, double* mad_per_s);
 
-/* Per-kernel timing of the last lsg_verify_jobs/lsg_batch_partial call, from HIP events
- * on the context's stream: names[i] / ms[i] for up to max entries; returns count. */
+/* Per-kernel timing of the most recently completed ticket (or synchronous call), from HIP
+ * events on the streams the kernels ran on: names[i] / ms[i] for up to max entries;
+ * returns the count. */
 int lsg_last_kernel_times(lsg_ctx* ctx, const char** names, double* ms, int max);
 
 #ifdef __cplusplus

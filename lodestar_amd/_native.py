@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(HERE, "liblodestar_bls.so")
 
 LSG_OK = 0
 LSG_ERR_NO_DEVICE = 2
+LSG_ERR_BUSY = 6
 
 LSG_INVALID = 0
 LSG_VALID = 1
@@ -75,7 +76,8 @@ EXPORTS = [
     "lsg_init", "lsg_destroy", "lsg_last_error", "lsg_device_name", "lsg_verify_jobs", "lsg_verify_sets",
     "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
     "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
-    "lsg_batch_stage", "lsg_batch_run",
+    "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
+    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait",
 ]
 
 
@@ -108,8 +110,16 @@ def load_library(path=LIB_PATH):
                                               ctypes.c_int]
         lib.lsg_sign.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u32, sz, ctypes.c_char_p]
         lib.lsg_sk_to_pk.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p]
-        lib.lsg_batch_stage.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64]
-        lib.lsg_batch_run.argtypes = [vp, ctypes.c_char_p, pi32, pi32]
+        pu64 = ctypes.POINTER(u64)
+        lib.lsg_submit_jobs.argtypes = [vp, ctypes.POINTER(LsgJob), sz, u64, pu64]
+        lib.lsg_wait_jobs.argtypes = [vp, u64, ctypes.POINTER(LsgJobResult), ctypes.POINTER(LsgStats)]
+        lib.lsg_poll.argtypes = [vp, u64, pi32]
+        lib.lsg_stage.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.POINTER(vp)]
+        lib.lsg_staged_free.argtypes = [vp, vp]
+        lib.lsg_batch_submit.argtypes = [vp, vp, pu64]
+        lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
+        lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
+        lib.lsg_final_wait.argtypes = [vp, u64, pi32]
         for name in EXPORTS:
             if name != "lsg_last_error":
                 getattr(lib, name).restype = ctypes.c_int
@@ -176,21 +186,52 @@ class Context:
         self._check(self.lib.lsg_device_name(self.h, b, 256), "lsg_device_name")
         return b.value.decode()
 
-    def verify_jobs(self, jobs, seed=0):
-        """jobs: list of (sets, flags) with sets = list of (pks, msg, sig).
-        Returns (results list of (status, err_code), stats dict)."""
+    @staticmethod
+    def _job_array(jobs):
         bufs = [SetBuffer(sets) for sets, _ in jobs]
         arr = (LsgJob * max(len(jobs), 1))()
         for i, ((sets, flags), b) in enumerate(zip(jobs, bufs)):
             arr[i].sets = b.arr
             arr[i].n_sets = b.n
             arr[i].flags = flags
+        return arr, bufs
+
+    def verify_jobs(self, jobs, seed=0):
+        """jobs: list of (sets, flags) with sets = list of (pks, msg, sig).
+        Returns (results list of (status, err_code), stats dict)."""
+        arr, _bufs = self._job_array(jobs)
         res = (LsgJobResult * max(len(jobs), 1))()
         st = LsgStats()
         self._check(self.lib.lsg_verify_jobs(self.h, arr, len(jobs), seed, res, ctypes.byref(st)), "lsg_verify_jobs")
         out = [(res[i].status, res[i].err_code) for i in range(len(jobs))]
         stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
         return out, stats
+
+    def submit_jobs(self, jobs, seed=0):
+        """Asynchronous verify_jobs: returns a ticket for wait_jobs, or None when both
+        pipeline slots are busy (LSG_ERR_BUSY).  The inputs are copied before returning."""
+        arr, _bufs = self._job_array(jobs)
+        t = ctypes.c_uint64()
+        rc = self.lib.lsg_submit_jobs(self.h, arr, len(jobs), seed, ctypes.byref(t))
+        if rc == LSG_ERR_BUSY:
+            return None
+        self._check(rc, "lsg_submit_jobs")
+        return (t.value, len(jobs))
+
+    def wait_jobs(self, ticket):
+        t, n = ticket
+        res = (LsgJobResult * max(n, 1))()
+        st = LsgStats()
+        self._check(self.lib.lsg_wait_jobs(self.h, t, res, ctypes.byref(st)), "lsg_wait_jobs")
+        out = [(res[i].status, res[i].err_code) for i in range(n)]
+        stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
+        return out, stats
+
+    def poll(self, ticket):
+        t = ticket[0] if isinstance(ticket, tuple) else ticket
+        d = ctypes.c_int32()
+        self._check(self.lib.lsg_poll(self.h, t, ctypes.byref(d)), "lsg_poll")
+        return bool(d.value)
 
     def verify_sets(self, sets, seed=0):
         b = SetBuffer(sets)
@@ -234,22 +275,47 @@ class Context:
                     "lsg_batch_partial")
         return out.raw, [errs[i] for i in range(b.n)], bool(anyerr.value)
 
-    def batch_stage(self, sets, seed=0):
-        self._staged = SetBuffer(sets)
-        self._check(self.lib.lsg_batch_stage(self.h, self._staged.arr, self._staged.n, seed), "lsg_batch_stage")
-        self._staged_n = self._staged.n
+    def stage(self, sets, seed=0):
+        """Copy a package into device memory once (lsg_stage); returns a Staged handle."""
+        b = SetBuffer(sets)
+        h = ctypes.c_void_p()
+        self._check(self.lib.lsg_stage(self.h, b.arr, b.n, seed, ctypes.byref(h)), "lsg_stage")
+        return Staged(self, h, b.n)
 
-    def batch_run(self):
+    def batch_submit(self, staged):
+        t = ctypes.c_uint64()
+        rc = self.lib.lsg_batch_submit(self.h, staged.h, ctypes.byref(t))
+        if rc == LSG_ERR_BUSY:
+            return None
+        self._check(rc, "lsg_batch_submit")
+        return (t.value, staged.n)
+
+    def batch_wait(self, ticket):
+        """-> (partial 576 bytes, per-set error codes, any_error)"""
+        t, n = ticket
         out = ctypes.create_string_buffer(576)
-        errs = (ctypes.c_int32 * max(self._staged_n, 1))()
+        errs = (ctypes.c_int32 * max(n, 1))()
         anyerr = ctypes.c_int32()
-        self._check(self.lib.lsg_batch_run(self.h, out, errs, ctypes.byref(anyerr)), "lsg_batch_run")
-        return out.raw, bool(anyerr.value)
+        self._check(self.lib.lsg_batch_wait(self.h, t, out, errs, ctypes.byref(anyerr)), "lsg_batch_wait")
+        return out.raw, [errs[i] for i in range(n)], bool(anyerr.value)
 
     def final_verify(self, partials):
         v = ctypes.c_int32()
         self._check(self.lib.lsg_final_verify(self.h, b"".join(partials), len(partials), ctypes.byref(v)),
                     "lsg_final_verify")
+        return bool(v.value)
+
+    def final_submit(self, partials):
+        t = ctypes.c_uint64()
+        rc = self.lib.lsg_final_submit(self.h, b"".join(partials), len(partials), ctypes.byref(t))
+        if rc == LSG_ERR_BUSY:
+            return None
+        self._check(rc, "lsg_final_submit")
+        return t.value
+
+    def final_wait(self, ticket):
+        v = ctypes.c_int32()
+        self._check(self.lib.lsg_final_wait(self.h, ticket, ctypes.byref(v)), "lsg_final_wait")
         return bool(v.value)
 
     def sign(self, sks, msgs):
@@ -280,3 +346,15 @@ class Context:
         ms = (ctypes.c_double * max_entries)()
         n = self.lib.lsg_last_kernel_times(self.h, names, ms, max_entries)
         return [(names[i].decode(), ms[i]) for i in range(n)]
+
+
+class Staged:
+    """A device-resident package (lsg_staged); must outlive the tickets that use it."""
+
+    def __init__(self, ctx, h, n):
+        self.ctx, self.h, self.n = ctx, h, n
+
+    def free(self):
+        if self.h:
+            self.ctx._check(self.ctx.lib.lsg_staged_free(self.ctx.h, self.h), "lsg_staged_free")
+            self.h = None

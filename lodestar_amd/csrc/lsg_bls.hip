@@ -341,10 +341,20 @@ __global__ void __launch_bounds__(LSG_TPB) k_probe_fp_mul(int n, int iters, uint
 }
 
 // ---------------------------------------------------------------------------- host side
+//
+// Pipelining.  A context owns LSG_SLOTS pipeline slots; each slot has two streams (main:
+// hash_to_G2 -> Miller loops -> products -> FE; side: pubkeys -> signatures -> RLC sums ->
+// signature Miller loop), its own device state and pinned host mirrors.  A submit call
+// launches one package on a free slot and returns a ticket without waiting; the matching
+// wait call synchronises on the slot's completion event and applies the reference's verdict
+// rules.  Final exponentiations of all-gathered partials run on a dedicated stream, so the
+// serial FE of batch k overlaps the per-set stages of batch k+1.
 namespace {
 
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
+constexpr int LSG_SLOTS = 2;   // batch / job slots in flight
+constexpr int LSG_FINALS = 4;  // final-exponentiation entries in flight
 
 // u32 words per item for each lane-form type
 constexpr size_t W_G1A = lane_words<g1a_t>();
@@ -352,7 +362,6 @@ constexpr size_t W_G1P = lane_words<g1p_t>();
 constexpr size_t W_G2A = lane_words<g2a_t>();
 constexpr size_t W_G2P = lane_words<g2p_t>();
 constexpr size_t W_F12 = lane_words<fp12_t>();
-constexpr size_t W_MAX = W_F12;
 
 uint64_t now_ns() {
   timespec ts;
@@ -372,56 +381,121 @@ struct DevBuf {
   size_t cap = 0;
 };
 
+struct HostBuf {  // pinned host memory (async copies)
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
 struct Timer {
   const char* name;
   hipEvent_t a, b;
 };
 
-}  // namespace
-
 struct TreeSlot {
   DevBuf idx, tA, tB;
-  std::vector<int32_t> host;  // index pairs of the last reduction (alive until the call syncs)
+  std::vector<int32_t> host;  // index pairs of the last reduction (alive until the slot completes)
 };
 
-// Three streams: S0 = hash_to_G2 -> Miller loops -> products -> FE, S1 = pubkeys,
-// S2 = signatures (decode, subgroup, RLC scaling, sums, sig Miller loop).  Stage order is
-// encoded with events; one synchronisation per phase.
-struct lsg_ctx {
-  int device = 0;
-  hipStream_t st[3] = {nullptr, nullptr, nullptr};
-  int cur = 0;
-  hipEvent_t ev_pk = nullptr, ev_sig = nullptr, ev_grp = nullptr;
-  std::mutex mu;
-  std::string err;
-  // inputs
-  DevBuf d_sig, d_siglen, d_msg, d_msgoff, d_msglen, d_pk, d_pklen, d_rnd, d_dst;
-  // per-set / per-pk state
-  DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_fall;
-  // groups and reductions
-  DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
-  TreeSlot tree[3];
-  std::vector<Timer> timers;
-  size_t ntimers = 0;
+// chunkifyMaximizeChunkSize (multithread/utils.ts:4-19)
+std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t chunk_count = len / min_per_chunk;
+  if (chunk_count <= 1) {
+    out.push_back({0, len});
+    return out;
+  }
+  size_t per = (len + chunk_count - 1) / chunk_count;
+  for (size_t i = 0; i < len; i += per) out.push_back({i, std::min(len, i + per)});
+  return out;
+}
+
+}  // namespace
+
+// A device-resident package of signature sets (inputs + randomizers), read-only to kernels.
+struct lsg_staged {
+  DevBuf d_sig, d_siglen, d_msg, d_msgoff, d_msglen, d_pk, d_pklen, d_rnd;
+  HostBuf h_arena;  // pinned staging copy
   size_t n_sets = 0, n_pks = 0;
-  std::vector<uint32_t> pk_off, pk_cnt;  // host copy of the staged set -> pk ranges
-  std::vector<std::vector<int32_t>> sets_pks;
+  std::vector<uint32_t> pk_cnt;
+  std::vector<std::vector<int32_t>> sets_pks;  // per set: indices of its pubkeys
 };
 
 namespace {
 
-int fail(lsg_ctx* c, const char* what, hipError_t e) {
+enum SlotKind { SLOT_FREE = 0, SLOT_JOBS = 1, SLOT_BATCH = 2, SLOT_FINAL = 3, SLOT_UTIL = 4 };
+
+struct JobsPlan {
+  std::vector<size_t> jfirst, jcount;
+  std::vector<std::vector<int32_t>> groups;
+  std::vector<std::vector<size_t>> group_jobs;
+  std::vector<bool> group_is_chunk;
+  std::vector<std::vector<size_t>> empty_chunks;
+  std::vector<lsg_job_result> results;
+  lsg_stats stats;
+};
+
+struct Slot {
+  lsg_ctx* c = nullptr;
+  int index = 0;
+  hipStream_t st[2] = {nullptr, nullptr};  // [0] main, [1] side
+  bool own_streams = true;
+  int cur = 0;
+  hipEvent_t ev_in = nullptr, ev_sig = nullptr, ev_grp = nullptr, ev_done = nullptr;
+  lsg_staged own;                  // inputs staged by submit calls
+  const lsg_staged* in = nullptr;  // inputs of the running package
+  DevBuf d_dst;
+  // per-set / per-pk state
+  DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_fall;
+  // groups, reductions, outputs
+  DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
+  TreeSlot tree[3];
+  HostBuf h_err, h_pinf, h_pkerr, h_verdict, h_blob;  // pinned result mirrors
+  size_t n_verdicts = 0;
+  std::vector<Timer> timers;
+  size_t ntimers = 0;
+  // ticket state
+  int kind = SLOT_FREE;
+  uint64_t serial = 0;
+  JobsPlan plan;
+};
+
+}  // namespace
+
+struct lsg_ctx {
+  int device = 0;
+  std::mutex mu;
+  std::string err;
+  hipStream_t s_final = nullptr;  // final exponentiations + utility calls
+  Slot slots[LSG_SLOTS];
+  Slot finals[LSG_FINALS];
+  Slot util;
+  uint64_t next_serial = 1;
+  const Slot* last = nullptr;  // slot whose timers lsg_last_kernel_times reports
+};
+
+namespace {
+
+int fail(Slot* s, const char* what, hipError_t e) {
+  s->c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return LSG_ERR_DEVICE;
+}
+int fail_c(lsg_ctx* c, const char* what, hipError_t e) {
   c->err = std::string(what) + ": " + hipGetErrorString(e);
   return LSG_ERR_DEVICE;
 }
 
-#define LSG_HIP(c, call)                               \
+#define LSG_HIP(s, call)                               \
   do {                                                 \
     hipError_t _e = (call);                            \
-    if (_e != hipSuccess) return fail((c), #call, _e); \
+    if (_e != hipSuccess) return fail((s), #call, _e); \
+  } while (0)
+#define LSG_HIPC(c, call)                                \
+  do {                                                   \
+    hipError_t _e = (call);                              \
+    if (_e != hipSuccess) return fail_c((c), #call, _e); \
   } while (0)
 
-int ensure(lsg_ctx* c, DevBuf& b, size_t bytes) {
+int ensure(Slot* s, DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 64;
   if (b.cap >= bytes) return LSG_OK;
   if (b.p) (void)hipFree(b.p);
@@ -429,148 +503,243 @@ int ensure(lsg_ctx* c, DevBuf& b, size_t bytes) {
   b.cap = 0;
   size_t cap = std::max(bytes + bytes / 4, (size_t)4096);
   hipError_t e = hipMalloc(&b.p, cap);
-  if (e != hipSuccess) return fail(c, "hipMalloc", e);
+  if (e != hipSuccess) return fail(s, "hipMalloc", e);
+  b.cap = cap;
+  return LSG_OK;
+}
+
+int ensure_host(Slot* s, HostBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 64;
+  if (b.cap >= bytes) return LSG_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)4096);
+  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(s, "hipHostMalloc", e);
   b.cap = cap;
   return LSG_OK;
 }
 
 template <class T>
-T* P_(DevBuf& b) {
+T* P_(const DevBuf& b) {
+  return (T*)b.p;
+}
+template <class T>
+T* H_(const HostBuf& b) {
   return (T*)b.p;
 }
 
 int lane_blocks(size_t items) { return (int)((items + LSG_ITEMS_PER_BLOCK - 1) / LSG_ITEMS_PER_BLOCK); }
 
-inline hipStream_t S_(lsg_ctx* c) { return c->st[c->cur]; }
+inline hipStream_t S_(Slot* s) { return s->st[s->cur]; }
 
-void timer_reset(lsg_ctx* c) {
-  c->ntimers = 0;
-  c->cur = 0;
+void timer_reset(Slot* s) {
+  s->ntimers = 0;
+  s->cur = 0;
 }
 
-void timer_begin(lsg_ctx* c, const char* name) {
-  if (c->ntimers >= c->timers.size()) {
+void timer_begin(Slot* s, const char* name) {
+  if (s->ntimers >= s->timers.size()) {
     Timer t;
     (void)hipEventCreate(&t.a);
     (void)hipEventCreate(&t.b);
-    c->timers.push_back(t);
+    s->timers.push_back(t);
   }
-  Timer& t = c->timers[c->ntimers];
+  Timer& t = s->timers[s->ntimers];
   t.name = name;
-  (void)hipEventRecord(t.a, S_(c));
+  (void)hipEventRecord(t.a, S_(s));
 }
 
-void timer_end(lsg_ctx* c) {
-  (void)hipEventRecord(c->timers[c->ntimers].b, S_(c));
-  c->ntimers++;
+void timer_end(Slot* s) {
+  (void)hipEventRecord(s->timers[s->ntimers].b, S_(s));
+  s->ntimers++;
 }
 
-#define LAUNCH_T(c, name, kern, grid, tpb, ...)                                       \
-  do {                                                                                \
-    timer_begin((c), name);                                                           \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb), 0, S_(c), __VA_ARGS__);           \
-    timer_end((c));                                                                   \
-    hipError_t _le = hipGetLastError();                                               \
-    if (_le != hipSuccess) return fail((c), name, _le);                               \
+#define LAUNCH_T(s, name, kern, grid, tpb, ...)                             \
+  do {                                                                      \
+    timer_begin((s), name);                                                 \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb), 0, S_(s), __VA_ARGS__); \
+    timer_end((s));                                                         \
+    hipError_t _le = hipGetLastError();                                     \
+    if (_le != hipSuccess) return fail((s), name, _le);                     \
   } while (0)
-#define LAUNCH(c, kern, items, ...) LAUNCH_T(c, #kern, kern, lane_blocks(items), LSG_TPB, __VA_ARGS__)
+#define LAUNCH(s, kern, items, ...) LAUNCH_T(s, #kern, kern, lane_blocks(items), LSG_TPB, __VA_ARGS__)
 
-int sync_all(lsg_ctx* c) {
-  for (int k = 0; k < 3; k++) LSG_HIP(c, hipStreamSynchronize(c->st[k]));
+int slot_create(lsg_ctx* c, Slot* s, int index, hipStream_t shared) {
+  s->c = c;
+  s->index = index;
+  if (shared) {
+    s->st[0] = s->st[1] = shared;
+    s->own_streams = false;
+  } else {
+    for (int k = 0; k < 2; k++) LSG_HIP(s, hipStreamCreateWithFlags(&s->st[k], hipStreamNonBlocking));
+  }
+  hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_done};
+  for (hipEvent_t* e : evs) LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  int rc = ensure(s, s->d_dst, 256);
+  if (rc) return rc;
+  LSG_HIP(s, hipMemcpy(s->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice));
   return LSG_OK;
 }
 
-// ---- stage a package of sets into device memory (one synchronous batch of copies)
-int stage_sets(lsg_ctx* c, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
+void free_dev(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+void free_host(HostBuf& b) {
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+void staged_free(lsg_staged* in) {
+  DevBuf* bufs[] = {&in->d_sig, &in->d_siglen, &in->d_msg, &in->d_msgoff, &in->d_msglen, &in->d_pk, &in->d_pklen, &in->d_rnd};
+  for (DevBuf* b : bufs) free_dev(*b);
+  free_host(in->h_arena);
+}
+
+void slot_destroy(Slot* s) {
+  if (!s->c) return;
+  for (int k = 0; k < 2; k++)
+    if (s->st[k]) (void)hipStreamSynchronize(s->st[k]);
+  staged_free(&s->own);
+  DevBuf* bufs[] = {&s->d_dst, &s->d_ub, &s->d_sigaff, &s->d_siginf, &s->d_seterr, &s->d_pkp, &s->d_pkerr,
+                    &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
+                    &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux};
+  for (DevBuf* b : bufs) free_dev(*b);
+  for (TreeSlot& t : s->tree) {
+    free_dev(t.idx);
+    free_dev(t.tA);
+    free_dev(t.tB);
+  }
+  HostBuf* hb[] = {&s->h_err, &s->h_pinf, &s->h_pkerr, &s->h_verdict, &s->h_blob};
+  for (HostBuf* b : hb) free_host(*b);
+  for (Timer& t : s->timers) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  hipEvent_t evs[] = {s->ev_in, s->ev_sig, s->ev_grp, s->ev_done};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  if (s->own_streams)
+    for (int k = 0; k < 2; k++)
+      if (s->st[k]) (void)hipStreamDestroy(s->st[k]);
+  s->c = nullptr;
+}
+
+// ---- stage a package of sets: host layout in a pinned arena, async copies on `stream`
+int stage_sets(Slot* s, lsg_staged* in, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale,
+               hipStream_t stream) {
   size_t npk = 0, msg_total = 0;
   for (size_t i = 0; i < n; i++) {
     npk += sets[i]->n_pks;
     msg_total += sets[i]->msg_len;
   }
-  c->n_sets = n;
-  c->n_pks = npk;
+  in->n_sets = n;
+  in->n_pks = npk;
   size_t nn = std::max(n, (size_t)1), np = std::max(npk, (size_t)1);
-  std::vector<uint8_t> sig(192 * nn, 0), msg(std::max(msg_total, (size_t)1)), pk(96 * np, 0);
-  std::vector<uint32_t> siglen(nn), msgoff(nn), msglen(nn), pklen(np);
-  std::vector<uint64_t> rnd(nn);
-  c->pk_off.assign(n, 0);
-  c->pk_cnt.assign(n, 0);
+  // arena layout (all offsets 8-byte aligned)
+  auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
+  size_t o_sig = 0, o_siglen = al(o_sig + 192 * nn), o_msgoff = al(o_siglen + 4 * nn), o_msglen = al(o_msgoff + 4 * nn),
+         o_pklen = al(o_msglen + 4 * nn), o_rnd = al(o_pklen + 4 * np), o_pk = al(o_rnd + 8 * nn),
+         o_msg = al(o_pk + 96 * np), total = al(o_msg + std::max(msg_total, (size_t)1));
+  int rc;
+  if ((rc = ensure_host(s, in->h_arena, total))) return rc;
+  uint8_t* A = H_<uint8_t>(in->h_arena);
+  memset(A + o_sig, 0, 192 * nn);
+  memset(A + o_pk, 0, 96 * np);
+  uint32_t* siglen = (uint32_t*)(A + o_siglen);
+  uint32_t* msgoff = (uint32_t*)(A + o_msgoff);
+  uint32_t* msglen = (uint32_t*)(A + o_msglen);
+  uint32_t* pklen = (uint32_t*)(A + o_pklen);
+  uint64_t* rnd = (uint64_t*)(A + o_rnd);
+  siglen[0] = msgoff[0] = msglen[0] = pklen[0] = 0;
+  rnd[0] = 0;
+  in->pk_cnt.assign(n, 0);
+  in->sets_pks.assign(n, {});
   size_t mo = 0, po = 0;
-  uint64_t s = seed;
+  uint64_t sd = seed;
   FILE* ur = nullptr;
   if (scale && seed == 0) ur = fopen("/dev/urandom", "rb");
   for (size_t i = 0; i < n; i++) {
     const lsg_set* q = sets[i];
     siglen[i] = q->sig_len;
-    if ((q->sig_len == 96 || q->sig_len == 192) && q->sig) memcpy(&sig[192 * i], q->sig, q->sig_len);
+    if ((q->sig_len == 96 || q->sig_len == 192) && q->sig) memcpy(A + o_sig + 192 * i, q->sig, q->sig_len);
     msgoff[i] = (uint32_t)mo;
     msglen[i] = q->msg_len;
-    if (q->msg_len) memcpy(&msg[mo], q->msg, q->msg_len);
+    if (q->msg_len) memcpy(A + o_msg + mo, q->msg, q->msg_len);
     mo += q->msg_len;
-    c->pk_off[i] = (uint32_t)po;
-    c->pk_cnt[i] = q->n_pks;
+    in->pk_cnt[i] = q->n_pks;
+    // a set without keys points at pk 0 and is reported as an empty aggregate
     for (uint32_t k = 0; k < q->n_pks; k++) {
       pklen[po] = q->pk_len;
-      if (q->pk_len == 48 || q->pk_len == 96) memcpy(&pk[96 * po], q->pks + (size_t)q->pk_len * k, q->pk_len);
+      if (q->pk_len == 48 || q->pk_len == 96) memcpy(A + o_pk + 96 * po, q->pks + (size_t)q->pk_len * k, q->pk_len);
+      in->sets_pks[i].push_back((int32_t)po);
       po++;
     }
+    if (in->sets_pks[i].empty()) in->sets_pks[i].push_back(0);
     uint64_t r = 0;
     if (scale) {
       do {
         if (ur) {
-          if (fread(&r, 8, 1, ur) != 1) r = splitmix64(s) ^ now_ns();
+          if (fread(&r, 8, 1, ur) != 1) r = splitmix64(sd) ^ now_ns();
         } else {
-          r = splitmix64(s);
+          r = splitmix64(sd);
         }
       } while (r == 0);
     }
     rnd[i] = r;
   }
   if (ur) fclose(ur);
-  // per-set pubkey index lists for the aggregation tree (a set without keys points at
-  // pk 0 and is reported as an empty aggregate by read_status)
-  c->sets_pks.assign(n, {});
-  for (size_t i = 0; i < n; i++) {
-    for (uint32_t k = 0; k < c->pk_cnt[i]; k++) c->sets_pks[i].push_back((int32_t)(c->pk_off[i] + k));
-    if (c->sets_pks[i].empty()) c->sets_pks[i].push_back(0);
-  }
-  int rc;
-  if ((rc = ensure(c, c->d_sig, sig.size())) || (rc = ensure(c, c->d_siglen, 4 * nn)) ||
-      (rc = ensure(c, c->d_msg, msg.size())) || (rc = ensure(c, c->d_msgoff, 4 * nn)) ||
-      (rc = ensure(c, c->d_msglen, 4 * nn)) || (rc = ensure(c, c->d_pk, pk.size())) ||
-      (rc = ensure(c, c->d_pklen, 4 * np)) || (rc = ensure(c, c->d_rnd, 8 * nn)) || (rc = ensure(c, c->d_dst, 256)) ||
-      (rc = ensure(c, c->d_ub, 256 * nn)) || (rc = ensure(c, c->d_sigaff, 4 * W_G2A * nn)) ||
-      (rc = ensure(c, c->d_siginf, nn)) || (rc = ensure(c, c->d_seterr, 4 * nn)) ||
-      (rc = ensure(c, c->d_pkp, 4 * W_G1P * np)) || (rc = ensure(c, c->d_pkerr, 4 * np)) ||
-      (rc = ensure(c, c->d_agg, 4 * W_G1P * nn)) || (rc = ensure(c, c->d_P, 4 * W_G1A * nn)) ||
-      (rc = ensure(c, c->d_pinf, nn)) || (rc = ensure(c, c->d_H, 4 * W_G2A * nn)) || (rc = ensure(c, c->d_hinf, nn)) ||
-      (rc = ensure(c, c->d_rs, 4 * W_G2P * nn)))
+  if ((rc = ensure(s, in->d_sig, 192 * nn)) || (rc = ensure(s, in->d_siglen, 4 * nn)) ||
+      (rc = ensure(s, in->d_msg, std::max(msg_total, (size_t)1))) || (rc = ensure(s, in->d_msgoff, 4 * nn)) ||
+      (rc = ensure(s, in->d_msglen, 4 * nn)) || (rc = ensure(s, in->d_pk, 96 * np)) ||
+      (rc = ensure(s, in->d_pklen, 4 * np)) || (rc = ensure(s, in->d_rnd, 8 * nn)))
     return rc;
-  hipStream_t S = c->st[0];
-  LSG_HIP(c, hipMemcpyAsync(c->d_sig.p, sig.data(), sig.size(), hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_siglen.p, siglen.data(), 4 * nn, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_msg.p, msg.data(), msg.size(), hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_msgoff.p, msgoff.data(), 4 * nn, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_msglen.p, msglen.data(), 4 * nn, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_pk.p, pk.data(), pk.size(), hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_pklen.p, pklen.data(), 4 * np, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_rnd.p, rnd.data(), 8 * nn, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice, S));
-  LSG_HIP(c, hipStreamSynchronize(S));  // host vectors die at return; other streams see the data
+  struct {
+    DevBuf* d;
+    size_t off, len;
+  } cp[] = {{&in->d_sig, o_sig, 192 * nn},      {&in->d_siglen, o_siglen, 4 * nn}, {&in->d_msg, o_msg, std::max(msg_total, (size_t)1)},
+            {&in->d_msgoff, o_msgoff, 4 * nn}, {&in->d_msglen, o_msglen, 4 * nn}, {&in->d_pk, o_pk, 96 * np},
+            {&in->d_pklen, o_pklen, 4 * np},   {&in->d_rnd, o_rnd, 8 * nn}};
+  for (auto& x : cp) LSG_HIP(s, hipMemcpyAsync(x.d->p, A + x.off, x.len, hipMemcpyHostToDevice, stream));
+  return LSG_OK;
+}
+
+// per-set device state for the slot's current package
+int size_state(Slot* s, size_t groups) {
+  const lsg_staged* in = s->in;
+  size_t nn = std::max(in->n_sets, (size_t)1), np = std::max(in->n_pks, (size_t)1);
+  int rc;
+  if ((rc = ensure(s, s->d_ub, 256 * nn)) || (rc = ensure(s, s->d_sigaff, 4 * W_G2A * nn)) ||
+      (rc = ensure(s, s->d_siginf, nn)) || (rc = ensure(s, s->d_seterr, 4 * nn)) ||
+      (rc = ensure(s, s->d_pkp, 4 * W_G1P * np)) || (rc = ensure(s, s->d_pkerr, 4 * np)) ||
+      (rc = ensure(s, s->d_agg, 4 * W_G1P * nn)) || (rc = ensure(s, s->d_P, 4 * W_G1A * nn)) ||
+      (rc = ensure(s, s->d_pinf, nn)) || (rc = ensure(s, s->d_H, 4 * W_G2A * nn)) || (rc = ensure(s, s->d_hinf, nn)) ||
+      (rc = ensure(s, s->d_rs, 4 * W_G2P * nn)) || (rc = ensure(s, s->d_fall, 4 * W_F12 * (nn + groups))) ||
+      (rc = ensure(s, s->d_S, 4 * W_G2P * std::max(groups, (size_t)1))) ||
+      (rc = ensure(s, s->d_F, 4 * W_F12 * std::max(groups, (size_t)1))) ||
+      (rc = ensure(s, s->d_verdict, 4 * std::max(groups, (size_t)1))) || (rc = ensure(s, s->d_blob, 576)) ||
+      (rc = ensure_host(s, s->h_err, 4 * nn)) || (rc = ensure_host(s, s->h_pinf, nn)) ||
+      (rc = ensure_host(s, s->h_pkerr, 4 * np)) || (rc = ensure_host(s, s->h_verdict, 4 * std::max(groups, (size_t)1))) ||
+      (rc = ensure_host(s, s->h_blob, 576)))
+    return rc;
   return LSG_OK;
 }
 
 // Segmented pairwise reduction of lane-form values on the current stream: for each group,
 // combine the slots groups[g] of `src` (OP 0: G1 add, 1: G2 add, 2: Fp12 mul) into dense
 // out[g].  All levels' index pairs are built on the host and uploaded once; each level is
-// one launch over all pairs of all groups.  `slot` selects private scratch so that trees on
+// one launch over all pairs of all groups.  `ts` selects private scratch so that trees on
 // different streams can run concurrently.
 template <int OP>
-int tree_reduce(lsg_ctx* c, int slot, const char* name, const uint32_t* src,
+int tree_reduce(Slot* s, int ts, const char* name, const uint32_t* src,
                 const std::vector<std::vector<int32_t>>& groups, uint32_t* out) {
   size_t ng = groups.size();
   if (ng == 0) return LSG_OK;
-  TreeSlot& T = c->tree[slot];
+  TreeSlot& T = s->tree[ts];
   size_t W = OP == 0 ? W_G1P : (OP == 1 ? W_G2P : W_F12);
   std::vector<std::vector<int32_t>> cur = groups;
   std::vector<int32_t>& idx = T.host;
@@ -607,10 +776,10 @@ int tree_reduce(lsg_ctx* c, int slot, const char* name, const uint32_t* src,
     cur.swap(nxt);
   }
   int rc;
-  if ((rc = ensure(c, T.idx, 4 * idx.size())) || (rc = ensure(c, T.tA, 4 * W * max_level)) ||
-      (rc = ensure(c, T.tB, 4 * W * max_level)))
+  if ((rc = ensure(s, T.idx, 4 * idx.size())) || (rc = ensure(s, T.tA, 4 * W * max_level)) ||
+      (rc = ensure(s, T.tB, 4 * W * max_level)))
     return rc;
-  LSG_HIP(c, hipMemcpyAsync(T.idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, S_(c)));
+  LSG_HIP(s, hipMemcpyAsync(T.idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, S_(s)));
   const uint32_t* in = src;
   uint32_t* bufs[2] = {P_<uint32_t>(T.tA), P_<uint32_t>(T.tB)};
   for (size_t L = 0; L < levels.size(); L++) {
@@ -618,129 +787,113 @@ int tree_reduce(lsg_ctx* c, int slot, const char* name, const uint32_t* src,
     bool last = L + 1 == levels.size();
     uint32_t* dst = last ? out : bufs[L & 1];
     const int32_t* ia = P_<int32_t>(T.idx) + off;
-    LAUNCH_T(c, name, k_tree_level<OP>, lane_blocks(cnt), LSG_TPB, (int)cnt, ia, ia + cnt, in, dst);
+    LAUNCH_T(s, name, k_tree_level<OP>, lane_blocks(cnt), LSG_TPB, (int)cnt, ia, ia + cnt, in, dst);
     in = dst;
   }
   return LSG_OK;
 }
 
-// Per-set stages on three streams (no host synchronisation):
-//   S1: pubkeys -> aggregation tree -> [r_i] scaling            (event ev_pk)
-//   S2: signature decode -> subgroup check (event ev_sig) -> [r_i] scaling
-//   S0: expand_message -> hash_to_G2 -> wait ev_pk -> Miller loops f_i
-// f_i is written to d_fall[0..n); the caller sized d_fall for n + groups slots.
-int launch_set_stages(lsg_ctx* c) {
-  int n = (int)c->n_sets, np = (int)c->n_pks;
+// Per-set stages (no host synchronisation):
+//   side: pubkeys -> aggregation tree -> [r_i] scaling -> signature decode -> subgroup
+//         check (event ev_sig) -> [r_i] sig_i
+//   main: expand_message -> hash_to_G2 -> wait ev_sig -> Miller loops f_i
+// f_i is written to d_fall[0..n); size_state reserved n + groups slots.
+int launch_set_stages(Slot* s) {
+  const lsg_staged* in = s->in;
+  int n = (int)in->n_sets, np = (int)in->n_pks;
   if (n == 0) return LSG_OK;
-  // S1: pubkeys
-  c->cur = 1;
+  LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
+  s->cur = 1;
+  LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
   if (np > 0) {
-    LAUNCH(c, k_pk_decode, np, np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<uint32_t>(c->d_pkp),
-           P_<int32_t>(c->d_pkerr));
-    int rc = tree_reduce<0>(c, 1, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), c->sets_pks, P_<uint32_t>(c->d_agg));
+    LAUNCH(s, k_pk_decode, np, np, P_<uint8_t>(in->d_pk), P_<uint32_t>(in->d_pklen), P_<uint32_t>(s->d_pkp),
+           P_<int32_t>(s->d_pkerr));
+    int rc = tree_reduce<0>(s, 1, "tree_g1_aggregate", P_<uint32_t>(s->d_pkp), in->sets_pks, P_<uint32_t>(s->d_agg));
     if (rc) return rc;
   }
-  LAUNCH(c, k_pk_scale, n, n, P_<uint32_t>(c->d_agg), P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_P),
-         P_<uint8_t>(c->d_pinf));
-  LSG_HIP(c, hipEventRecord(c->ev_pk, c->st[1]));
-  // S2: signatures
-  c->cur = 2;
-  LAUNCH(c, k_sig_decode, n, n, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
-         P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LAUNCH(c, k_sig_subgroup, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LSG_HIP(c, hipEventRecord(c->ev_sig, c->st[2]));  // signature errors known
-  LAUNCH(c, k_sig_scale, n, n, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr),
-         P_<uint64_t>(c->d_rnd), P_<uint32_t>(c->d_rs));
-  // S0: messages, then the per-set Miller loops once pubkeys are scaled and signature
-  // errors are known (k_miller_sets reads d_seterr)
-  c->cur = 0;
-  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
-           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), DST_POP_LEN, P_<uint8_t>(c->d_ub));
-  LAUNCH(c, k_hash_map, n, n, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
-  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_pk, 0));
-  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_sig, 0));
-  LAUNCH(c, k_miller_sets, n, n, P_<uint32_t>(c->d_P), P_<uint8_t>(c->d_pinf), P_<uint32_t>(c->d_H),
-         P_<uint8_t>(c->d_hinf), P_<int32_t>(c->d_seterr), P_<uint32_t>(c->d_fall));
+  LAUNCH(s, k_pk_scale, n, n, P_<uint32_t>(s->d_agg), P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_P),
+         P_<uint8_t>(s->d_pinf));
+  LAUNCH(s, k_sig_decode, n, n, P_<uint8_t>(in->d_sig), P_<uint32_t>(in->d_siglen), P_<uint32_t>(s->d_sigaff),
+         P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
+  LAUNCH(s, k_sig_subgroup, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
+  LSG_HIP(s, hipEventRecord(s->ev_sig, s->st[1]));  // pubkeys scaled, signature errors known
+  LAUNCH(s, k_sig_scale, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr),
+         P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_rs));
+  s->cur = 0;
+  LAUNCH_T(s, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(in->d_msg), P_<uint32_t>(in->d_msgoff),
+           P_<uint32_t>(in->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN, P_<uint8_t>(s->d_ub));
+  LAUNCH(s, k_hash_map, n, n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf));
+  LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
+  LAUNCH(s, k_miller_sets, n, n, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf), P_<uint32_t>(s->d_H),
+         P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_fall));
   return LSG_OK;
 }
 
-int size_miller_slots(lsg_ctx* c, size_t groups) {
-  return ensure(c, c->d_fall, 4 * W_F12 * std::max(c->n_sets + groups, (size_t)1));
-}
-
-// Group stages (no host synchronisation): S2 sums [r_i] sig_i per group and runs the
-// signature Miller loop; S0 multiplies each group's f_i with it and, if fe, runs the final
-// exponentiation into d_verdict (else leaves the products in d_F).  Sets with errors
-// contribute identities (f_i = 1, [r_i] sig_i = O), so groups may include them.
-int launch_groups(lsg_ctx* c, const std::vector<std::vector<int32_t>>& groups, bool fe) {
+// Group stages (no host synchronisation): the side stream sums [r_i] sig_i per group and
+// runs the signature Miller loop; the main stream multiplies each group's f_i with it and,
+// if fe, runs the final exponentiation into d_verdict (else leaves the products in d_F).
+// Sets with errors contribute identities (f_i = 1, [r_i] sig_i = O), so groups may contain
+// them; the host discards such groups' verdicts.
+int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool fe) {
   size_t ng = groups.size();
   if (ng == 0) return LSG_OK;
-  size_t n = c->n_sets;
-  int rc;
-  if (c->d_fall.cap < 4 * W_F12 * (n + ng)) {
-    c->err = "internal: Miller slot array too small";
+  size_t n = s->in->n_sets;
+  if (s->d_fall.cap < 4 * W_F12 * (n + ng) || s->d_S.cap < 4 * W_G2P * ng || s->d_F.cap < 4 * W_F12 * ng ||
+      s->d_verdict.cap < 4 * ng) {
+    s->c->err = "internal: group buffers too small";
     return LSG_ERR_INVALID_ARG;
   }
-  if ((rc = ensure(c, c->d_S, 4 * W_G2P * ng)) || (rc = ensure(c, c->d_F, 4 * W_F12 * ng)) ||
-      (rc = ensure(c, c->d_verdict, 4 * ng)))
-    return rc;
-  c->cur = 2;
-  if ((rc = tree_reduce<1>(c, 2, "tree_g2_sigsum", P_<uint32_t>(c->d_rs), groups, P_<uint32_t>(c->d_S)))) return rc;
-  LAUNCH(c, k_miller_groups, ng, (int)ng, P_<uint32_t>(c->d_S), n, P_<uint32_t>(c->d_fall));
-  LSG_HIP(c, hipEventRecord(c->ev_grp, c->st[2]));
-  c->cur = 0;
-  LSG_HIP(c, hipStreamWaitEvent(c->st[0], c->ev_grp, 0));
+  s->cur = 1;
+  int rc;
+  if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) return rc;
+  LAUNCH(s, k_miller_groups, ng, (int)ng, P_<uint32_t>(s->d_S), n, P_<uint32_t>(s->d_fall));
+  LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
+  s->cur = 0;
+  LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_grp, 0));
   std::vector<std::vector<int32_t>> fg = groups;
   for (size_t g = 0; g < ng; g++) fg[g].push_back((int32_t)(n + g));
-  if ((rc = tree_reduce<2>(c, 0, "tree_fp12_product", P_<uint32_t>(c->d_fall), fg, P_<uint32_t>(c->d_F)))) return rc;
-  if (fe) LAUNCH(c, k_final_exp_check, ng, (int)ng, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
+  if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_fall), fg, P_<uint32_t>(s->d_F)))) return rc;
+  if (fe) LAUNCH(s, k_final_exp_check, ng, (int)ng, P_<uint32_t>(s->d_F), P_<int32_t>(s->d_verdict));
+  return LSG_OK;
+}
+
+// enqueue D2H copies of per-set status (and ng verdicts) into the pinned mirrors, then
+// record ev_done on the main stream (which has joined the side stream through events)
+int launch_readback(Slot* s, bool status, size_t ng) {
+  hipStream_t S = s->st[0];
+  size_t n = s->in->n_sets, np = s->in->n_pks;
+  if (s->own_streams) {  // join the side stream even when no group was launched
+    LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
+    LSG_HIP(s, hipStreamWaitEvent(S, s->ev_grp, 0));
+  }
+  if (status) {
+    if (n) {
+      LSG_HIP(s, hipMemcpyAsync(s->h_err.p, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, S));
+      LSG_HIP(s, hipMemcpyAsync(s->h_pinf.p, s->d_pinf.p, n, hipMemcpyDeviceToHost, S));
+    }
+    if (np) LSG_HIP(s, hipMemcpyAsync(s->h_pkerr.p, s->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
+  }
+  s->n_verdicts = ng;
+  if (ng) LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
+  LSG_HIP(s, hipEventRecord(s->ev_done, S));
   return LSG_OK;
 }
 
 struct SetStatus {
-  std::vector<int32_t> err;    // per set: BLST code (0 ok)
+  const int32_t* err;    // per set: BLST code (0 ok)
   std::vector<uint8_t> pinf;   // per set: aggregated pk is infinity (2: no keys at all)
-  std::vector<int32_t> pkerr;  // per pubkey
+  const int32_t* pkerr;  // per pubkey
 };
 
-// Copies per-set status (and optionally ng verdicts) to the host on S0 and waits for all
-// streams; S0 has already waited on S1/S2 through events.
-int finish(lsg_ctx* c, SetStatus* ss, std::vector<int32_t>* verdict, size_t ng) {
-  size_t n = c->n_sets, np = c->n_pks;
-  hipStream_t S = c->st[0];
-  if (ss) {
-    ss->err.assign(n, 0);
-    ss->pinf.assign(n, 0);
-    ss->pkerr.assign(np, 0);
-    if (n) {
-      LSG_HIP(c, hipMemcpyAsync(ss->err.data(), c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, S));
-      LSG_HIP(c, hipMemcpyAsync(ss->pinf.data(), c->d_pinf.p, n, hipMemcpyDeviceToHost, S));
-    }
-    if (np) LSG_HIP(c, hipMemcpyAsync(ss->pkerr.data(), c->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
-  }
-  if (verdict) {
-    verdict->assign(ng, 0);
-    if (ng) LSG_HIP(c, hipMemcpyAsync(verdict->data(), c->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
-  }
-  int rc = sync_all(c);
-  if (rc) return rc;
-  if (ss)
-    for (size_t i = 0; i < n; i++)
-      if (c->pk_cnt[i] == 0) ss->pinf[i] = 2;  // PublicKey.aggregate([]) throws
-  return LSG_OK;
-}
-
-// chunkifyMaximizeChunkSize (multithread/utils.ts:4-19)
-std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk) {
-  std::vector<std::pair<size_t, size_t>> out;
-  size_t chunk_count = len / min_per_chunk;
-  if (chunk_count <= 1) {
-    out.push_back({0, len});
-    return out;
-  }
-  size_t per = (len + chunk_count - 1) / chunk_count;
-  for (size_t i = 0; i < len; i += per) out.push_back({i, std::min(len, i + per)});
-  return out;
+SetStatus read_status(Slot* s) {
+  SetStatus ss;
+  size_t n = s->in->n_sets;
+  ss.err = H_<int32_t>(s->h_err);
+  ss.pkerr = H_<int32_t>(s->h_pkerr);
+  ss.pinf.assign(H_<uint8_t>(s->h_pinf), H_<uint8_t>(s->h_pinf) + n);
+  for (size_t i = 0; i < n; i++)
+    if (s->in->pk_cnt[i] == 0) ss.pinf[i] = 2;  // PublicKey.aggregate([]) throws
+  return ss;
 }
 
 int32_t set_error(const SetStatus& ss, size_t s) {
@@ -761,9 +914,274 @@ int32_t job_error(const SetStatus& ss, size_t first, size_t count) {
   return 0;
 }
 
+Slot* free_slot(lsg_ctx* c, Slot* pool, int n) {
+  for (int i = 0; i < n; i++)
+    if (pool[i].kind == SLOT_FREE) return &pool[i];
+  return nullptr;
+}
+
+uint64_t make_ticket(lsg_ctx* c, Slot* s, int kind) {
+  s->kind = kind;
+  s->serial = c->next_serial++;
+  return (s->serial << 8) | ((uint64_t)kind << 4) | (uint64_t)s->index;
+}
+
+Slot* ticket_slot(lsg_ctx* c, uint64_t t, int kind) {
+  int k = (int)((t >> 4) & 15), i = (int)(t & 15);
+  if (k != kind) return nullptr;
+  Slot* s = nullptr;
+  if (kind == SLOT_FINAL) {
+    if (i < LSG_FINALS) s = &c->finals[i];
+  } else if (i < LSG_SLOTS) {
+    s = &c->slots[i];
+  }
+  if (!s || s->kind != kind || s->serial != (t >> 8)) return nullptr;
+  return s;
+}
+
+void release(lsg_ctx* c, Slot* s) {
+  s->kind = SLOT_FREE;
+  c->last = s;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- C ABI
+namespace {
+
+void sync_slot(Slot* s) {
+  for (int k = 0; k < 2; k++)
+    if (s->st[k]) (void)hipStreamSynchronize(s->st[k]);
+}
+
+// Phase A of verifyManySignatureSets, launched speculatively: every batchable chunk and
+// every non-batchable job gets its group (sum of [r_i] sig_i, Miller product, final
+// exponentiation) before the per-set status is known, so a package costs one host
+// synchronisation.  The wait applies the reference's verdict rules (worker.ts:51-96).
+int submit_jobs(lsg_ctx* c, Slot* s, const lsg_job* jobs, size_t n_jobs, uint64_t seed) {
+  JobsPlan& P = s->plan;
+  P = JobsPlan();
+  memset(&P.stats, 0, sizeof(P.stats));
+  P.stats.start_ns = now_ns();
+  timer_reset(s);
+  std::vector<const lsg_set*> flat;
+  P.jfirst.resize(n_jobs);
+  P.jcount.resize(n_jobs);
+  for (size_t j = 0; j < n_jobs; j++) {
+    P.jfirst[j] = flat.size();
+    P.jcount[j] = jobs[j].n_sets;
+    for (uint32_t k = 0; k < jobs[j].n_sets; k++) flat.push_back(&jobs[j].sets[k]);
+  }
+  P.results.assign(n_jobs, {LSG_INVALID, 0});
+  std::vector<size_t> batchable, nonbatch;
+  for (size_t j = 0; j < n_jobs; j++) (jobs[j].flags & LSG_JOB_BATCHABLE ? batchable : nonbatch).push_back(j);
+  auto job_group = [&](size_t j) {
+    std::vector<int32_t> m;
+    for (size_t k = 0; k < P.jcount[j]; k++) m.push_back((int32_t)(P.jfirst[j] + k));
+    return m;
+  };
+  // batchable chunks (worker.ts:51-86) + non-batchable jobs (worker.ts:88-96)
+  if (!batchable.empty()) {
+    for (auto ch : chunkify(batchable.size(), 16)) {
+      std::vector<int32_t> m;
+      std::vector<size_t> js;
+      for (size_t q = ch.first; q < ch.second; q++) {
+        size_t j = batchable[q];
+        js.push_back(j);
+        std::vector<int32_t> jm = job_group(j);
+        m.insert(m.end(), jm.begin(), jm.end());
+      }
+      if (m.empty()) {
+        P.empty_chunks.push_back(js);
+        continue;
+      }
+      P.groups.push_back(m);
+      P.group_jobs.push_back(js);
+      P.group_is_chunk.push_back(true);
+    }
+  }
+  for (size_t j : nonbatch) {
+    if (P.jcount[j] == 0) {
+      P.results[j] = {LSG_ERROR, LSG_ERR_EMPTY_SET};
+      continue;
+    }
+    P.groups.push_back(job_group(j));
+    P.group_jobs.push_back({j});
+    P.group_is_chunk.push_back(false);
+  }
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, flat.data(), flat.size(), seed, true, s->st[0]))) return rc;
+  if ((rc = size_state(s, std::max(P.groups.size(), n_jobs)))) return rc;
+  if ((rc = launch_set_stages(s))) return rc;
+  if ((rc = launch_groups(s, P.groups, true))) return rc;
+  return launch_readback(s, true, P.groups.size());
+}
+
+int wait_jobs(lsg_ctx* c, Slot* s, lsg_job_result* results, lsg_stats* stats) {
+  JobsPlan& P = s->plan;
+  LSG_HIP(s, hipEventSynchronize(s->ev_done));
+  size_t n_jobs = P.results.size();
+  SetStatus ss = read_status(s);
+  std::vector<int32_t> verdict(H_<int32_t>(s->h_verdict), H_<int32_t>(s->h_verdict) + P.groups.size());
+  P.stats.n_final_exps += (uint32_t)P.groups.size();
+  // worker.ts:108-114: deserializeSet runs before anything else; a bad pubkey throws
+  // out of verifyManySignatureSets and rejects every job of the package.
+  int32_t pkfail = 0;
+  for (size_t k = 0; k < s->in->n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
+  if (pkfail) {
+    for (size_t j = 0; j < n_jobs; j++) P.results[j] = {LSG_ERROR, pkfail};
+  } else {
+    std::vector<size_t> retry;
+    for (auto& js : P.empty_chunks) {
+      P.stats.batch_retries++;
+      retry.insert(retry.end(), js.begin(), js.end());
+    }
+    for (size_t g = 0; g < P.groups.size(); g++) {
+      if (P.group_is_chunk[g]) {
+        bool throws = false;
+        for (int32_t x : P.groups[g])
+          if (set_error(ss, (size_t)x)) throws = true;
+        if (!throws && verdict[g]) {
+          for (size_t j : P.group_jobs[g]) {
+            P.results[j] = {LSG_VALID, 0};
+            P.stats.batch_sigs_success += (uint32_t)P.jcount[j];
+          }
+        } else {
+          P.stats.batch_retries++;
+          retry.insert(retry.end(), P.group_jobs[g].begin(), P.group_jobs[g].end());
+        }
+      } else {
+        size_t j = P.group_jobs[g][0];
+        int32_t e = job_error(ss, P.jfirst[j], P.jcount[j]);
+        P.results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{verdict[g] ? LSG_VALID : LSG_INVALID, 0};
+      }
+    }
+    // Phase B: per-job retry of failed chunks (worker.ts:74-96) on the resident per-set state
+    if (!retry.empty()) {
+      std::vector<std::vector<int32_t>> g2;
+      std::vector<size_t> g2job;
+      for (size_t j : retry) {
+        int32_t e = job_error(ss, P.jfirst[j], P.jcount[j]);
+        if (e) {
+          P.results[j] = {LSG_ERROR, e};
+        } else {
+          std::vector<int32_t> m;
+          for (size_t k = 0; k < P.jcount[j]; k++) m.push_back((int32_t)(P.jfirst[j] + k));
+          g2.push_back(m);
+          g2job.push_back(j);
+        }
+      }
+      int rc;
+      if ((rc = launch_groups(s, g2, true))) return rc;
+      if ((rc = launch_readback(s, false, g2.size()))) return rc;
+      LSG_HIP(s, hipEventSynchronize(s->ev_done));
+      P.stats.n_final_exps += (uint32_t)g2.size();
+      const int32_t* v2 = H_<int32_t>(s->h_verdict);
+      for (size_t g = 0; g < g2.size(); g++) P.results[g2job[g]] = {v2[g] ? LSG_VALID : LSG_INVALID, 0};
+    }
+  }
+  for (size_t j = 0; j < n_jobs; j++) results[j] = P.results[j];
+  P.stats.end_ns = now_ns();
+  if (stats) *stats = P.stats;
+  return LSG_OK;
+}
+
+// per-shard Miller product over the slot's inputs (errored sets contribute identities, so
+// the partial covers exactly the valid sets; an empty package gives the identity)
+int submit_batch(Slot* s) {
+  int rc;
+  if ((rc = size_state(s, 1))) return rc;
+  if ((rc = launch_set_stages(s))) return rc;
+  std::vector<std::vector<int32_t>> groups(1);
+  for (size_t i = 0; i < s->in->n_sets; i++) groups[0].push_back((int32_t)i);
+  if ((rc = launch_groups(s, groups, false))) return rc;
+  LAUNCH(s, k_fp12_to_canon, 1, 1, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(s->h_blob.p, s->d_blob.p, 576, hipMemcpyDeviceToHost, s->st[0]));
+  return launch_readback(s, true, 0);
+}
+
+int wait_batch(Slot* s, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
+  LSG_HIP(s, hipEventSynchronize(s->ev_done));
+  memcpy(out576, s->h_blob.p, 576);
+  SetStatus ss = read_status(s);
+  *any_error = 0;
+  for (size_t i = 0; i < s->in->n_sets; i++) {
+    int32_t e = set_error(ss, i);
+    if (set_err) set_err[i] = e;
+    if (e) *any_error = 1;
+  }
+  for (size_t k = 0; k < s->in->n_pks; k++)
+    if (ss.pkerr[k]) *any_error = 1;
+  return LSG_OK;
+}
+
+int submit_final(Slot* s, const uint8_t* partials576, size_t n) {
+  timer_reset(s);
+  s->n_verdicts = 0;
+  int rc;
+  size_t np = std::max(n, (size_t)1);
+  if ((rc = ensure_host(s, s->h_blob, 576 * np)) || (rc = ensure(s, s->d_blob, 576 * np)) ||
+      (rc = ensure(s, s->d_aux, 4 * W_F12 * np)) || (rc = ensure(s, s->d_F, 4 * W_F12)) ||
+      (rc = ensure(s, s->d_verdict, 4)) || (rc = ensure_host(s, s->h_verdict, 4)))
+    return rc;
+  if (n) {
+    hipStream_t S = s->st[0];
+    memcpy(s->h_blob.p, partials576, 576 * n);
+    LSG_HIP(s, hipMemcpyAsync(s->d_blob.p, s->h_blob.p, 576 * n, hipMemcpyHostToDevice, S));
+    LAUNCH(s, k_blobs_to_fp12, n, (int)n, P_<uint8_t>(s->d_blob), P_<uint32_t>(s->d_aux));
+    std::vector<std::vector<int32_t>> g(1);
+    for (size_t k = 0; k < n; k++) g[0].push_back((int32_t)k);
+    if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_aux), g, P_<uint32_t>(s->d_F)))) return rc;
+    LAUNCH(s, k_final_exp_check, 1, 1, P_<uint32_t>(s->d_F), P_<int32_t>(s->d_verdict));
+    LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4, hipMemcpyDeviceToHost, S));
+    s->n_verdicts = 1;
+  }
+  LSG_HIP(s, hipEventRecord(s->ev_done, s->st[0]));
+  return LSG_OK;
+}
+
+int wait_final(Slot* s, int32_t* valid) {
+  LSG_HIP(s, hipEventSynchronize(s->ev_done));
+  *valid = s->n_verdicts ? H_<int32_t>(s->h_verdict)[0] : 0;
+  return LSG_OK;
+}
+
+Slot* take_slot(lsg_ctx* c) {
+  Slot* s = free_slot(c, c->slots, LSG_SLOTS);
+  if (!s) c->err = "all pipeline slots are busy (wait on an outstanding ticket first)";
+  return s;
+}
+
+// stage + expand + hash on the utility slot (synchronous callers only)
+int util_hash(Slot* s, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst, uint32_t dst_len) {
+  std::vector<lsg_set> sets(n);
+  std::vector<const lsg_set*> sp(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&sets[i], 0, sizeof(lsg_set));
+    sets[i].msg = msgs + (size_t)msg_len * i;
+    sets[i].msg_len = msg_len;
+    sp[i] = &sets[i];
+  }
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, sp.data(), n, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, 0))) return rc;
+  LSG_HIP(s, hipMemcpyAsync(s->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, s->st[0]));
+  int nn = (int)n;
+  LAUNCH_T(s, "k_expand_msg", k_expand_msg, (nn + 63) / 64, 64, nn, P_<uint8_t>(s->own.d_msg),
+           P_<uint32_t>(s->own.d_msgoff), P_<uint32_t>(s->own.d_msglen), P_<uint8_t>(s->d_dst), dst_len,
+           P_<uint8_t>(s->d_ub));
+  LAUNCH(s, k_hash_map, nn, nn, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf));
+  return LSG_OK;
+}
+
+#define LSG_ENTER(c)                         \
+  std::lock_guard<std::mutex> _lk((c)->mu); \
+  LSG_HIPC((c), hipSetDevice((c)->device))
+
+}  // namespace
+
 extern "C" {
 
 int lsg_init(int device_ordinal, lsg_ctx** out) {
@@ -778,11 +1196,10 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LSG_ERR_NO_DEVICE;
   lsg_ctx* c = new lsg_ctx();
   c->device = dev;
-  bool ok = hipSetDevice(dev) == hipSuccess;
-  for (int k = 0; k < 3 && ok; k++) ok = hipStreamCreateWithFlags(&c->st[k], hipStreamNonBlocking) == hipSuccess;
-  hipEvent_t* evs[] = {&c->ev_pk, &c->ev_sig, &c->ev_grp};
-  for (hipEvent_t* e : evs)
-    if (ok) ok = hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&c->s_final, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < LSG_SLOTS && ok; i++) ok = slot_create(c, &c->slots[i], i, nullptr) == LSG_OK;
+  for (int i = 0; i < LSG_FINALS && ok; i++) ok = slot_create(c, &c->finals[i], i, c->s_final) == LSG_OK;
+  if (ok) ok = slot_create(c, &c->util, 0, c->s_final) == LSG_OK;
   if (!ok) {
     lsg_destroy(c);
     return LSG_ERR_DEVICE;
@@ -794,29 +1211,10 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
 int lsg_destroy(lsg_ctx* c) {
   if (!c) return LSG_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
-  for (int k = 0; k < 3; k++)
-    if (c->st[k]) (void)hipStreamSynchronize(c->st[k]);
-  DevBuf* bufs[] = {&c->d_sig,   &c->d_siglen, &c->d_msg,    &c->d_msgoff, &c->d_msglen, &c->d_pk,
-                    &c->d_pklen, &c->d_rnd,    &c->d_dst,    &c->d_ub,     &c->d_sigaff, &c->d_siginf,
-                    &c->d_seterr, &c->d_pkp,   &c->d_pkerr,  &c->d_agg,    &c->d_P,      &c->d_pinf,
-                    &c->d_H,     &c->d_hinf,   &c->d_rs,     &c->d_fall,   &c->d_S,      &c->d_F,
-                    &c->d_verdict, &c->d_blob, &c->d_aux};
-  for (DevBuf* b : bufs)
-    if (b->p) (void)hipFree(b->p);
-  for (TreeSlot& t : c->tree) {
-    DevBuf* tb[] = {&t.idx, &t.tA, &t.tB};
-    for (DevBuf* b : tb)
-      if (b->p) (void)hipFree(b->p);
-  }
-  for (Timer& t : c->timers) {
-    (void)hipEventDestroy(t.a);
-    (void)hipEventDestroy(t.b);
-  }
-  hipEvent_t evs[] = {c->ev_pk, c->ev_sig, c->ev_grp};
-  for (hipEvent_t e : evs)
-    if (e) (void)hipEventDestroy(e);
-  for (int k = 0; k < 3; k++)
-    if (c->st[k]) (void)hipStreamDestroy(c->st[k]);
+  for (Slot& s : c->slots) slot_destroy(&s);
+  for (Slot& s : c->finals) slot_destroy(&s);
+  slot_destroy(&c->util);
+  if (c->s_final) (void)hipStreamDestroy(c->s_final);
   delete c;
   return LSG_OK;
 }
@@ -831,133 +1229,38 @@ int lsg_device_name(lsg_ctx* c, char* buf, size_t len) {
   return LSG_OK;
 }
 
-// Phase A is launched speculatively: every batchable chunk and every non-batchable job gets
-// its group (sum of [r_i] sig_i, Miller product, final exponentiation) before the per-set
-// status is known, so the whole package costs one host synchronisation.  Sets that fail
-// to decode contribute identities; the host then discards the verdicts of groups that the
-// reference would have thrown on (worker.ts:51-96) and re-runs those jobs one by one.
+int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_jobs && !jobs)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = take_slot(c);
+  if (!s) return LSG_ERR_BUSY;
+  int rc = submit_jobs(c, s, jobs, n_jobs, seed);
+  if (rc) {
+    sync_slot(s);
+    return rc;
+  }
+  *ticket = make_ticket(c, s, SLOT_JOBS);
+  return LSG_OK;
+}
+
+int lsg_wait_jobs(lsg_ctx* c, lsg_ticket ticket, lsg_job_result* results, lsg_stats* stats) {
+  if (!c) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = ticket_slot(c, ticket, SLOT_JOBS);
+  if (!s || (s->plan.results.size() && !results)) return LSG_ERR_INVALID_ARG;
+  int rc = wait_jobs(c, s, results, stats);
+  if (rc) sync_slot(s);
+  release(c, s);
+  return rc;
+}
+
 int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_job_result* results,
                     lsg_stats* stats) {
   if (!c || (n_jobs && (!jobs || !results))) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  lsg_stats stt;
-  memset(&stt, 0, sizeof(stt));
-  stt.start_ns = now_ns();
-  timer_reset(c);
-  std::vector<const lsg_set*> flat;
-  std::vector<size_t> jfirst(n_jobs), jcount(n_jobs);
-  for (size_t j = 0; j < n_jobs; j++) {
-    jfirst[j] = flat.size();
-    jcount[j] = jobs[j].n_sets;
-    for (uint32_t k = 0; k < jobs[j].n_sets; k++) flat.push_back(&jobs[j].sets[k]);
-  }
-  for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_INVALID, 0};
-  std::vector<size_t> batchable, nonbatch;
-  for (size_t j = 0; j < n_jobs; j++) (jobs[j].flags & LSG_JOB_BATCHABLE ? batchable : nonbatch).push_back(j);
-  auto job_group = [&](size_t j) {
-    std::vector<int32_t> m;
-    for (size_t k = 0; k < jcount[j]; k++) m.push_back((int32_t)(jfirst[j] + k));
-    return m;
-  };
-  // Phase A groups: batchable chunks (worker.ts:51-86) + non-batchable jobs (worker.ts:88-96)
-  std::vector<std::vector<int32_t>> groups;
-  std::vector<std::vector<size_t>> group_jobs;
-  std::vector<bool> group_is_chunk;
-  std::vector<std::vector<size_t>> empty_chunks;  // chunks without sets: always throw
-  if (!batchable.empty()) {
-    for (auto ch : chunkify(batchable.size(), 16)) {
-      std::vector<int32_t> m;
-      std::vector<size_t> js;
-      for (size_t q = ch.first; q < ch.second; q++) {
-        size_t j = batchable[q];
-        js.push_back(j);
-        std::vector<int32_t> jm = job_group(j);
-        m.insert(m.end(), jm.begin(), jm.end());
-      }
-      if (m.empty()) {
-        empty_chunks.push_back(js);
-        continue;
-      }
-      groups.push_back(m);
-      group_jobs.push_back(js);
-      group_is_chunk.push_back(true);
-    }
-  }
-  for (size_t j : nonbatch) {
-    if (jcount[j] == 0) {
-      results[j] = {LSG_ERROR, LSG_ERR_EMPTY_SET};
-      continue;
-    }
-    groups.push_back(job_group(j));
-    group_jobs.push_back({j});
-    group_is_chunk.push_back(false);
-  }
-  int rc = stage_sets(c, flat.data(), flat.size(), seed, true);
+  lsg_ticket t;
+  int rc = lsg_submit_jobs(c, jobs, n_jobs, seed, &t);
   if (rc) return rc;
-  if ((rc = size_miller_slots(c, std::max(groups.size(), n_jobs)))) return rc;
-  if ((rc = launch_set_stages(c))) return rc;
-  if ((rc = launch_groups(c, groups, true))) return rc;
-  SetStatus ss;
-  std::vector<int32_t> verdict;
-  if ((rc = finish(c, &ss, &verdict, groups.size()))) return rc;
-  stt.n_final_exps += (uint32_t)groups.size();
-  // worker.ts:108-114: deserializeSet runs before anything else; a bad pubkey throws
-  // out of verifyManySignatureSets and rejects every job of the package.
-  int32_t pkfail = 0;
-  for (size_t k = 0; k < c->n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
-  if (pkfail) {
-    for (size_t j = 0; j < n_jobs; j++) results[j] = {LSG_ERROR, pkfail};
-    stt.end_ns = now_ns();
-    if (stats) *stats = stt;
-    return LSG_OK;
-  }
-  std::vector<size_t> retry;
-  for (auto& js : empty_chunks) {
-    stt.batch_retries++;
-    retry.insert(retry.end(), js.begin(), js.end());
-  }
-  for (size_t g = 0; g < groups.size(); g++) {
-    if (group_is_chunk[g]) {
-      bool throws = false;
-      for (int32_t s : groups[g])
-        if (set_error(ss, (size_t)s)) throws = true;
-      if (!throws && verdict[g]) {
-        for (size_t j : group_jobs[g]) {
-          results[j] = {LSG_VALID, 0};
-          stt.batch_sigs_success += (uint32_t)jcount[j];
-        }
-      } else {
-        stt.batch_retries++;
-        retry.insert(retry.end(), group_jobs[g].begin(), group_jobs[g].end());
-      }
-    } else {
-      size_t j = group_jobs[g][0];
-      int32_t e = job_error(ss, jfirst[j], jcount[j]);
-      results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{verdict[g] ? LSG_VALID : LSG_INVALID, 0};
-    }
-  }
-  // Phase B: per-job retry of failed chunks (worker.ts:74-96)
-  if (!retry.empty()) {
-    std::vector<std::vector<int32_t>> g2;
-    std::vector<size_t> g2job;
-    for (size_t j : retry) {
-      int32_t e = job_error(ss, jfirst[j], jcount[j]);
-      if (e) {
-        results[j] = {LSG_ERROR, e};
-      } else {
-        g2.push_back(job_group(j));
-        g2job.push_back(j);
-      }
-    }
-    if ((rc = launch_groups(c, g2, true))) return rc;
-    if ((rc = finish(c, nullptr, &verdict, g2.size()))) return rc;
-    stt.n_final_exps += (uint32_t)g2.size();
-    for (size_t g = 0; g < g2.size(); g++) results[g2job[g]] = {verdict[g] ? LSG_VALID : LSG_INVALID, 0};
-  }
-  stt.end_ns = now_ns();
-  if (stats) *stats = stt;
-  return LSG_OK;
+  return lsg_wait_jobs(c, t, results, stats);
 }
 
 int lsg_verify_sets(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_job_result* result) {
@@ -969,37 +1272,170 @@ int lsg_verify_sets(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t see
   return lsg_verify_jobs(c, &job, 1, seed, result, nullptr);
 }
 
+int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
+  if (!c || !done) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = ticket_slot(c, ticket, (int)((ticket >> 4) & 15));
+  if (!s) return LSG_ERR_INVALID_ARG;
+  hipError_t e = hipEventQuery(s->ev_done);
+  if (e == hipErrorNotReady) {
+    *done = 0;
+    return LSG_OK;
+  }
+  if (e != hipSuccess) return fail(s, "hipEventQuery", e);
+  *done = 1;
+  return LSG_OK;
+}
+
+int lsg_stage(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_staged** out) {
+  if (!c || !out || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  *out = nullptr;
+  lsg_staged* in = new lsg_staged();
+  std::vector<const lsg_set*> sp(n_sets);
+  for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
+  Slot* u = &c->util;
+  int rc = stage_sets(u, in, sp.data(), n_sets, seed, true, u->st[0]);
+  if (!rc && hipStreamSynchronize(u->st[0]) != hipSuccess) rc = fail(u, "hipStreamSynchronize", hipGetLastError());
+  if (rc) {
+    staged_free(in);
+    delete in;
+    return rc;
+  }
+  *out = in;
+  return LSG_OK;
+}
+
+int lsg_staged_free(lsg_ctx* c, lsg_staged* staged) {
+  if (!c || !staged) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  for (Slot& s : c->slots)
+    if (s.kind != SLOT_FREE && s.in == staged) {
+      c->err = "staged package still in use by an outstanding ticket";
+      return LSG_ERR_BUSY;
+    }
+  staged_free(staged);
+  delete staged;
+  return LSG_OK;
+}
+
+int lsg_batch_submit(lsg_ctx* c, const lsg_staged* staged, lsg_ticket* ticket) {
+  if (!c || !staged || !ticket) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = take_slot(c);
+  if (!s) return LSG_ERR_BUSY;
+  timer_reset(s);
+  s->in = staged;
+  int rc = submit_batch(s);
+  if (rc) {
+    sync_slot(s);
+    return rc;
+  }
+  *ticket = make_ticket(c, s, SLOT_BATCH);
+  return LSG_OK;
+}
+
+int lsg_batch_wait(lsg_ctx* c, lsg_ticket ticket, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
+  if (!c || !out576 || !any_error) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = ticket_slot(c, ticket, SLOT_BATCH);
+  if (!s) return LSG_ERR_INVALID_ARG;
+  int rc = wait_batch(s, out576, set_err, any_error);
+  if (rc) sync_slot(s);
+  release(c, s);
+  return rc;
+}
+
+int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
+                      int32_t* set_err, int32_t* any_error) {
+  if (!c || !out576 || !any_error || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+  lsg_ticket t;
+  {
+    LSG_ENTER(c);
+    Slot* s = take_slot(c);
+    if (!s) return LSG_ERR_BUSY;
+    timer_reset(s);
+    std::vector<const lsg_set*> sp(n_sets);
+    for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
+    s->in = &s->own;
+    int rc = stage_sets(s, &s->own, sp.data(), n_sets, seed, true, s->st[0]);
+    if (!rc) rc = submit_batch(s);
+    if (rc) {
+      sync_slot(s);
+      return rc;
+    }
+    t = make_ticket(c, s, SLOT_BATCH);
+  }
+  return lsg_batch_wait(c, t, out576, set_err, any_error);
+}
+
+int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = free_slot(c, c->finals, LSG_FINALS);
+  if (!s) {
+    c->err = "all final-exponentiation entries are busy";
+    return LSG_ERR_BUSY;
+  }
+  int rc = submit_final(s, partials576, n_partials);
+  if (rc) {
+    sync_slot(s);
+    return rc;
+  }
+  *ticket = make_ticket(c, s, SLOT_FINAL);
+  return LSG_OK;
+}
+
+int lsg_final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) {
+  if (!c || !valid) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = ticket_slot(c, ticket, SLOT_FINAL);
+  if (!s) return LSG_ERR_INVALID_ARG;
+  int rc = wait_final(s, valid);
+  release(c, s);
+  return rc;
+}
+
+int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, int32_t* valid) {
+  if (!c || !valid || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+  lsg_ticket t;
+  int rc = lsg_final_submit(c, partials576, n_partials, &t);
+  if (rc) return rc;
+  return lsg_final_wait(c, t, valid);
+}
+
 int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96,
                           int32_t* err_code) {
   if (!c || !out96 || !err_code || (n && !pks)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  timer_reset(c);
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
   *err_code = 0;
   if (n == 0) {
     *err_code = LSG_ERR_EMPTY_AGGREGATE;
     return LSG_OK;
   }
-  lsg_set s;
-  memset(&s, 0, sizeof(s));
-  s.pks = pks;
-  s.pk_len = pk_len;
-  s.n_pks = (uint32_t)n;
-  const lsg_set* sp = &s;
-  int rc = stage_sets(c, &sp, 1, 0, false);
-  if (rc) return rc;
+  lsg_set q;
+  memset(&q, 0, sizeof(q));
+  q.pks = pks;
+  q.pk_len = pk_len;
+  q.n_pks = (uint32_t)n;
+  const lsg_set* qp = &q;
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, &qp, 1, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, 0))) return rc;
   int np = (int)n;
-  LAUNCH(c, k_pk_decode, np, np, P_<uint8_t>(c->d_pk), P_<uint32_t>(c->d_pklen), P_<uint32_t>(c->d_pkp),
-         P_<int32_t>(c->d_pkerr));
-  std::vector<std::vector<int32_t>> g(1);
-  for (int k = 0; k < np; k++) g[0].push_back(k);
-  if ((rc = tree_reduce<0>(c, 1, "tree_g1_aggregate", P_<uint32_t>(c->d_pkp), g, P_<uint32_t>(c->d_agg)))) return rc;
-  if ((rc = ensure(c, c->d_blob, 192))) return rc;
-  LAUNCH(c, k_g1p_to_bytes, 1, 1, P_<uint32_t>(c->d_agg), P_<uint8_t>(c->d_blob));
+  LAUNCH(s, k_pk_decode, np, np, P_<uint8_t>(s->own.d_pk), P_<uint32_t>(s->own.d_pklen), P_<uint32_t>(s->d_pkp),
+         P_<int32_t>(s->d_pkerr));
+  if ((rc = tree_reduce<0>(s, 1, "tree_g1_aggregate", P_<uint32_t>(s->d_pkp), s->own.sets_pks, P_<uint32_t>(s->d_agg))))
+    return rc;
+  LAUNCH(s, k_g1p_to_bytes, 1, 1, P_<uint32_t>(s->d_agg), P_<uint8_t>(s->d_blob));
   std::vector<int32_t> pkerr(n);
-  LSG_HIP(c, hipMemcpyAsync(pkerr.data(), c->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_blob.p, 96, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
   for (size_t k = 0; k < n; k++)
     if (pkerr[k]) {
       *err_code = pkerr[k];
@@ -1010,42 +1446,27 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
 
 int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst,
                    uint32_t dst_len, uint8_t* out192) {
-  if (!c || (n && msg_len && !msgs) || dst_len > 255 || (dst_len && !dst)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  timer_reset(c);
+  if (!c || !out192 || (n && msg_len && !msgs) || dst_len > 255 || (dst_len && !dst)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
   if (n == 0) return LSG_OK;
-  std::vector<lsg_set> sets(n);
-  std::vector<const lsg_set*> sp(n);
-  for (size_t i = 0; i < n; i++) {
-    memset(&sets[i], 0, sizeof(lsg_set));
-    sets[i].msg = msgs + (size_t)msg_len * i;
-    sets[i].msg_len = msg_len;
-    sp[i] = &sets[i];
-  }
-  int rc = stage_sets(c, sp.data(), n, 0, false);
-  if (rc) return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, c->st[0]));
+  int rc;
+  if ((rc = util_hash(s, msgs, msg_len, n, dst, dst_len))) return rc;
+  if ((rc = ensure(s, s->d_blob, 192 * n))) return rc;
   int nn = (int)n;
-  LAUNCH_T(c, "k_expand_msg", k_expand_msg, (nn + 63) / 64, 64, nn, P_<uint8_t>(c->d_msg), P_<uint32_t>(c->d_msgoff),
-           P_<uint32_t>(c->d_msglen), P_<uint8_t>(c->d_dst), dst_len, P_<uint8_t>(c->d_ub));
-  LAUNCH(c, k_hash_map, nn, nn, P_<uint8_t>(c->d_ub), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf));
-  if (!out192) {  // internal use (lsg_sign): leave H in d_H
-    LSG_HIP(c, hipStreamSynchronize(c->st[0]));
-    return LSG_OK;
-  }
-  if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
-  LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_hinf), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
+  LAUNCH(s, k_g2a_to_bytes, nn, nn, P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(out192, s->d_blob.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
   return LSG_OK;
 }
 
 int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, uint8_t* out192, int32_t* err) {
   if (!c || !out192 || !err || (n && !sigs)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  timer_reset(c);
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
   if (n == 0) return LSG_OK;
   std::vector<lsg_set> sets(n);
   std::vector<const lsg_set*> sp(n);
@@ -1055,147 +1476,81 @@ int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, 
     sets[i].sig_len = sig_len;
     sp[i] = &sets[i];
   }
-  int rc = stage_sets(c, sp.data(), n, 0, false);
-  if (rc) return rc;
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, sp.data(), n, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, 0)) || (rc = ensure(s, s->d_blob, 192 * n))) return rc;
   int nn = (int)n;
-  LAUNCH(c, k_sig_decode, nn, nn, P_<uint8_t>(c->d_sig), P_<uint32_t>(c->d_siglen), P_<uint32_t>(c->d_sigaff),
-         P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  LAUNCH(c, k_sig_subgroup, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<int32_t>(c->d_seterr));
-  if ((rc = ensure(c, c->d_blob, 192 * n))) return rc;
-  LAUNCH(c, k_g2a_to_bytes, nn, nn, P_<uint32_t>(c->d_sigaff), P_<uint8_t>(c->d_siginf), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out192, c->d_blob.p, 192 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipMemcpyAsync(err, c->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
+  LAUNCH(s, k_sig_decode, nn, nn, P_<uint8_t>(s->own.d_sig), P_<uint32_t>(s->own.d_siglen), P_<uint32_t>(s->d_sigaff),
+         P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
+  LAUNCH(s, k_sig_subgroup, nn, nn, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
+  LAUNCH(s, k_g2a_to_bytes, nn, nn, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(out192, s->d_blob.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(err, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
   return LSG_OK;
 }
 
 int lsg_sign(lsg_ctx* c, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96) {
   if (!c || !out96 || (n && (!sks32 || !msgs))) return LSG_ERR_INVALID_ARG;
-  int rc = lsg_hash_to_g2(c, msgs, msg_len, n, DST_POP, DST_POP_LEN, nullptr);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
-    return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->st[0]));
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  int rc;
+  if ((rc = util_hash(s, msgs, msg_len, n, DST_POP, DST_POP_LEN))) return rc;
+  if ((rc = ensure(s, s->d_blob, 96 * n)) || (rc = ensure(s, s->d_aux, 32 * n))) return rc;
+  LSG_HIP(s, hipMemcpyAsync(s->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, s->st[0]));
   int nn = (int)n;
-  LAUNCH(c, k_sign, nn, nn, P_<uint8_t>(c->d_aux), P_<uint32_t>(c->d_H), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
+  LAUNCH(s, k_sign, nn, nn, P_<uint8_t>(s->d_aux), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_blob.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   return LSG_OK;
 }
 
 int lsg_sk_to_pk(lsg_ctx* c, const uint8_t* sks32, size_t n, uint8_t* out96) {
   if (!c || !out96 || (n && !sks32)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
   int rc;
-  if ((rc = ensure(c, c->d_blob, 96 * std::max(n, (size_t)1))) || (rc = ensure(c, c->d_aux, 32 * std::max(n, (size_t)1))))
-    return rc;
-  LSG_HIP(c, hipMemcpyAsync(c->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, c->st[0]));
+  if ((rc = ensure(s, s->d_blob, 96 * n)) || (rc = ensure(s, s->d_aux, 32 * n))) return rc;
+  LSG_HIP(s, hipMemcpyAsync(s->d_aux.p, sks32, 32 * n, hipMemcpyHostToDevice, s->st[0]));
   int nn = (int)n;
-  LAUNCH(c, k_sk_to_pk, nn, nn, P_<uint8_t>(c->d_aux), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out96, c->d_blob.p, 96 * n, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
-  return LSG_OK;
-}
-
-int lsg_batch_stage(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed) {
-  if (!c || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  std::vector<const lsg_set*> sp(n_sets);
-  for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
-  return stage_sets(c, sp.data(), n_sets, seed, true);
-}
-
-int lsg_batch_run(lsg_ctx* c, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
-  if (!c || !out576 || !any_error) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  timer_reset(c);
-  size_t n_sets = c->n_sets;
-  int rc;
-  std::vector<std::vector<int32_t>> groups(1);
-  for (size_t i = 0; i < n_sets; i++) groups[0].push_back((int32_t)i);
-  if ((rc = size_miller_slots(c, 1))) return rc;
-  if ((rc = ensure(c, c->d_blob, 576))) return rc;
-  if ((rc = launch_set_stages(c))) return rc;
-  // errored sets contribute identities, so the partial covers exactly the valid sets (an
-  // empty package gives the identity)
-  if ((rc = launch_groups(c, groups, false))) return rc;
-  LAUNCH(c, k_fp12_to_canon, 1, 1, P_<uint32_t>(c->d_F), P_<uint8_t>(c->d_blob));
-  LSG_HIP(c, hipMemcpyAsync(out576, c->d_blob.p, 576, hipMemcpyDeviceToHost, c->st[0]));
-  SetStatus ss;
-  if ((rc = finish(c, &ss, nullptr, 0))) return rc;
-  *any_error = 0;
-  for (size_t i = 0; i < n_sets; i++) {
-    int32_t e = set_error(ss, i);
-    if (set_err) set_err[i] = e;
-    if (e) *any_error = 1;
-  }
-  for (size_t k = 0; k < c->n_pks; k++)
-    if (ss.pkerr[k]) *any_error = 1;
-  return LSG_OK;
-}
-
-int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
-                      int32_t* set_err, int32_t* any_error) {
-  int rc = lsg_batch_stage(c, sets, n_sets, seed);
-  if (rc) return rc;
-  return lsg_batch_run(c, out576, set_err, any_error);
-}
-
-int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, int32_t* valid) {
-  if (!c || !valid || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
-  timer_reset(c);
-  int rc;
-  size_t np = std::max(n_partials, (size_t)1);
-  if ((rc = ensure(c, c->d_blob, 576 * np)) || (rc = ensure(c, c->d_aux, 4 * W_F12 * np)) ||
-      (rc = ensure(c, c->d_F, 4 * W_F12)) || (rc = ensure(c, c->d_verdict, 4)))
-    return rc;
-  if (n_partials == 0) {
-    *valid = 0;
-    return LSG_OK;
-  }
-  LSG_HIP(c, hipMemcpyAsync(c->d_blob.p, partials576, 576 * n_partials, hipMemcpyHostToDevice, c->st[0]));
-  LAUNCH(c, k_blobs_to_fp12, n_partials, (int)n_partials, P_<uint8_t>(c->d_blob), P_<uint32_t>(c->d_aux));
-  std::vector<std::vector<int32_t>> g(1);
-  for (size_t k = 0; k < n_partials; k++) g[0].push_back((int32_t)k);
-  if ((rc = tree_reduce<2>(c, 0, "tree_fp12_product", P_<uint32_t>(c->d_aux), g, P_<uint32_t>(c->d_F)))) return rc;
-  LAUNCH(c, k_final_exp_check, 1, 1, P_<uint32_t>(c->d_F), P_<int32_t>(c->d_verdict));
-  LSG_HIP(c, hipMemcpyAsync(valid, c->d_verdict.p, 4, hipMemcpyDeviceToHost, c->st[0]));
-  LSG_HIP(c, hipStreamSynchronize(c->st[0]));
+  LAUNCH(s, k_sk_to_pk, nn, nn, P_<uint8_t>(s->d_aux), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_blob.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   return LSG_OK;
 }
 
 int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
   if (!c || !fp_mul_per_s || !mad_per_s) return LSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  LSG_HIP(c, hipSetDevice(c->device));
+  LSG_ENTER(c);
+  Slot* s = &c->util;
   hipDeviceProp_t prop;
-  LSG_HIP(c, hipGetDeviceProperties(&prop, c->device));
+  LSG_HIP(s, hipGetDeviceProperties(&prop, c->device));
   int items = prop.multiProcessorCount * 128;  // 32 waves of 4 rows per CU
   int rc;
-  if ((rc = ensure(c, c->d_aux, 4 * 16 * (size_t)items))) return rc;
+  if ((rc = ensure(s, s->d_aux, 4 * 16 * (size_t)items))) return rc;
   std::vector<uint32_t> init(16 * (size_t)items, 0);
   for (size_t i = 0; i < init.size(); i++)
     if ((i & 15) < 11) init[i] = (uint32_t)(i * 2654435761u);
-  LSG_HIP(c, hipMemcpy(c->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
+  LSG_HIP(s, hipMemcpy(s->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
   const int iters = 64;
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->st[0], items, 2,
-                     P_<uint32_t>(c->d_aux));
+  hipStream_t S = s->st[0];
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, S, items, 2, P_<uint32_t>(s->d_aux));
   hipEvent_t a, b;
-  LSG_HIP(c, hipEventCreate(&a));
-  LSG_HIP(c, hipEventCreate(&b));
-  LSG_HIP(c, hipEventRecord(a, c->st[0]));
-  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, c->st[0], items, iters,
-                     P_<uint32_t>(c->d_aux));
-  LSG_HIP(c, hipEventRecord(b, c->st[0]));
-  LSG_HIP(c, hipEventSynchronize(b));
+  LSG_HIP(s, hipEventCreate(&a));
+  LSG_HIP(s, hipEventCreate(&b));
+  LSG_HIP(s, hipEventRecord(a, S));
+  hipLaunchKernelGGL(k_probe_fp_mul, dim3(lane_blocks(items)), dim3(LSG_TPB), 0, S, items, iters,
+                     P_<uint32_t>(s->d_aux));
+  LSG_HIP(s, hipEventRecord(b, S));
+  LSG_HIP(s, hipEventSynchronize(b));
   float ms = 0;
-  LSG_HIP(c, hipEventElapsedTime(&ms, a, b));
+  LSG_HIP(s, hipEventElapsedTime(&ms, a, b));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   double muls = (double)items * iters * 4.0;
@@ -1206,12 +1561,15 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
 
 int lsg_last_kernel_times(lsg_ctx* c, const char** names, double* ms, int max) {
   if (!c) return 0;
-  for (int k = 0; k < 3; k++) (void)hipStreamSynchronize(c->st[k]);
+  std::lock_guard<std::mutex> lk(c->mu);
+  const Slot* s = c->last;
+  if (!s) return 0;
+  for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(s->st[k]);
   int n = 0;
-  for (size_t i = 0; i < c->ntimers && n < max; i++) {
+  for (size_t i = 0; i < s->ntimers && n < max; i++) {
     float t = 0;
-    if (hipEventElapsedTime(&t, c->timers[i].a, c->timers[i].b) != hipSuccess) t = -1;
-    if (names) names[n] = c->timers[i].name;
+    if (hipEventElapsedTime(&t, s->timers[i].a, s->timers[i].b) != hipSuccess) t = -1;
+    if (names) names[n] = s->timers[i].name;
     if (ms) ms[n] = t;
     n++;
   }

@@ -182,3 +182,56 @@ def test_batch_partial_and_final_verify(ctx):
 def test_probe_rate_positive(ctx):
     fp, mad = ctx.probe_fp_mul_rate()
     assert fp > 1e9 and mad == pytest.approx(fp * 300)
+
+
+def test_async_jobs_two_slots_match_sync(ctx):
+    import random
+    rng = random.Random(5)
+    pkgs = []
+    for p in range(2):
+        jobs = []
+        for j in range(20):
+            n = rng.choice([1, 2, 3])
+            sets = [bd.single_set(300 + 40 * p + 2 * j + k) for k in range(n)]
+            if rng.random() < 0.25:
+                k = rng.randrange(n)
+                sets[k] = bd.CORRUPTIONS[rng.randrange(len(bd.CORRUPTIONS))](sets[k])
+            jobs.append((sets, 1 if rng.random() < 0.8 else 0))
+        pkgs.append(jobs)
+    t0 = ctx.submit_jobs(pkgs[0], seed=21)
+    t1 = ctx.submit_jobs(pkgs[1], seed=22)
+    assert t0 is not None and t1 is not None
+    assert ctx.submit_jobs(pkgs[0], seed=23) is None  # both slots outstanding -> LSG_ERR_BUSY
+    r1, _ = ctx.wait_jobs(t1)  # out of order
+    r0, _ = ctx.wait_jobs(t0)
+    for jobs, got in ((pkgs[0], r0), (pkgs[1], r1)):
+        exp, _ = oracle_job_results(jobs)
+        assert [g[0] for g in got] == [e[0] for e in exp]
+    assert ctx.verify_jobs(pkgs[0], seed=21)[0] == r0
+
+
+def test_staged_batches_and_async_finals(ctx):
+    sets = [bd.single_set(400 + i) for i in range(24)]
+    staged = ctx.stage(sets, seed=77)
+    try:
+        ta, tb = ctx.batch_submit(staged), ctx.batch_submit(staged)
+        assert ctx.batch_submit(staged) is None
+        pa, ea, aa = ctx.batch_wait(ta)
+        pb, eb, ab = ctx.batch_wait(tb)
+        assert pa == pb and not aa and not ab and ea == [0] * 24
+        # the same package through the synchronous path gives the same partial
+        ps, _, _ = ctx.batch_partial(sets, seed=77)
+        assert ps == pa
+        fs = [ctx.final_submit([pa]), ctx.final_submit([pa, pb]), ctx.final_submit([])]
+        assert [ctx.final_wait(t) for t in fs] == [True, True, False]
+    finally:
+        staged.free()
+
+
+def test_batch_partial_excludes_errored_sets(ctx):
+    sets = [bd.single_set(500 + i) for i in range(6)]
+    sets[3] = bd.corrupt_truncate(sets[3])
+    sets[4] = bd.corrupt_not_in_group(sets[4])
+    part, errs, anyerr = ctx.batch_partial(sets, seed=9)
+    assert anyerr and errs == [0, 0, 0, 10, 3, 0]
+    assert ctx.final_verify([part])  # the remaining sets are valid; errored ones are identities
