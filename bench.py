@@ -30,7 +30,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # 2 pipeline slots x 2 streams + the final-exponentiation stream (+ RCCL's): give each its
 # own hardware queue instead of HIP's default 4 shared ones
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--depth", type=int, default=2, help="batches in flight (<= library pipeline slots)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,10 +143,10 @@ def main():
             times += ctx.last_kernel_times()
         return lat, times
 
-    run(args.warmup)
+    run(args.warmup, depth=args.depth)
     barrier()
     t0 = time.perf_counter()
-    lat, ktimes = run(args.steps, capture=True)
+    lat, ktimes = run(args.steps, depth=args.depth, capture=True)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -192,7 +193,7 @@ def main():
                        "parallelism": f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
-            "pipeline_depth": 2,
+            "pipeline_depth": args.depth,
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},

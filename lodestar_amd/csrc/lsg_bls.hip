@@ -353,7 +353,7 @@ namespace {
 
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
-constexpr int LSG_SLOTS = 2;   // batch / job slots in flight
+constexpr int LSG_SLOTS = 6;   // batch / job slots in flight
 constexpr int LSG_FINALS = 4;  // final-exponentiation entries in flight
 
 // u32 words per item for each lane-form type

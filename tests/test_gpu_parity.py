@@ -201,9 +201,17 @@ def test_async_jobs_two_slots_match_sync(ctx):
     t0 = ctx.submit_jobs(pkgs[0], seed=21)
     t1 = ctx.submit_jobs(pkgs[1], seed=22)
     assert t0 is not None and t1 is not None
-    assert ctx.submit_jobs(pkgs[0], seed=23) is None  # both slots outstanding -> LSG_ERR_BUSY
+    extra = []
+    while True:  # fill the remaining pipeline slots; then every slot is outstanding -> LSG_ERR_BUSY
+        t = ctx.submit_jobs(pkgs[0], seed=23)
+        if t is None:
+            break
+        extra.append(t)
+        assert len(extra) < 64
     r1, _ = ctx.wait_jobs(t1)  # out of order
     r0, _ = ctx.wait_jobs(t0)
+    for t in extra:
+        assert [g[0] for g in ctx.wait_jobs(t)[0]] == [g[0] for g in r0]
     for jobs, got in ((pkgs[0], r0), (pkgs[1], r1)):
         exp, _ = oracle_job_results(jobs)
         assert [g[0] for g in got] == [e[0] for e in exp]
