@@ -126,6 +126,9 @@ int lsg_device_name(lsg_ctx* ctx, char* buf, size_t len);
  * randomizers deterministic (tests); seed == 0 draws them from the OS CSPRNG. */
 int lsg_submit_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket);
 int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n_jobs] */, lsg_stats* stats);
+/* Number of pipeline slots (packages that may be outstanding at once): the back-pressure
+ * bound of canAcceptWork (multithread/index.ts:143-149 workersBusy < poolSize). */
+int lsg_pipeline_slots(lsg_ctx* ctx, int32_t* n);
 /* *done = 1 once the ticket's device work has finished (any ticket kind). */
 int lsg_poll(lsg_ctx* ctx, lsg_ticket ticket, int32_t* done);
 /* submit + wait */

@@ -48,5 +48,29 @@ def build(force=False, verbose=True):
     return OUT
 
 
+NAPI_SRC = os.path.join(HERE, "napi", "lsg_napi.c")
+NAPI_OUT = os.path.join(HERE, "napi", "lsg_napi.node")
+NODE_INCLUDE = "/usr/include/node"
+
+
+def build_napi(verbose=True):
+    """Thin N-API addon (lodestar_amd/napi/lsg_napi.node) over the C ABI, for the Node host
+    (lodestar_amd/js/blsGpuVerifier.js).  Skipped (returns None) when Node's headers are absent."""
+    if not os.path.exists(os.path.join(NODE_INCLUDE, "node_api.h")):
+        return None
+    deps = [NAPI_SRC, OUT, os.path.join(ROOT, "include", "lodestar_bls.h")]
+    if os.path.exists(NAPI_OUT) and max(os.path.getmtime(d) for d in deps) <= os.path.getmtime(NAPI_OUT):
+        return NAPI_OUT
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-DNODE_GYP_MODULE_NAME=lsg_napi",
+           "-I", NODE_INCLUDE, "-I", os.path.join(ROOT, "include"), NAPI_SRC, "-o", NAPI_OUT + ".tmp",
+           "-L", HERE, "-llodestar_bls", "-Wl,-rpath,$ORIGIN/.."]
+    if verbose:
+        print("[lodestar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(NAPI_OUT + ".tmp", NAPI_OUT)
+    return NAPI_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_napi()

@@ -1180,6 +1180,22 @@ int util_hash(Slot* s, const uint8_t* msgs, uint32_t msg_len, size_t n, const ui
   std::lock_guard<std::mutex> _lk((c)->mu); \
   LSG_HIPC((c), hipSetDevice((c)->device))
 
+// Block until a ticket's device work is done WITHOUT holding the context mutex, so a
+// waiter (e.g. an N-API worker thread) never stalls submissions from another thread.  The
+// ticket's slot cannot be recycled meanwhile: only the ticket's own wait call releases it.
+int presync(lsg_ctx* c, lsg_ticket ticket, int kind) {
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot* s = ticket_slot(c, ticket, kind);
+    if (!s) return LSG_ERR_INVALID_ARG;
+    ev = s->ev_done;
+  }
+  hipError_t e = hipEventSynchronize(ev);
+  if (e != hipSuccess) return fail_c(c, "hipEventSynchronize", e);
+  return LSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1245,6 +1261,7 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
 
 int lsg_wait_jobs(lsg_ctx* c, lsg_ticket ticket, lsg_job_result* results, lsg_stats* stats) {
   if (!c) return LSG_ERR_INVALID_ARG;
+  if (int prc = presync(c, ticket, SLOT_JOBS)) return prc;
   LSG_ENTER(c);
   Slot* s = ticket_slot(c, ticket, SLOT_JOBS);
   if (!s || (s->plan.results.size() && !results)) return LSG_ERR_INVALID_ARG;
@@ -1270,6 +1287,12 @@ int lsg_verify_sets(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t see
   job.n_sets = (uint32_t)n_sets;
   job.flags = 0;
   return lsg_verify_jobs(c, &job, 1, seed, result, nullptr);
+}
+
+int lsg_pipeline_slots(lsg_ctx* c, int32_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  *n = LSG_SLOTS;
+  return LSG_OK;
 }
 
 int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
@@ -1337,6 +1360,7 @@ int lsg_batch_submit(lsg_ctx* c, const lsg_staged* staged, lsg_ticket* ticket) {
 
 int lsg_batch_wait(lsg_ctx* c, lsg_ticket ticket, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
   if (!c || !out576 || !any_error) return LSG_ERR_INVALID_ARG;
+  if (int prc = presync(c, ticket, SLOT_BATCH)) return prc;
   LSG_ENTER(c);
   Slot* s = ticket_slot(c, ticket, SLOT_BATCH);
   if (!s) return LSG_ERR_INVALID_ARG;
@@ -1388,6 +1412,7 @@ int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, 
 
 int lsg_final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) {
   if (!c || !valid) return LSG_ERR_INVALID_ARG;
+  if (int prc = presync(c, ticket, SLOT_FINAL)) return prc;
   LSG_ENTER(c);
   Slot* s = ticket_slot(c, ticket, SLOT_FINAL);
   if (!s) return LSG_ERR_INVALID_ARG;

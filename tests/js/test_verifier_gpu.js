@@ -1,0 +1,60 @@
+"use strict";
+/**
+ * BlsGpuVerifier through the real N-API addon on an MI355X (driven by
+ * tests/test_gpu_parity.py::test_node_host_on_gpu, which writes the input file with
+ * oracle-made sets and expected results).  Restates test/e2e/chain/bls/multithread.test.ts:
+ * 25-103 against the GPU: 8 x 3 valid sets (sync, async, batchable) -> true; a 32-byte zero
+ * signature rejects with BLST_INVALID_SIZE and does not poison co-batched jobs.
+ * Run: node tests/js/test_verifier_gpu.js <cases.json>
+ */
+const assert = require("assert");
+const fs = require("fs");
+const path = require("path");
+const V = require(path.join(__dirname, "..", "..", "lodestar_amd", "js", "blsGpuVerifier.js"));
+
+const hex = (s) => Uint8Array.from(Buffer.from(s, "hex"));
+const cases = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
+const toSet = (c) =>
+  c.pks.length === 1
+    ? {type: V.SignatureSetType.single, pubkey: hex(c.pks[0]), signingRoot: hex(c.msg), signature: hex(c.sig)}
+    : {type: V.SignatureSetType.aggregate, pubkeys: c.pks.map(hex), signingRoot: hex(c.msg), signature: hex(c.sig)};
+const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
+
+(async () => {
+  const pool = new V.BlsGpuVerifier({seed: 7});
+  const sets = cases.valid.map(toSet);
+  // multithread.test.ts:72-86
+  assert.deepStrictEqual(await Promise.all(Array.from({length: 8}, () => pool.verifySignatureSets(sets))), Array(8).fill(true));
+  const ps = [];
+  for (let i = 0; i < 8; i++) {
+    ps.push(pool.verifySignatureSets(sets, {batchable: true}));
+    await sleep(5);
+  }
+  assert.deepStrictEqual(await Promise.all(ps), Array(8).fill(true));
+  // multithread.test.ts:88-103
+  const invalidSet = Object.assign({}, sets[0], {signature: new Uint8Array(32)});
+  const pBad = pool.verifySignatureSets([invalidSet], {batchable: true});
+  const pGood = Array.from({length: 8}, () => pool.verifySignatureSets(sets, {batchable: true}));
+  await assert.rejects(pBad, /BLST_INVALID_SIZE/);
+  assert.deepStrictEqual(await Promise.all(pGood), Array(8).fill(true));
+  // wrong message -> false; aggregate set -> true; main-thread path
+  assert.strictEqual(await pool.verifySignatureSets([sets[0], toSet(cases.wrong_message)]), false);
+  assert.strictEqual(await pool.verifySignatureSets([toSet(cases.aggregate)]), true);
+  assert.strictEqual(await pool.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  // per-set verdicts for one message
+  const sm = cases.same_message;
+  const got = await pool.verifySignatureSetsSameMessage(
+    sm.sets.map((s) => ({publicKey: hex(s.pk), signature: hex(s.sig)})), hex(sm.msg));
+  assert.deepStrictEqual(got, sm.expected);
+  // parity exports
+  const agg = pool.addon.aggregatePubkeys(pool.ctx, cases.aggregate.pks.map(hex));
+  assert.strictEqual(agg.errCode, 0);
+  assert.strictEqual(Buffer.from(agg.bytes).toString("hex"), cases.aggregate_pk);
+  const h = pool.addon.hashToG2(pool.ctx, hex(cases.h2c.msg), Buffer.from(cases.h2c.dst, "latin1"));
+  assert.strictEqual(Buffer.from(h).toString("hex"), cases.h2c.out);
+  await pool.close();
+  console.log("node host on GPU: all checks passed");
+})().catch((e) => {
+  console.log("FAIL", e && e.stack);
+  process.exit(1);
+});

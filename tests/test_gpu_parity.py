@@ -243,3 +243,44 @@ def test_batch_partial_excludes_errored_sets(ctx):
     part, errs, anyerr = ctx.batch_partial(sets, seed=9)
     assert anyerr and errs == [0, 0, 0, 10, 3, 0]
     assert ctx.final_verify([part])  # the remaining sets are valid; errored ones are identities
+
+
+def test_node_host_on_gpu(ctx, tmp_path):
+    """BlsGpuVerifier (Node) -> N-API addon -> C ABI on the GPU: multithread.test.ts:25-103."""
+    import shutil
+    import subprocess
+    if shutil.which("node") is None:
+        pytest.skip("node not installed")
+    addon = os.path.join(HERE, "..", "lodestar_amd", "napi", "lsg_napi.node")
+    assert os.path.exists(addon), "N-API addon not built"
+    from oracle.curves import g1_serialize, g2_serialize
+    valid = [bd.single_set(900 + i, tag="node") for i in range(3)]
+    agg = bd.aggregate_set(5, [11, 12, 13], tag="node")
+    wrong = bd.corrupt_wrong_message(bd.single_set(904, tag="node"))
+    sm_msg = bd.msg("node-same", 0)
+    sm_sets, sm_exp = [], []
+    for k in range(4):
+        pks, _, sig = bd.single_set(920 + k, tag="x")
+        good = k != 2
+        m = sm_msg if good else bd.msg("node-other", k)
+        s = bd.single_set(920 + k, tag="x")
+        sig = bd.g2_compress(bd.sig_point((920 + k,), m))
+        sm_sets.append({"pk": pks[0].hex(), "sig": sig.hex()})
+        sm_exp.append(good)
+    pts = [ov.public_key_from_bytes(p) for p in agg[0]]
+    h2c_msg = bd.msg("node-h2c", 0)
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    cases = {
+        "valid": [{"pks": [p.hex() for p in s[0]], "msg": s[1].hex(), "sig": s[2].hex()} for s in valid],
+        "wrong_message": {"pks": [p.hex() for p in wrong[0]], "msg": wrong[1].hex(), "sig": wrong[2].hex()},
+        "aggregate": {"pks": [p.hex() for p in agg[0]], "msg": agg[1].hex(), "sig": agg[2].hex()},
+        "aggregate_pk": g1_serialize(ov.aggregate_pubkeys(pts)).hex(),
+        "same_message": {"msg": sm_msg.hex(), "sets": sm_sets, "expected": sm_exp},
+        "h2c": {"msg": h2c_msg.hex(), "dst": dst.decode(), "out": g2_serialize(h2c.hash_to_g2(h2c_msg, dst)).hex()},
+    }
+    f = tmp_path / "cases.json"
+    f.write_text(json.dumps(cases))
+    r = subprocess.run(["node", os.path.join(HERE, "js", "test_verifier_gpu.js"), str(f)], capture_output=True,
+                       text=True, timeout=180)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
