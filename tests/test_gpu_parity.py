@@ -223,9 +223,18 @@ def test_staged_batches_and_async_finals(ctx):
     staged = ctx.stage(sets, seed=77)
     try:
         ta, tb = ctx.batch_submit(staged), ctx.batch_submit(staged)
-        assert ctx.batch_submit(staged) is None
+        extra = []
+        while True:  # every pipeline slot outstanding -> LSG_ERR_BUSY (None)
+            t = ctx.batch_submit(staged)
+            if t is None:
+                break
+            extra.append(t)
+            assert len(extra) < 64
+        assert len(extra) + 2 == ctx.pipeline_slots()
         pa, ea, aa = ctx.batch_wait(ta)
         pb, eb, ab = ctx.batch_wait(tb)
+        for t in extra:
+            assert ctx.batch_wait(t)[0] == pa
         assert pa == pb and not aa and not ab and ea == [0] * 24
         # the same package through the synchronous path gives the same partial
         ps, _, _ = ctx.batch_partial(sets, seed=77)
