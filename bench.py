@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=2, help="batches in flight (<= library pipeline slots)")
+    ap.add_argument("--depth", type=int, default=4, help="batches in flight (<= library pipeline slots)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

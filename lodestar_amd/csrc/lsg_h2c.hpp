@@ -162,6 +162,13 @@ LSG_INL fp_t fp_from_be64_mod(const uint8_t* b) {
 }
 
 // ------------------------------------------------------------------ SSWU on E2' (RFC 9380 6.6.2)
+// One exponentiation decides between x1 and x2 for every row of the wave at once (no
+// divergent second square root): with gx2 = (Z u^2)^3 gx1 and N(Z) = 5 a non-square in Fp,
+// if N(gx1) is a non-square then
+//   sqrt(N(gx2)) = N(Z u^2) N(u) (N(Z) N(gx1))^((p+1)/4) = N(Z u^2) N(u) 5^((p+1)/4) s1,
+// where s1 = N(gx1)^((p+1)/4) is the candidate already computed.  The root of gx (x1 or
+// x2) then costs one more exponentiation.  The result equals RFC 9380's: the square root
+// is unique up to sign and the sign is fixed by sgn0 below.
 LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) {
   fp2_t u2 = fp2_sqr(u);
   fp2_t zu2 = fp2_mul(SSWU_Z, u2);
@@ -172,15 +179,13 @@ LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) {
   fp2_t gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
   fp2_t x2 = fp2_mul(zu2, x1);
   fp2_t gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), SSWU_A), x2), SSWU_B);
-  fp2_t y;
-  bool sq1 = fp2_sqrt(y, gx1);
+  bool sq1;
+  fp_t s1 = fp2_norm_sqrt_candidate(gx1, &sq1);
+  fp_t s2 = fp_mul(fp_mul(fp2_norm(zu2), fp2_norm(u)), fp_mul(s1, fp_t(SSWU_NZ_POW_P1D4)));
   g2a_t r;
-  if (sq1) {
-    r.x = x1;
-  } else {
-    (void)fp2_sqrt(y, gx2);  // exactly one of gx1, gx2 is square
-    r.x = x2;
-  }
+  r.x = fp2_select(sq1, x1, x2);
+  fp2_t y;
+  (void)fp2_sqrt_with_norm_root(y, fp2_select(sq1, gx1, gx2), fp_select(sq1, s1, s2));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   r.y = y;
   return r;

@@ -184,11 +184,17 @@ LSG_INL bool fp2_lexi_largest(const fp2_t& y) {
 //   n = a0^2 + a1^2, s = sqrt(n);  c = (a0 + s)/2 (c = a0 if that is 0);  t = c^((p-3)/4)
 //   c square:      root = (c t, a1 t / 2)
 //   c non-square:  root = (a1 t / 2, -c t)
-// Returns false when a is not a square.  Callers fix the root's sign afterwards.
-LSG_BIGFN bool fp2_sqrt(fp2_t& out, fp2_t a) {
+// Any square root s of n works (the two cases cover both signs).  Returns false when a is
+// not a square.  Callers fix the root's sign afterwards.
+// Stage 1: the norm's candidate root s = n^((p+1)/4); *is_sq = (s^2 == n).
+LSG_INL fp_t fp2_norm_sqrt_candidate(const fp2_t& a, bool* is_sq) {
   fp_t n = fp2_norm(a);
   fp_t s = fp_pow_fixed(n, LSG_EXP_P_PLUS_1_DIV_4);
-  bool ok = fp_eq(fp_sqr(s), n);
+  *is_sq = fp_eq(fp_sqr(s), n);
+  return s;
+}
+// Stage 2: the root of a from a square root s of N(a).
+LSG_BIGFN bool fp2_sqrt_with_norm_root(fp2_t& out, fp2_t a, fp_t s) {
   fp_t c = fp_mul(fp_add(a.c0, s), fp_t(FP_HALF));
   c = fp_select(fp_is_zero(c), a.c0, c);
   fp_t t = fp_pow_fixed(c, LSG_EXP_P_MINUS_3_DIV_4);
@@ -196,9 +202,14 @@ LSG_BIGFN bool fp2_sqrt(fp2_t& out, fp2_t a) {
   bool c_sq = fp_eq(fp_mul(ct, t), fp_one()) || fp_is_zero(c);
   fp_t h = fp_mul(fp_mul(a.c1, t), fp_t(FP_HALF));
   fp2_t r = c_sq ? fp2_t(ct, h) : fp2_t(h, fp_neg(ct));
-  ok = ok && fp2_eq(fp2_sqr(r), a);
   out = r;
-  return ok;
+  return fp2_eq(fp2_sqr(r), a);
+}
+LSG_BIGFN bool fp2_sqrt(fp2_t& out, fp2_t a) {
+  bool ok;
+  fp_t s = fp2_norm_sqrt_candidate(a, &ok);
+  bool r = fp2_sqrt_with_norm_root(out, a, s);
+  return ok && r;
 }
 
 // ------------------------------------------------------------------ Fp6
