@@ -180,7 +180,32 @@ __global__ void __launch_bounds__(LSG_TPB) k_miller_sets(int n, const uint32_t* 
   lane_store(f, item, r);
 }
 
-// f_g = ML(-G1, S_g) = conj(ML(G1, S_g)) written at slot n_sets + g
+// f_item = prod over the item's sets (<= K consecutive sets of one job) of ML(P_i, H(m_i)):
+// one shared f and one squaring per loop step for all K pairs.  Sets with errors or an
+// infinite point contribute 1.
+template <int K>
+__global__ void __launch_bounds__(LSG_TPB) k_miller_multi(int n_items, const int32_t* __restrict__ item_first,
+                                                           const int32_t* __restrict__ item_cnt,
+                                                           const uint32_t* __restrict__ P,
+                                                           const uint8_t* __restrict__ pinf, const uint32_t* __restrict__ H,
+                                                           const uint8_t* __restrict__ hinf,
+                                                           const int32_t* __restrict__ err, uint32_t* __restrict__ f) {
+  LANE_ITEM(n_items);
+  const int first = item_first[item], cnt = item_cnt[item];
+  g1a_t Pk[K];
+  g2a_t Qk[K];
+  bool use[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = first + (k < cnt ? k : cnt - 1);
+    use[k] = k < cnt && err[i] == 0 && !pinf[i] && !hinf[i];
+    Pk[k] = lane_load<g1a_t>(P, i);
+    Qk[k] = lane_load<g2a_t>(H, i);
+  }
+  lane_store(f, item, miller_loop_multi<K>(Pk, Qk, use));
+}
+
+// f_g = ML(-G1, S_g) = conj(ML(G1, S_g)) written at slot n_items + g
 __global__ void __launch_bounds__(LSG_TPB) k_miller_groups(int ng, const uint32_t* __restrict__ S, size_t slot0,
                                                             uint32_t* __restrict__ f) {
   LANE_ITEM(ng);
@@ -449,6 +474,11 @@ struct Slot {
   // groups, reductions, outputs
   DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
   TreeSlot tree[3];
+  // Miller items: <= LSG_MILLER_K consecutive sets of one job share one multi-Miller loop
+  std::vector<int32_t> item_host;  // [first..., count...]
+  std::vector<int32_t> set_item;   // set -> item
+  size_t n_items = 0;
+  DevBuf d_items;
   HostBuf h_err, h_pinf, h_pkerr, h_verdict, h_blob;  // pinned result mirrors
   size_t n_verdicts = 0;
   std::vector<Timer> timers;
@@ -609,6 +639,7 @@ void slot_destroy(Slot* s) {
                     &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
                     &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux};
   for (DevBuf* b : bufs) free_dev(*b);
+  free_dev(s->d_items);
   for (TreeSlot& t : s->tree) {
     free_dev(t.idx);
     free_dev(t.tA);
@@ -793,6 +824,47 @@ int tree_reduce(Slot* s, int ts, const char* name, const uint32_t* src,
   return LSG_OK;
 }
 
+constexpr int LSG_MILLER_KMAX = 4;  // pairs per multi-Miller item: 1, 2 or 4 (env LSG_MILLER_K)
+int miller_k() {
+  static int k = [] {
+    const char* e = getenv("LSG_MILLER_K");
+    int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
+  return k;
+}
+
+// Items of <= LSG_MILLER_K consecutive sets that never cross a range (a job): per-job Miller
+// products, needed by the per-job retry, stay products of whole items.
+void plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges) {
+  std::vector<int32_t> first, cnt;
+  s->set_item.assign(s->in->n_sets, 0);
+  for (auto& r : ranges)
+    for (size_t i = r.first; i < r.second; i += (size_t)miller_k()) {
+      size_t c = std::min((size_t)miller_k(), r.second - i);
+      for (size_t k = 0; k < c; k++) s->set_item[i + k] = (int32_t)first.size();
+      first.push_back((int32_t)i);
+      cnt.push_back((int32_t)c);
+    }
+  s->n_items = first.size();
+  s->item_host = first;
+  s->item_host.insert(s->item_host.end(), cnt.begin(), cnt.end());
+}
+
+// set-index groups -> item-index groups (every group is a union of whole jobs)
+std::vector<std::vector<int32_t>> item_groups(const Slot* s, const std::vector<std::vector<int32_t>>& groups) {
+  std::vector<std::vector<int32_t>> out(groups.size());
+  for (size_t g = 0; g < groups.size(); g++) {
+    int32_t last = -1;
+    for (int32_t i : groups[g]) {
+      int32_t it = s->set_item[(size_t)i];
+      if (it != last) out[g].push_back(it);
+      last = it;
+    }
+  }
+  return out;
+}
+
 // Per-set stages (no host synchronisation):
 //   side: pubkeys -> aggregation tree -> [r_i] scaling -> signature decode -> subgroup
 //         check (event ev_sig) -> [r_i] sig_i
@@ -824,8 +896,31 @@ int launch_set_stages(Slot* s) {
            P_<uint32_t>(in->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN, P_<uint8_t>(s->d_ub));
   LAUNCH(s, k_hash_map, n, n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf));
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
-  LAUNCH(s, k_miller_sets, n, n, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf), P_<uint32_t>(s->d_H),
-         P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_fall));
+  int ni = (int)s->n_items;
+  if (ni <= 0 || s->item_host.size() != 2 * (size_t)ni) {
+    s->c->err = "internal: Miller items not planned";
+    return LSG_ERR_INVALID_ARG;
+  }
+  int rc2;
+  if ((rc2 = ensure(s, s->d_items, 4 * s->item_host.size()))) return rc2;
+  LSG_HIP(s, hipMemcpyAsync(s->d_items.p, s->item_host.data(), 4 * s->item_host.size(), hipMemcpyHostToDevice,
+                            s->st[0]));
+  const int32_t* items = P_<int32_t>(s->d_items);
+  const uint32_t* mP = P_<uint32_t>(s->d_P);
+  const uint32_t* mH = P_<uint32_t>(s->d_H);
+  const uint8_t* mpi = P_<uint8_t>(s->d_pinf);
+  const uint8_t* mhi = P_<uint8_t>(s->d_hinf);
+  const int32_t* merr = P_<int32_t>(s->d_seterr);
+  uint32_t* mf = P_<uint32_t>(s->d_fall);
+  if (miller_k() == 1)
+    LAUNCH_T(s, "k_miller_multi", k_miller_multi<1>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mH, mhi,
+             merr, mf);
+  else if (miller_k() == 2)
+    LAUNCH_T(s, "k_miller_multi", k_miller_multi<2>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mH, mhi,
+             merr, mf);
+  else
+    LAUNCH_T(s, "k_miller_multi", k_miller_multi<4>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mH, mhi,
+             merr, mf);
   return LSG_OK;
 }
 
@@ -837,7 +932,7 @@ int launch_set_stages(Slot* s) {
 int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool fe) {
   size_t ng = groups.size();
   if (ng == 0) return LSG_OK;
-  size_t n = s->in->n_sets;
+  size_t n = s->n_items;  // Miller items occupy d_fall[0..n_items)
   if (s->d_fall.cap < 4 * W_F12 * (n + ng) || s->d_S.cap < 4 * W_G2P * ng || s->d_F.cap < 4 * W_F12 * ng ||
       s->d_verdict.cap < 4 * ng) {
     s->c->err = "internal: group buffers too small";
@@ -850,7 +945,7 @@ int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool
   LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
   s->cur = 0;
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_grp, 0));
-  std::vector<std::vector<int32_t>> fg = groups;
+  std::vector<std::vector<int32_t>> fg = item_groups(s, groups);
   for (size_t g = 0; g < ng; g++) fg[g].push_back((int32_t)(n + g));
   if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_fall), fg, P_<uint32_t>(s->d_F)))) return rc;
   if (fe) LAUNCH(s, k_final_exp_check, ng, (int)ng, P_<uint32_t>(s->d_F), P_<int32_t>(s->d_verdict));
@@ -1013,6 +1108,12 @@ int submit_jobs(lsg_ctx* c, Slot* s, const lsg_job* jobs, size_t n_jobs, uint64_
   int rc;
   if ((rc = stage_sets(s, &s->own, flat.data(), flat.size(), seed, true, s->st[0]))) return rc;
   if ((rc = size_state(s, std::max(P.groups.size(), n_jobs)))) return rc;
+  {
+    std::vector<std::pair<size_t, size_t>> ranges;
+    for (size_t j = 0; j < n_jobs; j++)
+      if (P.jcount[j]) ranges.push_back({P.jfirst[j], P.jfirst[j] + P.jcount[j]});
+    plan_items(s, ranges);
+  }
   if ((rc = launch_set_stages(s))) return rc;
   if ((rc = launch_groups(s, P.groups, true))) return rc;
   return launch_readback(s, true, P.groups.size());
@@ -1092,6 +1193,7 @@ int wait_jobs(lsg_ctx* c, Slot* s, lsg_job_result* results, lsg_stats* stats) {
 int submit_batch(Slot* s) {
   int rc;
   if ((rc = size_state(s, 1))) return rc;
+  plan_items(s, {{(size_t)0, s->in->n_sets}});
   if ((rc = launch_set_stages(s))) return rc;
   std::vector<std::vector<int32_t>> groups(1);
   for (size_t i = 0; i < s->in->n_sets; i++) groups[0].push_back((int32_t)i);

@@ -89,6 +89,61 @@ LSG_BIGFN fp12_t miller_loop(g1a_t P, g2a_t Q) {
   return fp12_conj(f);
 }
 
+LSG_INL fp12_t fp12_from_line(const line_t& L) {
+  fp12_t f;
+  f.c0 = fp6_make(L.l00, L.l01, fp2_zero());
+  f.c1 = fp6_make(fp2_zero(), L.l11, fp2_zero());
+  return f;
+}
+LSG_INL fp12_t fp12_select(bool c, const fp12_t& a, const fp12_t& b) {
+  fp12_t r;
+  r.c0 = fp6_make(fp2_select(c, a.c0.c0, b.c0.c0), fp2_select(c, a.c0.c1, b.c0.c1), fp2_select(c, a.c0.c2, b.c0.c2));
+  r.c1 = fp6_make(fp2_select(c, a.c1.c0, b.c1.c0), fp2_select(c, a.c1.c1, b.c1.c1), fp2_select(c, a.c1.c2, b.c1.c2));
+  return r;
+}
+
+// Multi-Miller loop over K pairs sharing one f and its squarings (blst miller_loop_n):
+// returns prod_{k: use[k]} conj(f_{|x|,Q_k}(P_k)), the same field element as the product of
+// the per-pair miller_loop() values.  Pairs with use[k] == false contribute 1 (their point
+// arithmetic still runs so that every row of a wave follows one control path).
+template <int K>
+LSG_INL fp12_t miller_loop_multi(const g1a_t (&P)[K], const g2a_t (&Q)[K], const bool (&use)[K]) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  g2p_t T[K];
+  fp12_t f = fp12_one();
+  bool started = false;  // row-uniform: f still 1
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    T[k] = proj_from_aff(Q[k]);
+    line_t L = ml_dbl_step(T[k], P[k].x, P[k].y);
+    fp12_t g = started ? fp12_mul_line(f, L.l00, L.l01, L.l11) : fp12_from_line(L);
+    f = fp12_select(use[k], g, f);
+    started = true;
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) {  // bit 62 of |x| is 1
+    line_t L = ml_add_step(T[k], Q[k], P[k].x, P[k].y);
+    f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
+  }
+#pragma unroll 1
+  for (int b = 61; b >= 0; b--) {
+    f = fp12_sqr(f);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      line_t L = ml_dbl_step(T[k], P[k].x, P[k].y);
+      f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
+    }
+    if ((xa >> b) & 1u) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        line_t L = ml_add_step(T[k], Q[k], P[k].x, P[k].y);
+        f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
+      }
+    }
+  }
+  return fp12_conj(f);
+}
+
 // g^x for g in the cyclotomic subgroup
 LSG_BIGFN fp12_t fp12_exp_by_x(fp12_t g) {
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;

@@ -125,6 +125,20 @@ void hc_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
 // Fp-multiplication counts of each device stage for one representative set (bench/opcount.json).
 // counts[]: sig_decode, sig_subgroup, pk_decode, pk_scale, hash_map, sig_scale, miller,
 //           g2_add, fp12_mul, final_exp, g1_add
+// multi-Miller loop over 4 pairs (use[k] = 0 drops pair k) -- lsg_pairing.hpp:miller_loop_multi
+void hc_miller_multi4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t* use4, uint8_t* out576) {
+  g1a_t P[4];
+  g2a_t Q[4];
+  bool use[4];
+  for (int k = 0; k < 4; k++) {
+    bool inf;
+    g1_deserialize(P[k], inf, p96x4 + 96 * k, 96);
+    g2_deserialize_uncompressed(Q[k], inf, q192x4 + 192 * k);
+    use[k] = use4[k] != 0;
+  }
+  wr12(out576, miller_loop_multi<4>(P, Q, use));
+}
+
 void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32, uint64_t r, unsigned long long* counts) {
   g2a_t s;
   g1a_t pk;

@@ -221,3 +221,21 @@ def test_miller_loop_and_final_exp(hc):
     o2 = buf(576)
     hc.hc_final_exp(o.raw, o2)
     assert ub12(o2.raw) == final_exp_fast(f)
+
+
+def test_miller_loop_multi_is_product_of_single_loops(hc):
+    """lsg_pairing.hpp:miller_loop_multi (blst miller_loop_n form: shared f and squarings)
+    equals the product of the per-pair Miller values; dropped pairs contribute 1."""
+    from oracle.fields import f12_mul, F12_ONE
+    pairs = [(E1.mul(G1_GEN, 11 + k), E2.mul(G2_GEN, 23 + 7 * k)) for k in range(4)]
+    pb = b"".join(g1_serialize(p) for p, _ in pairs)
+    qb = b"".join(g2_serialize(q) for _, q in pairs)
+    singles = [miller_loop_fast(p, q) for p, q in pairs]
+    for use in ([1, 1, 1, 1], [0, 1, 1, 1], [1, 0, 1, 0], [0, 0, 0, 1], [0, 0, 0, 0]):
+        o = buf(576)
+        hc.hc_miller_multi4(pb, qb, (ctypes.c_int32 * 4)(*use), o)
+        exp = F12_ONE
+        for u, f in zip(use, singles):
+            if u:
+                exp = f12_mul(exp, f)
+        assert ub12(o.raw) == exp, use
