@@ -30,7 +30,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # 2 pipeline slots x 2 streams + the final-exponentiation stream (+ RCCL's): give each its
 # own hardware queue instead of HIP's default 4 shared ones
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=4, help="batches in flight (<= library pipeline slots)")
+    ap.add_argument("--depth", type=int, default=8, help="batches in flight (<= library pipeline slots)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -12,9 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
-SOURCES = ["lsg_bls.hip"]
+SOURCES = ["lsg_bls.hip", "lsg_serial.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
-           "lsg_pairing.hpp", "lsg_constants.hpp"]
+           "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_quad.hpp", "lsg_io.hpp", "lsg_serial.h"]
 
 
 def hipcc():

@@ -39,19 +39,29 @@
 #include <vector>
 
 #include "../../include/lodestar_bls.h"
-#include "lsg_fp_lane.hpp"
-#include "lsg_h2c.hpp"
-#include "lsg_pairing.hpp"
+#include "lsg_serial.h"
 
-#define LSG_TPB 256          // threads per block (16 lane-items)
-#define LSG_ITEMS_PER_BLOCK 16
+// The math headers go into an anonymous namespace: lsg_serial.hip instantiates the same
+// generic code over the row backend, and the two fp_t must never be merged at link time.
+namespace {
+#ifdef LSG_BACKEND_ROW
+#include "lsg_fp_lane.hpp"  // one element per 16-lane DPP row
+#else
+#include "lsg_fp_quad.hpp"  // one element per 4-lane quad (default)
+#endif
+#include "lsg_h2c.hpp"
+#include "lsg_io.hpp"
+}  // namespace
+
+#define LSG_TPB 256  // threads per block
+#define LSG_ITEMS_PER_BLOCK (LSG_TPB / LSG_GROUP)
 
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 #define LANE_ITEM(n)                        \
   lsg_lane_setup();                         \
-  const size_t item = gtid() >> 4;          \
+  const size_t item = gtid() / LSG_GROUP;   \
   if (item >= (size_t)(n)) return;          \
-  const bool lead = (threadIdx.x & 15) == 0
+  const bool lead = (threadIdx.x % LSG_GROUP) == 0
 
 // ---------------------------------------------------------------------------- kernels
 // expand_message_xmd(msg_i, DST, 256): one thread per set (byte-serial SHA-256)
@@ -169,17 +179,6 @@ __global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const uint32_t* __
   lane_store(rs, item, r);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_miller_sets(int n, const uint32_t* __restrict__ P,
-                                                          const uint8_t* __restrict__ pinf, const uint32_t* __restrict__ H,
-                                                          const uint8_t* __restrict__ hinf,
-                                                          const int32_t* __restrict__ err, uint32_t* __restrict__ f) {
-  LANE_ITEM(n);
-  fp12_t r = fp12_one();
-  if (err[item] == 0 && !pinf[item] && !hinf[item])
-    r = miller_loop(lane_load<g1a_t>(P, item), lane_load<g2a_t>(H, item));
-  lane_store(f, item, r);
-}
-
 // f_item = prod over the item's sets (<= K consecutive sets of one job) of ML(P_i, H(m_i)):
 // one shared f and one squaring per loop step for all K pairs.  Sets with errors or an
 // infinite point contribute 1.
@@ -205,21 +204,6 @@ __global__ void __launch_bounds__(LSG_TPB) k_miller_multi(int n_items, const int
   lane_store(f, item, miller_loop_multi<K>(Pk, Qk, use));
 }
 
-// f_g = ML(-G1, S_g) = conj(ML(G1, S_g)) written at slot n_items + g
-__global__ void __launch_bounds__(LSG_TPB) k_miller_groups(int ng, const uint32_t* __restrict__ S, size_t slot0,
-                                                            uint32_t* __restrict__ f) {
-  LANE_ITEM(ng);
-  g2p_t s = lane_load<g2p_t>(S, item);
-  fp12_t r = fp12_one();
-  if (!proj_is_inf(s)) {
-    g1a_t ng1;
-    ng1.x = fp_t(G1_GEN_X);
-    ng1.y = fp_t(G1_GEN_NEG_Y);
-    r = miller_loop(ng1, proj_to_aff(s));
-  }
-  lane_store(f, slot0 + item, r);
-}
-
 // one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy)
 template <int OP>
 __global__ void __launch_bounds__(LSG_TPB) k_tree_level(int n, const int32_t* __restrict__ ia,
@@ -242,23 +226,6 @@ __global__ void __launch_bounds__(LSG_TPB) k_tree_level(int n, const int32_t* __
   }
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_final_exp_check(int ng, const uint32_t* __restrict__ F,
-                                                              int32_t* __restrict__ verdict) {
-  LANE_ITEM(ng);
-  bool one = fp12_is_one(final_exp(lane_load<fp12_t>(F, item)));
-  if (lead) verdict[item] = one ? 1 : 0;
-}
-
-LSG_DEVI fp12_t fp12_from_canon_bytes(const uint8_t* b) {
-  fp12_t f;
-  fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-  for (int j = 0; j < 6; j++) {
-    c[j]->c0 = fp_to_mont(fp_from_be48(b + 96 * j));
-    c[j]->c1 = fp_to_mont(fp_from_be48(b + 96 * j + 48));
-  }
-  return f;
-}
-
 // partials: canonical big-endian 576-byte Fp12 blobs -> lane form (one item each)
 __global__ void __launch_bounds__(LSG_TPB) k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs,
                                                             uint32_t* __restrict__ out) {
@@ -269,13 +236,14 @@ __global__ void __launch_bounds__(LSG_TPB) k_blobs_to_fp12(int n, const uint8_t*
 __global__ void __launch_bounds__(LSG_TPB) k_fp12_to_canon(int n, const uint32_t* __restrict__ in,
                                                             uint8_t* __restrict__ out) {
   LANE_ITEM(n);
-  const fp12_t f = lane_load<fp12_t>(in, item);
-  const fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-  uint8_t* o = out + 576 * item;
-  for (int j = 0; j < 6; j++) {
-    fp_to_be48(o + 96 * j, fp_from_mont(c[j]->c0));
-    fp_to_be48(o + 96 * j + 48, fp_from_mont(c[j]->c1));
-  }
+  fp12_to_canon_bytes(out + 576 * item, lane_load<fp12_t>(in, item));
+}
+
+// group signature sums S_g (lane form) -> canonical 288-byte projective points for the row stage
+__global__ void __launch_bounds__(LSG_TPB) k_g2p_to_canon(int n, const uint32_t* __restrict__ in,
+                                                           uint8_t* __restrict__ out) {
+  LANE_ITEM(n);
+  g2p_to_canon_bytes(out + 288 * item, lane_load<g2p_t>(in, item));
 }
 
 __global__ void __launch_bounds__(LSG_TPB) k_g1p_to_bytes(int n, const uint32_t* __restrict__ pts,
@@ -378,8 +346,8 @@ namespace {
 
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
-constexpr int LSG_SLOTS = 6;   // batch / job slots in flight
-constexpr int LSG_FINALS = 4;  // final-exponentiation entries in flight
+constexpr int LSG_SLOTS = 16;  // batch / job slots in flight
+constexpr int LSG_FINALS = 8;  // final-exponentiation entries in flight
 
 // u32 words per item for each lane-form type
 constexpr size_t W_G1A = lane_words<g1a_t>();
@@ -473,6 +441,7 @@ struct Slot {
   DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_fall;
   // groups, reductions, outputs
   DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
+  DevBuf d_Sb, d_fgb, d_Fb;  // canonical blobs handed to / from the row-backend group stages
   TreeSlot tree[3];
   // Miller items: <= LSG_MILLER_K consecutive sets of one job share one multi-Miller loop
   std::vector<int32_t> item_host;  // [first..., count...]
@@ -596,6 +565,15 @@ void timer_end(Slot* s) {
   } while (0)
 #define LAUNCH(s, kern, items, ...) LAUNCH_T(s, #kern, kern, lane_blocks(items), LSG_TPB, __VA_ARGS__)
 
+// a row-backend stage (lsg_serial.hip) on the slot's current stream, timed like LAUNCH_T
+#define LAUNCH_ROW(s, name, call)                     \
+  do {                                                \
+    timer_begin((s), name);                           \
+    hipError_t _le = (call);                          \
+    timer_end((s));                                   \
+    if (_le != hipSuccess) return fail((s), name, _le); \
+  } while (0)
+
 int slot_create(lsg_ctx* c, Slot* s, int index, hipStream_t shared) {
   s->c = c;
   s->index = index;
@@ -637,7 +615,7 @@ void slot_destroy(Slot* s) {
   staged_free(&s->own);
   DevBuf* bufs[] = {&s->d_dst, &s->d_ub, &s->d_sigaff, &s->d_siginf, &s->d_seterr, &s->d_pkp, &s->d_pkerr,
                     &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
-                    &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux};
+                    &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux, &s->d_Sb, &s->d_fgb, &s->d_Fb};
   for (DevBuf* b : bufs) free_dev(*b);
   free_dev(s->d_items);
   for (TreeSlot& t : s->tree) {
@@ -938,17 +916,26 @@ int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool
     s->c->err = "internal: group buffers too small";
     return LSG_ERR_INVALID_ARG;
   }
-  s->cur = 1;
   int rc;
+  if ((rc = ensure(s, s->d_Sb, 288 * ng)) || (rc = ensure(s, s->d_fgb, 576 * ng)) || (rc = ensure(s, s->d_Fb, 576 * ng)))
+    return rc;
+  s->cur = 1;
   if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) return rc;
-  LAUNCH(s, k_miller_groups, ng, (int)ng, P_<uint32_t>(s->d_S), n, P_<uint32_t>(s->d_fall));
+  // f_g = ML(-G1, S_g) on the row backend, written at d_fall slot n_items + g
+  LAUNCH(s, k_g2p_to_canon, ng, (int)ng, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_Sb));
+  LAUNCH_ROW(s, "k_row_miller_neg_g1",
+             lsg_row_miller_neg_g1(S_(s), (int)ng, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
+  LAUNCH(s, k_blobs_to_fp12, ng, (int)ng, P_<uint8_t>(s->d_fgb), P_<uint32_t>(s->d_fall) + W_F12 * n);
   LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
   s->cur = 0;
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_grp, 0));
   std::vector<std::vector<int32_t>> fg = item_groups(s, groups);
   for (size_t g = 0; g < ng; g++) fg[g].push_back((int32_t)(n + g));
   if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_fall), fg, P_<uint32_t>(s->d_F)))) return rc;
-  if (fe) LAUNCH(s, k_final_exp_check, ng, (int)ng, P_<uint32_t>(s->d_F), P_<int32_t>(s->d_verdict));
+  if (fe) {
+    LAUNCH(s, k_fp12_to_canon, ng, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_Fb));
+    LAUNCH_ROW(s, "k_row_final_exp", lsg_row_final_exp(S_(s), (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
+  }
   return LSG_OK;
 }
 
@@ -1235,7 +1222,8 @@ int submit_final(Slot* s, const uint8_t* partials576, size_t n) {
     std::vector<std::vector<int32_t>> g(1);
     for (size_t k = 0; k < n; k++) g[0].push_back((int32_t)k);
     if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_aux), g, P_<uint32_t>(s->d_F)))) return rc;
-    LAUNCH(s, k_final_exp_check, 1, 1, P_<uint32_t>(s->d_F), P_<int32_t>(s->d_verdict));
+    LAUNCH(s, k_fp12_to_canon, 1, 1, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
+    LAUNCH_ROW(s, "k_row_final_exp", lsg_row_final_exp(S, 1, P_<uint8_t>(s->d_blob), P_<int32_t>(s->d_verdict)));
     LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4, hipMemcpyDeviceToHost, S));
     s->n_verdicts = 1;
   }
@@ -1316,7 +1304,8 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
   c->device = dev;
   bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&c->s_final, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < LSG_SLOTS && ok; i++) ok = slot_create(c, &c->slots[i], i, nullptr) == LSG_OK;
-  for (int i = 0; i < LSG_FINALS && ok; i++) ok = slot_create(c, &c->finals[i], i, c->s_final) == LSG_OK;
+  // each final exponentiation entry has its own stream: consecutive batches' FEs overlap
+  for (int i = 0; i < LSG_FINALS && ok; i++) ok = slot_create(c, &c->finals[i], i, nullptr) == LSG_OK;
   if (ok) ok = slot_create(c, &c->util, 0, c->s_final) == LSG_OK;
   if (!ok) {
     lsg_destroy(c);
@@ -1658,12 +1647,11 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
   Slot* s = &c->util;
   hipDeviceProp_t prop;
   LSG_HIP(s, hipGetDeviceProperties(&prop, c->device));
-  int items = prop.multiProcessorCount * 128;  // 32 waves of 4 rows per CU
+  int items = prop.multiProcessorCount * 32 * (64 / LSG_GROUP);  // 32 waves per CU
   int rc;
   if ((rc = ensure(s, s->d_aux, 4 * 16 * (size_t)items))) return rc;
   std::vector<uint32_t> init(16 * (size_t)items, 0);
-  for (size_t i = 0; i < init.size(); i++)
-    if ((i & 15) < 11) init[i] = (uint32_t)(i * 2654435761u);
+  for (size_t i = 0; i < init.size(); i += 4) init[i] = (uint32_t)(i * 2654435761u);  // small values < p
   LSG_HIP(s, hipMemcpy(s->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
   const int iters = 64;
   hipStream_t S = s->st[0];

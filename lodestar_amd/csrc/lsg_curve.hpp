@@ -260,17 +260,8 @@ LSG_INL proj_t<F> proj_mul_u64(const proj_t<F>& p, uint64_t k) {
   T[2] = gdbl(p);
 #pragma unroll 1
   for (int d = 3; d < 16; d++) T[d] = gadd(T[d - 1], p);
-  auto pick = [&](uint32_t d) {
-    proj_t<F> r = T[0];
-#pragma unroll
-    for (int j = 1; j < 16; j++) {
-      bool hit = d == (uint32_t)j;
-      r.X = fselect(hit, T[j].X, r.X);
-      r.Y = fselect(hit, T[j].Y, r.Y);
-      r.Z = fselect(hit, T[j].Z, r.Z);
-    }
-    return r;
-  };
+  // the digit is uniform over the lanes of one element: a per-lane indexed read of the table
+  auto pick = [&](uint32_t d) { return T[d]; };
   jac_t<F> acc = jac_from_proj(pick((uint32_t)(k >> 60) & 15u));
 #pragma unroll 1
   for (int w = 14; w >= 0; w--) {

@@ -20,6 +20,7 @@
 #include "lsg_constants.hpp"
 
 #define LSG_LANE_MODE 1
+#define LSG_GROUP 16  // lanes per field element
 // the generic layers built on this backend are device-only code
 #undef LSG_INL
 #define LSG_INL __device__ __forceinline__

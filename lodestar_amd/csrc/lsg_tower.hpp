@@ -257,12 +257,26 @@ LSG_INL fp6_t fp6_mul_fin(const fp2_t* V) {
   r.c2 = c2;
   return r;
 }
+#ifdef LSG_QUAD_MODE
+// Quad backend: an Fp takes three VGPRs, so the products are issued one Fp2 product (three
+// interleaved Montgomery chains) at a time instead of in wide batches; same values.
+LSG_BIGFN fp6_t fp6_mul(fp6_t a, fp6_t b) {
+  fp2_t v0 = fp2_mul(a.c0, b.c0);
+  fp2_t v1 = fp2_mul(a.c1, b.c1);
+  fp2_t v2 = fp2_mul(a.c2, b.c2);
+  fp2_t c0 = fp2_add(v0, fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), v1), v2)));
+  fp2_t c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), v0), v1), fp2_mul_xi(v2));
+  fp2_t c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), v0), v2), v1);
+  return fp6_make(c0, c1, c2);
+}
+#else
 LSG_BIGFN fp6_t fp6_mul(fp6_t a, fp6_t b) {
   fp2_t A[6], B[6], V[6];
   fp6_mul_prep(A, B, a, b);
   fp2_mul_n<6>(V, A, B);
   return fp6_mul_fin(V);
 }
+#endif
 
 LSG_INL fp6_t fp6_mul_v(const fp6_t& a) { return fp6_make(fp2_mul_xi(a.c2), a.c0, a.c1); }
 
@@ -304,6 +318,19 @@ LSG_INL bool fp12_is_one(const fp12_t& a) {
 }
 LSG_INL fp12_t fp12_conj(const fp12_t& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
+#ifdef LSG_QUAD_MODE
+LSG_BIGFN fp12_t fp12_mul(fp12_t a, fp12_t b) {
+  fp6_t t0 = fp6_mul(a.c0, b.c0);
+  fp6_t t1 = fp6_mul(a.c1, b.c1);
+  fp6_t t2 = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1));
+  return fp12_make(fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_sub(t2, t0), t1));
+}
+LSG_BIGFN fp12_t fp12_sqr(fp12_t a) {
+  fp6_t t = fp6_mul(a.c0, a.c1);
+  fp6_t u = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  return fp12_make(fp6_sub(fp6_sub(u, t), fp6_mul_v(t)), fp6_add(t, t));
+}
+#else
 // Karatsuba over Fp6: the three Fp6 products (18 Fp2 products) are issued as one batch
 LSG_BIGFN fp12_t fp12_mul(fp12_t a, fp12_t b) {
   fp2_t A[18], B[18], V[18];
@@ -324,6 +351,7 @@ LSG_BIGFN fp12_t fp12_sqr(fp12_t a) {
   fp6_t t = fp6_mul_fin(V), u = fp6_mul_fin(V + 6);
   return fp12_make(fp6_sub(fp6_sub(u, t), fp6_mul_v(t)), fp6_add(t, t));
 }
+#endif
 
 // (a + b t)^2 in Fp4 = Fp2[t]/(t^2 - xi)  -- oracle/pairing.py:_fp4_square
 LSG_INL void fp4_square(fp2_t& c0, fp2_t& c1, const fp2_t& a, const fp2_t& b) {
@@ -337,6 +365,12 @@ LSG_INL void fp4_square(fp2_t& c0, fp2_t& c1, const fp2_t& a, const fp2_t& b) {
 // (the three Fp4 squarings = 9 Fp2 squarings issued as one batch)
 LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
   fp2_t z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+#ifdef LSG_QUAD_MODE
+  fp2_t t0, t1, u0, u1, t2, t3;
+  fp4_square(t0, t1, z0, z1);
+  fp4_square(u0, u1, z2, z3);
+  fp4_square(t2, t3, z4, z5);
+#else
   fp2_t S[9], Q[9];
   S[0] = z0;
   S[1] = z1;
@@ -355,6 +389,7 @@ LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
   fp2_t u1 = fp2_sub(fp2_sub(Q[5], Q[3]), Q[4]);
   fp2_t t2 = fp2_add(fp2_mul_xi(Q[7]), Q[6]);
   fp2_t t3 = fp2_sub(fp2_sub(Q[8], Q[6]), Q[7]);
+#endif
   z0 = fp2_sub(t0, z0);
   z0 = fp2_add(fp2_add(z0, z0), t0);
   z1 = fp2_add(t1, z1);
@@ -377,6 +412,12 @@ LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
 // fp6_mul_01(f0, l00, l01), fp6_mul_01(f0 + f1, l00, l01 + l11) and fp6_mul_1(f1, l11):
 // 13 independent Fp2 products issued as one batch.
 LSG_BIGFN fp12_t fp12_mul_line(fp12_t f, fp2_t l00, fp2_t l01, fp2_t l11) {
+#ifdef LSG_QUAD_MODE
+  fp6_t t0 = fp6_mul_01(f.c0, l00, l01);
+  fp6_t u = fp6_mul_01(fp6_add(f.c0, f.c1), l00, fp2_add(l01, l11));
+  fp6_t t1 = fp6_mul_1(f.c1, l11);
+  return fp12_make(fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_sub(u, t0), t1));
+#else
   const fp6_t& a = f.c0;
   const fp6_t& c = f.c1;
   fp6_t s = fp6_add(f.c0, f.c1);
@@ -403,6 +444,7 @@ LSG_BIGFN fp12_t fp12_mul_line(fp12_t f, fp2_t l00, fp2_t l01, fp2_t l11) {
   fp6_t u = fp6_make(fp2_add(fp2_mul_xi(V[7]), V[5]), fp2_sub(fp2_sub(V[8], V[5]), V[6]), fp2_add(V[9], V[6]));
   fp6_t t1 = fp6_make(fp2_mul_xi(V[10]), V[11], V[12]);
   return fp12_make(fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_sub(u, t0), t1));
+#endif
 }
 
 LSG_BIGFN fp12_t fp12_inv(fp12_t a) {
