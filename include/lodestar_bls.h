@@ -164,6 +164,11 @@ int lsg_stage(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, l
 int lsg_staged_free(lsg_ctx* ctx, lsg_staged* staged);
 int lsg_batch_submit(lsg_ctx* ctx, const lsg_staged* staged, lsg_ticket* ticket);
 int lsg_batch_wait(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* set_err, int32_t* any_error);
+/* Several RLC batches in one submission: groups of group_size consecutive sets (the last may
+ * be shorter; 0 = one group) each get their own Miller partial, so the matching
+ * lsg_batch_wait writes ceil(n_sets / group_size) x 576 bytes.  One launch then carries the
+ * per-set work of every group, which keeps more waves in flight than one group per ticket. */
+int lsg_batch_submit_groups(lsg_ctx* ctx, const lsg_staged* staged, size_t group_size, lsg_ticket* ticket);
 /* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1).  The
  * submit/wait pair runs on the context's final stream, overlapping later batches. */
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);

@@ -77,7 +77,7 @@ EXPORTS = [
     "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
     "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
     "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
-    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots",
+    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups",
 ]
 
 
@@ -117,6 +117,7 @@ def load_library(path=LIB_PATH):
         lib.lsg_stage.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.POINTER(vp)]
         lib.lsg_staged_free.argtypes = [vp, vp]
         lib.lsg_batch_submit.argtypes = [vp, vp, pu64]
+        lib.lsg_batch_submit_groups.argtypes = [vp, vp, sz, pu64]
         lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
@@ -288,22 +289,28 @@ class Context:
         self._check(self.lib.lsg_stage(self.h, b.arr, b.n, seed, ctypes.byref(h)), "lsg_stage")
         return Staged(self, h, b.n)
 
-    def batch_submit(self, staged):
+    def batch_submit(self, staged, group_size=0):
+        """Submit a staged package; group_size > 0 splits it into RLC groups of that many
+        consecutive sets, each with its own partial.  None when every slot is busy."""
         t = ctypes.c_uint64()
-        rc = self.lib.lsg_batch_submit(self.h, staged.h, ctypes.byref(t))
+        rc = self.lib.lsg_batch_submit_groups(self.h, staged.h, int(group_size), ctypes.byref(t))
         if rc == LSG_ERR_BUSY:
             return None
-        self._check(rc, "lsg_batch_submit")
-        return (t.value, staged.n)
+        self._check(rc, "lsg_batch_submit_groups")
+        ng = 1 if group_size <= 0 or group_size >= staged.n else -(-staged.n // group_size)
+        return (t.value, staged.n, ng)
 
     def batch_wait(self, ticket):
-        """-> (partial 576 bytes, per-set error codes, any_error)"""
-        t, n = ticket
-        out = ctypes.create_string_buffer(576)
+        """-> (partial 576 bytes, per-set error codes, any_error); for a grouped submission the
+        first element is the list of the groups' partials"""
+        t, n, ng = ticket
+        out = ctypes.create_string_buffer(576 * ng)
         errs = (ctypes.c_int32 * max(n, 1))()
         anyerr = ctypes.c_int32()
         self._check(self.lib.lsg_batch_wait(self.h, t, out, errs, ctypes.byref(anyerr)), "lsg_batch_wait")
-        return out.raw, [errs[i] for i in range(n)], bool(anyerr.value)
+        raw = out.raw
+        parts = raw if ng == 1 else [raw[576 * g:576 * g + 576] for g in range(ng)]
+        return parts, [errs[i] for i in range(n)], bool(anyerr.value)
 
     def final_verify(self, partials):
         v = ctypes.c_int32()

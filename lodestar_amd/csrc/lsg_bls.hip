@@ -347,7 +347,7 @@ namespace {
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
 constexpr int LSG_SLOTS = 16;  // batch / job slots in flight
-constexpr int LSG_FINALS = 8;  // final-exponentiation entries in flight
+constexpr int LSG_FINALS = 16;  // final-exponentiation entries in flight
 
 // u32 words per item for each lane-form type
 constexpr size_t W_G1A = lane_words<g1a_t>();
@@ -450,6 +450,7 @@ struct Slot {
   DevBuf d_items;
   HostBuf h_err, h_pinf, h_pkerr, h_verdict, h_blob;  // pinned result mirrors
   size_t n_verdicts = 0;
+  size_t n_partials = 1;  // batch tickets: Miller partials produced
   std::vector<Timer> timers;
   size_t ntimers = 0;
   // ticket state
@@ -806,7 +807,7 @@ constexpr int LSG_MILLER_KMAX = 4;  // pairs per multi-Miller item: 1, 2 or 4 (e
 int miller_k() {
   static int k = [] {
     const char* e = getenv("LSG_MILLER_K");
-    int v = e ? atoi(e) : 2;
+    int v = e ? atoi(e) : 2;  // K=2 measured best on MI355X (profiles/r01_bench_sweeps.txt)
     return (v == 1 || v == 2 || v == 4) ? v : 2;
   }();
   return k;
@@ -1177,22 +1178,35 @@ int wait_jobs(lsg_ctx* c, Slot* s, lsg_job_result* results, lsg_stats* stats) {
 
 // per-shard Miller product over the slot's inputs (errored sets contribute identities, so
 // the partial covers exactly the valid sets; an empty package gives the identity)
-int submit_batch(Slot* s) {
+// per-group Miller products over the slot's inputs: groups of group_size consecutive sets
+// (errored sets contribute identities, so each partial covers exactly its valid sets; an
+// empty package gives one identity partial)
+int submit_batch(Slot* s, size_t group_size) {
   int rc;
-  if ((rc = size_state(s, 1))) return rc;
-  plan_items(s, {{(size_t)0, s->in->n_sets}});
+  const size_t n = s->in->n_sets;
+  if (group_size == 0 || group_size > n) group_size = std::max(n, (size_t)1);
+  size_t ng = std::max((n + group_size - 1) / group_size, (size_t)1);
+  if ((rc = size_state(s, ng))) return rc;
+  std::vector<std::pair<size_t, size_t>> ranges;
+  std::vector<std::vector<int32_t>> groups(ng);
+  for (size_t g = 0; g < ng; g++) {
+    size_t a = g * group_size, b = std::min(n, a + group_size);
+    if (a < b) ranges.push_back({a, b});
+    for (size_t i = a; i < b; i++) groups[g].push_back((int32_t)i);
+  }
+  plan_items(s, ranges);
   if ((rc = launch_set_stages(s))) return rc;
-  std::vector<std::vector<int32_t>> groups(1);
-  for (size_t i = 0; i < s->in->n_sets; i++) groups[0].push_back((int32_t)i);
   if ((rc = launch_groups(s, groups, false))) return rc;
-  LAUNCH(s, k_fp12_to_canon, 1, 1, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
-  LSG_HIP(s, hipMemcpyAsync(s->h_blob.p, s->d_blob.p, 576, hipMemcpyDeviceToHost, s->st[0]));
+  if ((rc = ensure(s, s->d_blob, 576 * ng)) || (rc = ensure_host(s, s->h_blob, 576 * ng))) return rc;
+  LAUNCH(s, k_fp12_to_canon, ng, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(s->h_blob.p, s->d_blob.p, 576 * ng, hipMemcpyDeviceToHost, s->st[0]));
+  s->n_partials = ng;
   return launch_readback(s, true, 0);
 }
 
 int wait_batch(Slot* s, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
   LSG_HIP(s, hipEventSynchronize(s->ev_done));
-  memcpy(out576, s->h_blob.p, 576);
+  memcpy(out576, s->h_blob.p, 576 * s->n_partials);
   SetStatus ss = read_status(s);
   *any_error = 0;
   for (size_t i = 0; i < s->in->n_sets; i++) {
@@ -1434,13 +1448,17 @@ int lsg_staged_free(lsg_ctx* c, lsg_staged* staged) {
 }
 
 int lsg_batch_submit(lsg_ctx* c, const lsg_staged* staged, lsg_ticket* ticket) {
+  return lsg_batch_submit_groups(c, staged, 0, ticket);
+}
+
+int lsg_batch_submit_groups(lsg_ctx* c, const lsg_staged* staged, size_t group_size, lsg_ticket* ticket) {
   if (!c || !staged || !ticket) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
   Slot* s = take_slot(c);
   if (!s) return LSG_ERR_BUSY;
   timer_reset(s);
   s->in = staged;
-  int rc = submit_batch(s);
+  int rc = submit_batch(s, group_size);
   if (rc) {
     sync_slot(s);
     return rc;
@@ -1474,7 +1492,7 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
     for (size_t i = 0; i < n_sets; i++) sp[i] = &sets[i];
     s->in = &s->own;
     int rc = stage_sets(s, &s->own, sp.data(), n_sets, seed, true, s->st[0]);
-    if (!rc) rc = submit_batch(s);
+    if (!rc) rc = submit_batch(s, 0);
     if (rc) {
       sync_slot(s);
       return rc;

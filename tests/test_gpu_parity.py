@@ -293,3 +293,22 @@ def test_node_host_on_gpu(ctx, tmp_path):
                        text=True, timeout=180)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_grouped_batch_submission(ctx):
+    """lsg_batch_submit_groups: one launch, three RLC groups, one partial per group."""
+    sets = [bd.single_set(600 + i) for i in range(20)]
+    bad = list(sets)
+    bad[13] = bd.corrupt_wrong_message(bad[13])  # group 1 (sets 8..15)
+    for pkg, expect in ((sets, [True, True, True]), (bad, [True, False, True])):
+        staged = ctx.stage(pkg, seed=31)
+        try:
+            t = ctx.batch_submit(staged, group_size=8)
+            parts, errs, anyerr = ctx.batch_wait(t)
+            assert len(parts) == 3 and not anyerr and errs == [0] * 20
+            assert [ctx.final_verify([p]) for p in parts] == expect
+            assert ctx.final_verify(parts) == all(expect)
+            whole, _, _ = ctx.batch_wait(ctx.batch_submit(staged))  # one group: product of the three
+            assert ctx.final_verify([whole]) == all(expect)
+        finally:
+            staged.free()
