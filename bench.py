@@ -74,8 +74,8 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="submissions in flight (<= library pipeline slots)")
@@ -142,8 +142,8 @@ def main():
             check(anyerr, True)
             if M == 1:
                 parts = [parts]
-            if capture and not pend_b and submitted == k_tickets:
-                times += ctx.last_kernel_times()
+            if capture:  # HIP-event kernel times of this ticket (recorded on the kernels' own streams)
+                times.append(ctx.last_kernel_times())
             fts = [ctx.final_submit(pg) for pg in gather(parts)]
             pend_f.append((fts, t_sub, anyerr))
             if submitted < k_tickets:
@@ -154,8 +154,6 @@ def main():
                 for tf0 in fts0:
                     check(ae, ctx.final_wait(tf0))
                 lat.append(time.perf_counter() - t0)
-        if capture:
-            times += ctx.last_kernel_times()
         return lat, times
 
     tickets = -(-args.steps // M)
@@ -178,11 +176,13 @@ def main():
     # the kernels ran on during the last timed batch
     opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
     probe_fp, probe_mad = ctx.probe_fp_mul_rate()
-    peak_mad = float(os.environ.get("LSG_PEAK_MAD_PER_S", "2.827e13"))  # measured v_mad_u64_u32 peak (profiles/)
+    peak_mad = ctx.probe_mad_peak()  # measured v_mad_u64_u32 issue rate of this GPU (k_probe_mad)
+    # per-ticket sum per kernel name (tree levels add up), averaged over the timed tickets
     agg = {}
-    for name, ms in ktimes:
-        agg[name] = agg.get(name, 0.0) + ms
-    stage_of = {"k_miller_multi": "miller", "k_hash_map": "hash_map", "k_sig_scale": "sig_scale",
+    for ticket_times in ktimes:
+        for name, ms in ticket_times:
+            agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
+    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_hash_map": "hash_map", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
     per_set = {k: v for k, v in agg.items() if k in stage_of}
     dom = max(per_set, key=per_set.get)

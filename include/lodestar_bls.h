@@ -184,6 +184,10 @@ int lsg_sk_to_pk(lsg_ctx* ctx, const uint8_t* sks32, size_t n, uint8_t* out96);
  * Montgomery multiplications; reports Fp-mul/s and v_mad_u64_u32/s (x300 per mul). */
 int lsg_probe_fp_mul_rate(lsg_ctx* ctx, double* fp_mul_per_s, double* mad_per_s);
 
+/* Integer-VALU peak probe: issue rate of v_mad_u64_u32 (16 independent accumulators per lane,
+ * 8 waves per SIMD) -- the roofline denominator bench.py reports. */
+int lsg_probe_mad_peak(lsg_ctx* ctx, double* mad_per_s);
+
 /* Per-kernel timing of the most recently completed ticket (or synchronous call), from HIP
  * events on the streams the kernels ran on: names[i] / ms[i] for up to max entries;
  * returns the count. */

@@ -77,7 +77,7 @@ EXPORTS = [
     "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
     "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
     "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
-    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups",
+    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups", "lsg_probe_mad_peak",
 ]
 
 
@@ -122,6 +122,7 @@ def load_library(path=LIB_PATH):
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
         lib.lsg_pipeline_slots.argtypes = [vp, pi32]
+        lib.lsg_probe_mad_peak.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         for name in EXPORTS:
             if name != "lsg_last_error":
                 getattr(lib, name).restype = ctypes.c_int
@@ -228,6 +229,11 @@ class Context:
         out = [(res[i].status, res[i].err_code) for i in range(n)]
         stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
         return out, stats
+
+    def probe_mad_peak(self):
+        v = ctypes.c_double()
+        self._check(self.lib.lsg_probe_mad_peak(self.h, ctypes.byref(v)), "lsg_probe_mad_peak")
+        return v.value
 
     def pipeline_slots(self):
         n = ctypes.c_int32()

@@ -333,6 +333,27 @@ __global__ void __launch_bounds__(LSG_TPB) k_probe_fp_mul(int n, int iters, uint
   lane_store(io, item, fp_add(fp_add(a, b), fp_add(c, d)));
 }
 
+// roofline probe: raw v_mad_u64_u32 issue rate, 16 independent 64-bit accumulators per lane
+__global__ void __launch_bounds__(256) k_probe_mad(int iters, uint32_t seed, uint64_t* __restrict__ io) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[16];
+  uint32_t x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    acc[k] = t + k;
+    x[k] = (t * 2654435761u) ^ (seed + 977u * k);
+  }
+  const uint32_t y = seed | 1u;
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = (uint64_t)x[k] * y + acc[k];
+  }
+  uint64_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) r ^= acc[k];
+  io[t] = r;
+}
+
 // ---------------------------------------------------------------------------- host side
 //
 // Pipelining.  A context owns LSG_SLOTS pipeline slots; each slot has two streams (main:
@@ -1689,6 +1710,34 @@ int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
   double muls = (double)items * iters * 4.0;
   *fp_mul_per_s = muls / (ms * 1e-3);
   *mad_per_s = *fp_mul_per_s * 300.0;
+  return LSG_OK;
+}
+
+int lsg_probe_mad_peak(lsg_ctx* c, double* mad_per_s) {
+  if (!c || !mad_per_s) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  hipDeviceProp_t prop;
+  LSG_HIP(s, hipGetDeviceProperties(&prop, c->device));
+  const int blocks = prop.multiProcessorCount * 32;  // 32 waves per CU (8 per SIMD)
+  const size_t threads = (size_t)blocks * 256;
+  int rc;
+  if ((rc = ensure(s, s->d_aux, 8 * threads))) return rc;
+  hipStream_t S = s->st[0];
+  const int iters = 4096;
+  hipLaunchKernelGGL(k_probe_mad, dim3(blocks), dim3(256), 0, S, 16, 3u, P_<uint64_t>(s->d_aux));
+  hipEvent_t a, b;
+  LSG_HIP(s, hipEventCreate(&a));
+  LSG_HIP(s, hipEventCreate(&b));
+  LSG_HIP(s, hipEventRecord(a, S));
+  hipLaunchKernelGGL(k_probe_mad, dim3(blocks), dim3(256), 0, S, iters, 5u, P_<uint64_t>(s->d_aux));
+  LSG_HIP(s, hipEventRecord(b, S));
+  LSG_HIP(s, hipEventSynchronize(b));
+  float ms = 0;
+  LSG_HIP(s, hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *mad_per_s = (double)threads * iters * 16.0 / (ms * 1e-3);
   return LSG_OK;
 }
 

@@ -168,6 +168,14 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
   lsg_mul_count = 0;
   fp12_t f = miller_loop(P, H);
   counts[6] = lsg_mul_count;
+  {  // the device runs the multi-Miller loop with K = 2 pairs per item: cost per set
+    g1a_t P2[2] = {P, P};
+    g2a_t H2[2] = {H, H};
+    bool use2[2] = {true, true};
+    lsg_mul_count = 0;
+    (void)miller_loop_multi<2>(P2, H2, use2);
+    counts[11] = lsg_mul_count / 2;
+  }
   lsg_mul_count = 0;
   (void)g2_add(rs, rs);
   counts[7] = lsg_mul_count;
