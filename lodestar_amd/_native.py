@@ -9,7 +9,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblodestar_bls.so")
+LIB_PATH = os.environ.get("LSG_LIB", os.path.join(HERE, "liblodestar_bls.so"))  # LSG_LIB: A/B builds
 
 LSG_OK = 0
 LSG_ERR_NO_DEVICE = 2

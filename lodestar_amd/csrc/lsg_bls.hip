@@ -16,8 +16,9 @@
 //   k_sig_subgroup    psi(P) == [x]P                                             [M2]
 //   k_pk_decode       48/96-byte pubkey -> projective G1 (on-curve only)         [H8]
 //   tree(G1 add)      per-set pubkey aggregation, pairwise over levels           [M1]
-//   k_pk_scale        P_i = [r_i] agg_i (affine)                                 [M4]
-//   k_hash_map        SSWU x2 -> 3-isogeny -> add -> clear_cofactor -> affine     [M3]
+//   k_pk_scale        P_i = [r_i] agg_i; batched 1/Z; k_pk_affine               [M4]
+//   k_h2c_prep/map/affine  hash_to_field -> SSWU x2 -> 3-isogeny -> add ->
+//                     clear_cofactor -> affine, inversions batched per stage       [M3]
 //   k_sig_scale       [r_i] sig_i                                                [M4]
 //   k_miller_sets     f_i = ML(P_i, H(m_i))                                      [M5]
 // then per group (an RLC batch = a chunk of batchable jobs, or one job):
@@ -130,44 +131,114 @@ __global__ void __launch_bounds__(LSG_TPB) k_pk_decode(int n, const uint8_t* __r
   if (lead) err[item] = e;
 }
 
-// P_i = [r_i] agg_i in affine (r_i == 0: no scaling); pinf = aggregate is infinity
+// ---- batched field inversion (Montgomery's trick as a product tree over the batch): every
+// field inversion of a stage -- 1/Z of the scaled pubkeys, 1/N(tv1) of the SSWU maps, 1/N(Z)
+// of the hashed points -- shares one exponentiation per batch instead of one per set.
+// Zero inputs (points at infinity, the SSWU exceptional case) are carried as 1 through the
+// tree and come out as 0, the value fp_inv(0) gives.
+// level up: out[i] = in[2i] * in[2i+1] (a missing right child is 1)
+__global__ void __launch_bounds__(LSG_TPB) k_binv_up(int n_out, int n_in, int zero_to_one,
+                                                      const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  LANE_ITEM(n_out);
+  const fp_t one = fp_one();
+  fp_t a = lane_load<fp_t>(in, 2 * item);
+  fp_t b = (2 * (int)item + 1 < n_in) ? lane_load<fp_t>(in, 2 * item + 1) : one;
+  if (zero_to_one) {
+    a = fp_select(fp_is_zero(a), one, a);
+    b = fp_select(fp_is_zero(b), one, b);
+  }
+  lane_store(out, item, fp_mul(a, b));
+}
+__global__ void __launch_bounds__(LSG_TPB) k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
+  LANE_ITEM(1);
+  lane_store(inv, 0, fp_inv(lane_load<fp_t>(top, 0)));
+}
+// level down: inv(child c) = inv(parent c/2) * value(sibling c^1); at level 0 (zero_to_one)
+// zero children get 0
+__global__ void __launch_bounds__(LSG_TPB) k_binv_down(int n_child, int zero_to_one, const uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ pinv, uint32_t* __restrict__ cinv) {
+  LANE_ITEM(n_child);
+  const fp_t one = fp_one();
+  const int sib = (int)item ^ 1;
+  fp_t s = sib < n_child ? lane_load<fp_t>(vals, sib) : one;
+  if (zero_to_one) s = fp_select(fp_is_zero(s), one, s);
+  fp_t r = fp_mul(lane_load<fp_t>(pinv, item >> 1), s);
+  if (zero_to_one) r = fp_select(fp_is_zero(lane_load<fp_t>(vals, item)), fp_zero(), r);
+  lane_store(cinv, item, r);
+}
+
+// P_i = [r_i] agg_i, projective (r_i == 0: no scaling); zP_i = its Z (0 at infinity) for the
+// batched inversion; pinf = aggregate is infinity
 __global__ void __launch_bounds__(LSG_TPB) k_pk_scale(int n, const uint32_t* __restrict__ agg,
-                                                       const uint64_t* __restrict__ rnd, uint32_t* __restrict__ P,
-                                                       uint8_t* __restrict__ pinf) {
+                                                       const uint64_t* __restrict__ rnd, uint32_t* __restrict__ Pp,
+                                                       uint32_t* __restrict__ zP, uint8_t* __restrict__ pinf) {
   LANE_ITEM(n);
   g1p_t acc = lane_load<g1p_t>(agg, item);
   uint64_t r = rnd[item];
   bool is_inf = proj_is_inf(acc);
   if (r != 0 && !is_inf) acc = proj_mul_u64(acc, r);
-  g1a_t a;
-  if (is_inf) {
-    a.x = fp_zero();
-    a.y = fp_zero();
-  } else {
-    a = proj_to_aff(acc);
-  }
-  lane_store(P, item, a);
+  lane_store(Pp, item, acc);
+  lane_store(zP, item, is_inf ? fp_zero() : acc.Z);
   if (lead) pinf[item] = is_inf ? 1 : 0;
 }
+// P_i affine = (X / Z, Y / Z) with 1/Z from the batched inversion
+__global__ void __launch_bounds__(LSG_TPB) k_pk_affine(int n, const uint32_t* __restrict__ Pp,
+                                                        const uint32_t* __restrict__ zinv, uint32_t* __restrict__ P) {
+  LANE_ITEM(n);
+  g1p_t p = lane_load<g1p_t>(Pp, item);
+  fp_t zi = lane_load<fp_t>(zinv, item);
+  g1a_t a;
+  fp_mul2(a.x, a.y, p.X, zi, p.Y, zi);
+  lane_store(P, item, a);
+}
 
-__global__ void __launch_bounds__(LSG_TPB) k_hash_map(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ H,
-                                                       uint8_t* __restrict__ hinf) {
+// hash_to_G2, stage 1: u0, u1 = hash_to_field(expand_message_xmd); norms N(tv1(u0)),
+// N(tv1(u1)) at slots 2i, 2i+1 for the batched inversion
+struct h2c_u_t {
+  fp2_t u0, u1;
+};
+__global__ void __launch_bounds__(LSG_TPB) k_h2c_prep(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ U,
+                                                       uint32_t* __restrict__ norms) {
   LANE_ITEM(n);
   const uint8_t* b = ub + 256 * item;
-  fp2_t u0 = fp2_make(fp_from_be64_mod(b), fp_from_be64_mod(b + 64));
-  fp2_t u1 = fp2_make(fp_from_be64_mod(b + 128), fp_from_be64_mod(b + 192));
-  g2p_t q = g2_add(iso_map3(map_to_curve_sswu(u0)), iso_map3(map_to_curve_sswu(u1)));
-  q = clear_cofactor_g2(q);
+  h2c_u_t u;
+  u.u0 = fp2_make(fp_from_be64_mod(b), fp_from_be64_mod(b + 64));
+  u.u1 = fp2_make(fp_from_be64_mod(b + 128), fp_from_be64_mod(b + 192));
+  lane_store(U, item, u);
+  lane_store(norms, 2 * item, fp2_norm(sswu_tv1(u.u0)));
+  lane_store(norms, 2 * item + 1, fp2_norm(sswu_tv1(u.u1)));
+}
+// stage 2: SSWU x2 (with the batched 1/N(tv1)) -> 3-isogeny -> add -> clear_cofactor,
+// projective; zN_i = N(Z) (0 at infinity) for the second batched inversion
+__global__ void __launch_bounds__(LSG_TPB) k_h2c_map(int n, const uint32_t* __restrict__ U,
+                                                      const uint32_t* __restrict__ ninv, uint32_t* __restrict__ Hp,
+                                                      uint32_t* __restrict__ zN, uint8_t* __restrict__ hinf) {
+  LANE_ITEM(n);
+  h2c_u_t u = lane_load<h2c_u_t>(U, item);
+  g2p_t q0 = iso_map3(map_to_curve_sswu_ni(u.u0, lane_load<fp_t>(ninv, 2 * item)));
+  g2p_t q1 = iso_map3(map_to_curve_sswu_ni(u.u1, lane_load<fp_t>(ninv, 2 * item + 1)));
+  g2p_t q = clear_cofactor_g2(g2_add(q0, q1));
   bool is_inf = proj_is_inf(q);
+  lane_store(Hp, item, q);
+  lane_store(zN, item, is_inf ? fp_zero() : fp2_norm(q.Z));
+  if (lead) hinf[item] = is_inf ? 1 : 0;
+}
+// stage 3: H affine = (X, Y) * conj(Z) / N(Z)   (= proj_to_aff, 1/Z = conj(Z) / N(Z))
+__global__ void __launch_bounds__(LSG_TPB) k_h2c_affine(int n, const uint32_t* __restrict__ Hp,
+                                                         const uint32_t* __restrict__ ninv, const uint8_t* __restrict__ hinf,
+                                                         uint32_t* __restrict__ H) {
+  LANE_ITEM(n);
+  g2p_t q = lane_load<g2p_t>(Hp, item);
   g2a_t a;
-  if (is_inf) {
+  if (hinf[item]) {
     a.x = fp2_zero();
     a.y = fp2_zero();
   } else {
-    a = proj_to_aff(q);
+    fp2_t zi = fp2_inv_with_norm_inv(q.Z, lane_load<fp_t>(ninv, item));
+    a.x = fp2_mul(q.X, zi);
+    a.y = fp2_mul(q.Y, zi);
   }
   lane_store(H, item, a);
-  if (lead) hinf[item] = is_inf ? 1 : 0;
 }
 
 __global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const uint32_t* __restrict__ sig_aff,
@@ -463,6 +534,10 @@ struct Slot {
   // groups, reductions, outputs
   DevBuf d_S, d_F, d_verdict, d_blob, d_aux;
   DevBuf d_Sb, d_fgb, d_Fb;  // canonical blobs handed to / from the row-backend group stages
+  // batched inversions: projective pubkeys and their Z; hash_to_field elements, SSWU norms,
+  // projective hashes and their norms; inverses; product-tree scratch per stream
+  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi;
+  DevBuf binv_lv[2], binv_iv[2];
   TreeSlot tree[3];
   // Miller items: <= LSG_MILLER_K consecutive sets of one job share one multi-Miller loop
   std::vector<int32_t> item_host;  // [first..., count...]
@@ -637,7 +712,9 @@ void slot_destroy(Slot* s) {
   staged_free(&s->own);
   DevBuf* bufs[] = {&s->d_dst, &s->d_ub, &s->d_sigaff, &s->d_siginf, &s->d_seterr, &s->d_pkp, &s->d_pkerr,
                     &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
-                    &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux, &s->d_Sb, &s->d_fgb, &s->d_Fb};
+                    &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux, &s->d_Sb, &s->d_fgb, &s->d_Fb,
+                    &s->d_Pp,  &s->d_zP, &s->d_zPi, &s->d_U, &s->d_nrm, &s->d_nrmi, &s->d_Hp, &s->d_zN, &s->d_zNi,
+                    &s->binv_lv[0], &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1]};
   for (DevBuf* b : bufs) free_dev(*b);
   free_dev(s->d_items);
   for (TreeSlot& t : s->tree) {
@@ -757,6 +834,57 @@ int size_state(Slot* s, size_t groups) {
       (rc = ensure_host(s, s->h_pkerr, 4 * np)) || (rc = ensure_host(s, s->h_verdict, 4 * std::max(groups, (size_t)1))) ||
       (rc = ensure_host(s, s->h_blob, 576)))
     return rc;
+  const size_t WF = lane_words<fp_t>();
+  if ((rc = ensure(s, s->d_Pp, 4 * W_G1P * nn)) || (rc = ensure(s, s->d_zP, 4 * WF * nn)) ||
+      (rc = ensure(s, s->d_zPi, 4 * WF * nn)) || (rc = ensure(s, s->d_U, 4 * lane_words<h2c_u_t>() * nn)) ||
+      (rc = ensure(s, s->d_nrm, 4 * WF * 2 * nn)) || (rc = ensure(s, s->d_nrmi, 4 * WF * 2 * nn)) ||
+      (rc = ensure(s, s->d_Hp, 4 * W_G2P * nn)) || (rc = ensure(s, s->d_zN, 4 * WF * nn)) ||
+      (rc = ensure(s, s->d_zNi, 4 * WF * nn)))
+    return rc;
+  return LSG_OK;
+}
+
+// out[i] = 1 / v[i] (0 for v[i] = 0) for n lane-form Fp values, on the slot's current stream:
+// a product tree up, one inversion at the root, products back down (Montgomery's trick).
+// ws selects the per-stream tree scratch.
+int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, uint32_t* out) {
+  if (n == 0) return LSG_OK;
+  const size_t WF = lane_words<fp_t>();
+  std::vector<size_t> sz{n}, off{0};
+  size_t total = 0;
+  do {
+    size_t m = (sz.back() + 1) / 2;
+    off.push_back(total);
+    sz.push_back(m);
+    total += m;
+  } while (sz.back() > 1);
+  int rc;
+  if ((rc = ensure(s, s->binv_lv[ws], 4 * WF * total)) || (rc = ensure(s, s->binv_iv[ws], 4 * WF * total))) return rc;
+  uint32_t* lv = P_<uint32_t>(s->binv_lv[ws]);
+  uint32_t* iv = P_<uint32_t>(s->binv_iv[ws]);
+  const size_t L = sz.size() - 1;  // levels above the inputs
+  auto lvl = [&](size_t k) { return k == 0 ? (uint32_t*)v : lv + WF * off[k]; };
+  for (size_t k = 1; k <= L; k++)
+    LAUNCH_T(s, name, k_binv_up, lane_blocks(sz[k]), LSG_TPB, (int)sz[k], (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1),
+             lvl(k));
+  LAUNCH_T(s, name, k_binv_root, 1, LSG_TPB, lvl(L), iv + WF * off[L]);
+  for (size_t k = L; k >= 1; k--)
+    LAUNCH_T(s, name, k_binv_down, lane_blocks(sz[k - 1]), LSG_TPB, (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1),
+             iv + WF * off[k], k == 1 ? out : iv + WF * off[k - 1]);
+  return LSG_OK;
+}
+
+// hash_to_G2 of the slot's n expanded messages (d_ub) into d_H / d_hinf, on the current
+// stream, with the field inversions batched over the n sets
+int launch_hash(Slot* s, int n) {
+  int rc;
+  LAUNCH(s, k_h2c_prep, n, n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrm));
+  if ((rc = batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)))) return rc;
+  LAUNCH(s, k_h2c_map, n, n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp),
+         P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf));
+  if ((rc = batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)))) return rc;
+  LAUNCH(s, k_h2c_affine, n, n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi), P_<uint8_t>(s->d_hinf),
+         P_<uint32_t>(s->d_H));
   return LSG_OK;
 }
 
@@ -883,8 +1011,13 @@ int launch_set_stages(Slot* s) {
     int rc = tree_reduce<0>(s, 1, "tree_g1_aggregate", P_<uint32_t>(s->d_pkp), in->sets_pks, P_<uint32_t>(s->d_agg));
     if (rc) return rc;
   }
-  LAUNCH(s, k_pk_scale, n, n, P_<uint32_t>(s->d_agg), P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_P),
-         P_<uint8_t>(s->d_pinf));
+  LAUNCH(s, k_pk_scale, n, n, P_<uint32_t>(s->d_agg), P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_Pp),
+         P_<uint32_t>(s->d_zP), P_<uint8_t>(s->d_pinf));
+  {
+    int rc = batch_inv(s, 1, "binv_pk", P_<uint32_t>(s->d_zP), (size_t)n, P_<uint32_t>(s->d_zPi));
+    if (rc) return rc;
+  }
+  LAUNCH(s, k_pk_affine, n, n, P_<uint32_t>(s->d_Pp), P_<uint32_t>(s->d_zPi), P_<uint32_t>(s->d_P));
   LAUNCH(s, k_sig_decode, n, n, P_<uint8_t>(in->d_sig), P_<uint32_t>(in->d_siglen), P_<uint32_t>(s->d_sigaff),
          P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
   LAUNCH(s, k_sig_subgroup, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
@@ -894,7 +1027,10 @@ int launch_set_stages(Slot* s) {
   s->cur = 0;
   LAUNCH_T(s, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(in->d_msg), P_<uint32_t>(in->d_msgoff),
            P_<uint32_t>(in->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN, P_<uint8_t>(s->d_ub));
-  LAUNCH(s, k_hash_map, n, n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf));
+  {
+    int rc = launch_hash(s, n);
+    if (rc) return rc;
+  }
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
   int ni = (int)s->n_items;
   if (ni <= 0 || s->item_host.size() != 2 * (size_t)ni) {
@@ -1297,8 +1433,7 @@ int util_hash(Slot* s, const uint8_t* msgs, uint32_t msg_len, size_t n, const ui
   LAUNCH_T(s, "k_expand_msg", k_expand_msg, (nn + 63) / 64, 64, nn, P_<uint8_t>(s->own.d_msg),
            P_<uint32_t>(s->own.d_msgoff), P_<uint32_t>(s->own.d_msglen), P_<uint8_t>(s->d_dst), dst_len,
            P_<uint8_t>(s->d_ub));
-  LAUNCH(s, k_hash_map, nn, nn, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf));
-  return LSG_OK;
+  return launch_hash(s, nn);
 }
 
 #define LSG_ENTER(c)                         \

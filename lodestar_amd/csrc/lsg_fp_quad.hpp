@@ -266,17 +266,34 @@ LSG_DEVI fp_t fp_add(const fp_t& a, const fp_t& b) { return quad_add(a, b); }
 LSG_DEVI fp_t fp_sub(const fp_t& a, const fp_t& b) { return quad_sub(a, b); }
 LSG_DEVI fp_t fp_neg(const fp_t& a) { return quad_sub(fp_zero(), a); }
 LSG_DEVI fp_t fp_mul(const fp_t& a, const fp_t& b) { return quad_mont_mul(a, b); }
+#ifndef LSG_QUAD_MUL_WIDTH
+#define LSG_QUAD_MUL_WIDTH 1  // chains per call: 1 keeps the leaf inside v0..v39
+#endif
 LSG_DEVI void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+#if LSG_QUAD_MUL_WIDTH >= 2
   lsg_fp2x_t r = quad_mont_mul2(a0, b0, a1, b1);
   r0 = r.a;
   r1 = r.b;
+#else
+  fp_t t = quad_mont_mul(a0, b0);
+  r1 = quad_mont_mul(a1, b1);
+  r0 = t;
+#endif
 }
 LSG_DEVI void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
                       const fp_t& a2, const fp_t& b2) {
+#if LSG_QUAD_MUL_WIDTH >= 3
   lsg_fp3x_t r = quad_mont_mul3(a0, b0, a1, b1, a2, b2);
   r0 = r.a;
   r1 = r.b;
   r2 = r.c;
+#else
+  fp_t t0 = quad_mont_mul(a0, b0);
+  fp_t t1 = quad_mont_mul(a1, b1);
+  r2 = quad_mont_mul(a2, b2);
+  r0 = t0;
+  r1 = t1;
+#endif
 }
 // nine products: three interleaved triples (three limbs x three chains per lane in flight)
 LSG_DEVI void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {

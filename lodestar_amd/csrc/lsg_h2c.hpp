@@ -169,12 +169,24 @@ LSG_INL fp_t fp_from_be64_mod(const uint8_t* b) {
 // where s1 = N(gx1)^((p+1)/4) is the candidate already computed.  The root of gx (x1 or
 // x2) then costs one more exponentiation.  The result equals RFC 9380's: the square root
 // is unique up to sign and the sign is fixed by sgn0 below.
-LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) {
+//
+// The one inversion, 1/tv1 = conj(tv1) / N(tv1), is split out so that a batch of sets can
+// share one field inversion for all its N(tv1) (Montgomery's trick, done by the caller):
+// sswu_tv1(u) gives tv1, and map_to_curve_sswu_ni(u, ni) finishes with ni = 1/N(tv1)
+// (ni = 0 when tv1 = 0, the exceptional case, as fp_inv(0) = 0 gives).
+LSG_INL fp2_t sswu_tv1(const fp2_t& u) {
+  fp2_t zu2 = fp2_mul(SSWU_Z, fp2_sqr(u));
+  return fp2_add(fp2_sqr(zu2), zu2);
+}
+LSG_INL fp2_t fp2_inv_with_norm_inv(const fp2_t& a, const fp_t& ni) {
+  return fp2_t(fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni)));
+}
+LSG_BIGFN g2a_t map_to_curve_sswu_ni(fp2_t u, fp_t ni) {
   fp2_t u2 = fp2_sqr(u);
   fp2_t zu2 = fp2_mul(SSWU_Z, u2);
   fp2_t tv1 = fp2_add(fp2_sqr(zu2), zu2);
   bool exc = fp2_is_zero(tv1);
-  fp2_t x1 = fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv(tv1)));
+  fp2_t x1 = fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv_with_norm_inv(tv1, ni)));
   x1 = fp2_select(exc, SSWU_B_OVER_ZA, x1);
   fp2_t gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
   fp2_t x2 = fp2_mul(zu2, x1);
@@ -190,6 +202,7 @@ LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) {
   r.y = y;
   return r;
 }
+LSG_BIGFN g2a_t map_to_curve_sswu(fp2_t u) { return map_to_curve_sswu_ni(u, fp_inv(fp2_norm(sswu_tv1(u)))); }
 
 // 3-isogeny E2' -> E2, projective output (X, Y, Z) = (xn yd, y yn xd, xd yd)
 LSG_BIGFN g2p_t iso_map3(g2a_t p) {
