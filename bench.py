@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=3, help="submissions in flight (<= library pipeline slots)")
+    ap.add_argument("--depth", type=int, default=4, help="submissions in flight (<= library pipeline slots)")
     ap.add_argument("--groups", type=int, default=4, help="batches (steps) per submission, verified as separate RLC groups")
     args = ap.parse_args()
 
@@ -182,7 +182,7 @@ def main():
     for ticket_times in ktimes:
         for name, ms in ticket_times:
             agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
-    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_hash_map": "hash_map", "k_sig_scale": "sig_scale",
+    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_h2c_map": "hash_map", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
     per_set = {k: v for k, v in agg.items() if k in stage_of}
     dom = max(per_set, key=per_set.get)

@@ -55,6 +55,12 @@ namespace {
 }  // namespace
 
 #define LSG_TPB 256  // threads per block
+// Register budget of the lane kernels: waves per SIMD the compiler must leave room for
+// (it spills beyond that).  See DESIGN.md section 4 for the measured trade-off.
+#ifndef LSG_WAVES_PER_EU
+#define LSG_WAVES_PER_EU 4
+#endif
+#define LSG_KERNEL_ATTR __launch_bounds__(LSG_TPB) __attribute__((amdgpu_waves_per_eu(LSG_WAVES_PER_EU)))
 #define LSG_ITEMS_PER_BLOCK (LSG_TPB / LSG_GROUP)
 
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
@@ -83,7 +89,7 @@ __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restr
   }
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_sig_decode(int n, const uint8_t* __restrict__ sig,
+__global__ void LSG_KERNEL_ATTR k_sig_decode(int n, const uint8_t* __restrict__ sig,
                                                          const uint32_t* __restrict__ sig_len,
                                                          uint32_t* __restrict__ sig_aff, uint8_t* __restrict__ inf,
                                                          int32_t* __restrict__ err) {
@@ -107,7 +113,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_sig_decode(int n, const uint8_t* __
   }
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_sig_subgroup(int n, const uint32_t* __restrict__ sig_aff,
+__global__ void LSG_KERNEL_ATTR k_sig_subgroup(int n, const uint32_t* __restrict__ sig_aff,
                                                            const uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
   LANE_ITEM(n);
   if (err[item] != 0 || inf[item]) return;
@@ -116,7 +122,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_sig_subgroup(int n, const uint32_t*
 }
 
 // pubkey -> projective G1 (infinity and undecodable keys become (0:1:0))
-__global__ void __launch_bounds__(LSG_TPB) k_pk_decode(int n, const uint8_t* __restrict__ pk,
+__global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ pk,
                                                         const uint32_t* __restrict__ pk_len, uint32_t* __restrict__ pkp,
                                                         int32_t* __restrict__ err) {
   LANE_ITEM(n);
@@ -137,7 +143,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_pk_decode(int n, const uint8_t* __r
 // Zero inputs (points at infinity, the SSWU exceptional case) are carried as 1 through the
 // tree and come out as 0, the value fp_inv(0) gives.
 // level up: out[i] = in[2i] * in[2i+1] (a missing right child is 1)
-__global__ void __launch_bounds__(LSG_TPB) k_binv_up(int n_out, int n_in, int zero_to_one,
+__global__ void LSG_KERNEL_ATTR k_binv_up(int n_out, int n_in, int zero_to_one,
                                                       const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
   LANE_ITEM(n_out);
   const fp_t one = fp_one();
@@ -149,13 +155,13 @@ __global__ void __launch_bounds__(LSG_TPB) k_binv_up(int n_out, int n_in, int ze
   }
   lane_store(out, item, fp_mul(a, b));
 }
-__global__ void __launch_bounds__(LSG_TPB) k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
+__global__ void LSG_KERNEL_ATTR k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
   LANE_ITEM(1);
   lane_store(inv, 0, fp_inv(lane_load<fp_t>(top, 0)));
 }
 // level down: inv(child c) = inv(parent c/2) * value(sibling c^1); at level 0 (zero_to_one)
 // zero children get 0
-__global__ void __launch_bounds__(LSG_TPB) k_binv_down(int n_child, int zero_to_one, const uint32_t* __restrict__ vals,
+__global__ void LSG_KERNEL_ATTR k_binv_down(int n_child, int zero_to_one, const uint32_t* __restrict__ vals,
                                                         const uint32_t* __restrict__ pinv, uint32_t* __restrict__ cinv) {
   LANE_ITEM(n_child);
   const fp_t one = fp_one();
@@ -169,7 +175,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_binv_down(int n_child, int zero_to_
 
 // P_i = [r_i] agg_i, projective (r_i == 0: no scaling); zP_i = its Z (0 at infinity) for the
 // batched inversion; pinf = aggregate is infinity
-__global__ void __launch_bounds__(LSG_TPB) k_pk_scale(int n, const uint32_t* __restrict__ agg,
+__global__ void LSG_KERNEL_ATTR k_pk_scale(int n, const uint32_t* __restrict__ agg,
                                                        const uint64_t* __restrict__ rnd, uint32_t* __restrict__ Pp,
                                                        uint32_t* __restrict__ zP, uint8_t* __restrict__ pinf) {
   LANE_ITEM(n);
@@ -182,7 +188,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_pk_scale(int n, const uint32_t* __r
   if (lead) pinf[item] = is_inf ? 1 : 0;
 }
 // P_i affine = (X / Z, Y / Z) with 1/Z from the batched inversion
-__global__ void __launch_bounds__(LSG_TPB) k_pk_affine(int n, const uint32_t* __restrict__ Pp,
+__global__ void LSG_KERNEL_ATTR k_pk_affine(int n, const uint32_t* __restrict__ Pp,
                                                         const uint32_t* __restrict__ zinv, uint32_t* __restrict__ P) {
   LANE_ITEM(n);
   g1p_t p = lane_load<g1p_t>(Pp, item);
@@ -197,7 +203,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_pk_affine(int n, const uint32_t* __
 struct h2c_u_t {
   fp2_t u0, u1;
 };
-__global__ void __launch_bounds__(LSG_TPB) k_h2c_prep(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ U,
+__global__ void LSG_KERNEL_ATTR k_h2c_prep(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ U,
                                                        uint32_t* __restrict__ norms) {
   LANE_ITEM(n);
   const uint8_t* b = ub + 256 * item;
@@ -210,7 +216,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_h2c_prep(int n, const uint8_t* __re
 }
 // stage 2: SSWU x2 (with the batched 1/N(tv1)) -> 3-isogeny -> add -> clear_cofactor,
 // projective; zN_i = N(Z) (0 at infinity) for the second batched inversion
-__global__ void __launch_bounds__(LSG_TPB) k_h2c_map(int n, const uint32_t* __restrict__ U,
+__global__ void LSG_KERNEL_ATTR k_h2c_map(int n, const uint32_t* __restrict__ U,
                                                       const uint32_t* __restrict__ ninv, uint32_t* __restrict__ Hp,
                                                       uint32_t* __restrict__ zN, uint8_t* __restrict__ hinf) {
   LANE_ITEM(n);
@@ -224,7 +230,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_h2c_map(int n, const uint32_t* __re
   if (lead) hinf[item] = is_inf ? 1 : 0;
 }
 // stage 3: H affine = (X, Y) * conj(Z) / N(Z)   (= proj_to_aff, 1/Z = conj(Z) / N(Z))
-__global__ void __launch_bounds__(LSG_TPB) k_h2c_affine(int n, const uint32_t* __restrict__ Hp,
+__global__ void LSG_KERNEL_ATTR k_h2c_affine(int n, const uint32_t* __restrict__ Hp,
                                                          const uint32_t* __restrict__ ninv, const uint8_t* __restrict__ hinf,
                                                          uint32_t* __restrict__ H) {
   LANE_ITEM(n);
@@ -241,7 +247,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_h2c_affine(int n, const uint32_t* _
   lane_store(H, item, a);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const uint32_t* __restrict__ sig_aff,
+__global__ void LSG_KERNEL_ATTR k_sig_scale(int n, const uint32_t* __restrict__ sig_aff,
                                                         const uint8_t* __restrict__ inf, const int32_t* __restrict__ err,
                                                         const uint64_t* __restrict__ rnd, uint32_t* __restrict__ rs) {
   LANE_ITEM(n);
@@ -254,7 +260,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_sig_scale(int n, const uint32_t* __
 // one shared f and one squaring per loop step for all K pairs.  Sets with errors or an
 // infinite point contribute 1.
 template <int K>
-__global__ void __launch_bounds__(LSG_TPB) k_miller_multi(int n_items, const int32_t* __restrict__ item_first,
+__global__ void LSG_KERNEL_ATTR k_miller_multi(int n_items, const int32_t* __restrict__ item_first,
                                                            const int32_t* __restrict__ item_cnt,
                                                            const uint32_t* __restrict__ P,
                                                            const uint8_t* __restrict__ pinf, const uint32_t* __restrict__ H,
@@ -277,7 +283,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_miller_multi(int n_items, const int
 
 // one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy)
 template <int OP>
-__global__ void __launch_bounds__(LSG_TPB) k_tree_level(int n, const int32_t* __restrict__ ia,
+__global__ void LSG_KERNEL_ATTR k_tree_level(int n, const int32_t* __restrict__ ia,
                                                          const int32_t* __restrict__ ib, const uint32_t* __restrict__ src,
                                                          uint32_t* __restrict__ dst) {
   LANE_ITEM(n);
@@ -298,26 +304,26 @@ __global__ void __launch_bounds__(LSG_TPB) k_tree_level(int n, const int32_t* __
 }
 
 // partials: canonical big-endian 576-byte Fp12 blobs -> lane form (one item each)
-__global__ void __launch_bounds__(LSG_TPB) k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs,
+__global__ void LSG_KERNEL_ATTR k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs,
                                                             uint32_t* __restrict__ out) {
   LANE_ITEM(n);
   lane_store(out, item, fp12_from_canon_bytes(blobs + 576 * item));
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_fp12_to_canon(int n, const uint32_t* __restrict__ in,
+__global__ void LSG_KERNEL_ATTR k_fp12_to_canon(int n, const uint32_t* __restrict__ in,
                                                             uint8_t* __restrict__ out) {
   LANE_ITEM(n);
   fp12_to_canon_bytes(out + 576 * item, lane_load<fp12_t>(in, item));
 }
 
 // group signature sums S_g (lane form) -> canonical 288-byte projective points for the row stage
-__global__ void __launch_bounds__(LSG_TPB) k_g2p_to_canon(int n, const uint32_t* __restrict__ in,
+__global__ void LSG_KERNEL_ATTR k_g2p_to_canon(int n, const uint32_t* __restrict__ in,
                                                            uint8_t* __restrict__ out) {
   LANE_ITEM(n);
   g2p_to_canon_bytes(out + 288 * item, lane_load<g2p_t>(in, item));
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_g1p_to_bytes(int n, const uint32_t* __restrict__ pts,
+__global__ void LSG_KERNEL_ATTR k_g1p_to_bytes(int n, const uint32_t* __restrict__ pts,
                                                            uint8_t* __restrict__ out) {
   LANE_ITEM(n);
   g1p_t p = lane_load<g1p_t>(pts, item);
@@ -332,7 +338,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_g1p_to_bytes(int n, const uint32_t*
   g1_serialize(out + 96 * item, a, inf);
 }
 
-__global__ void __launch_bounds__(LSG_TPB) k_g2a_to_bytes(int n, const uint32_t* __restrict__ pts,
+__global__ void LSG_KERNEL_ATTR k_g2a_to_bytes(int n, const uint32_t* __restrict__ pts,
                                                            const uint8_t* __restrict__ inf, uint8_t* __restrict__ out) {
   LANE_ITEM(n);
   g2_serialize(out + 192 * item, lane_load<g2a_t>(pts, item), inf[item] != 0);
@@ -357,7 +363,7 @@ __device__ proj_t<F> proj_mul_be256(const proj_t<F>& p, const uint8_t* k) {
 }
 
 // sig_i = [sk_i] H(m_i), ZCash-compressed (bench/test input generation; not on the verify path)
-__global__ void __launch_bounds__(LSG_TPB) k_sign(int n, const uint8_t* __restrict__ sks, const uint32_t* __restrict__ H,
+__global__ void LSG_KERNEL_ATTR k_sign(int n, const uint8_t* __restrict__ sks, const uint32_t* __restrict__ H,
                                                    uint8_t* __restrict__ out96) {
   LANE_ITEM(n);
   g2p_t s = proj_mul_be256(proj_from_aff(lane_load<g2a_t>(H, item)), sks + 32 * item);
@@ -373,7 +379,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_sign(int n, const uint8_t* __restri
 }
 
 // pk_i = [sk_i] G1, uncompressed 96 bytes (bench/test input generation)
-__global__ void __launch_bounds__(LSG_TPB) k_sk_to_pk(int n, const uint8_t* __restrict__ sks,
+__global__ void LSG_KERNEL_ATTR k_sk_to_pk(int n, const uint8_t* __restrict__ sks,
                                                        uint8_t* __restrict__ out96) {
   LANE_ITEM(n);
   g1a_t g;
@@ -392,7 +398,7 @@ __global__ void __launch_bounds__(LSG_TPB) k_sk_to_pk(int n, const uint8_t* __re
 }
 
 // roofline probe: 4 independent limb-parallel Montgomery chains per row
-__global__ void __launch_bounds__(LSG_TPB) k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
+__global__ void LSG_KERNEL_ATTR k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
   LANE_ITEM(n);
   fp_t a = lane_load<fp_t>(io, item), b = fp_t(FP_R2), c = fp_t(FP_R3), d = fp_t(FP_HALF);
   for (int k = 0; k < iters; k++) {
