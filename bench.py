@@ -74,12 +74,12 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--sets-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=4, help="submissions in flight (<= library pipeline slots)")
-    ap.add_argument("--groups", type=int, default=4, help="batches (steps) per submission, verified as separate RLC groups")
+    ap.add_argument("--groups", type=int, default=6, help="batches (steps) per submission, verified as separate RLC groups")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

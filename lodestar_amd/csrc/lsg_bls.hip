@@ -445,7 +445,8 @@ namespace {
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
 constexpr int LSG_SLOTS = 16;  // batch / job slots in flight
-constexpr int LSG_FINALS = 16;  // final-exponentiation entries in flight
+constexpr int LSG_FINALS = 64;  // final-exponentiation entries in flight
+constexpr int LSG_FE_STREAMS = 8;  // streams the final exponentiations run on
 
 // u32 words per item for each lane-form type
 constexpr size_t W_G1A = lane_words<g1a_t>();
@@ -567,7 +568,8 @@ struct lsg_ctx {
   int device = 0;
   std::mutex mu;
   std::string err;
-  hipStream_t s_final = nullptr;  // final exponentiations + utility calls
+  hipStream_t s_final = nullptr;  // utility calls
+  hipStream_t s_fe[LSG_FE_STREAMS] = {};  // final exponentiations (entries share these round-robin)
   Slot slots[LSG_SLOTS];
   Slot finals[LSG_FINALS];
   Slot util;
@@ -1169,11 +1171,11 @@ Slot* free_slot(lsg_ctx* c, Slot* pool, int n) {
 uint64_t make_ticket(lsg_ctx* c, Slot* s, int kind) {
   s->kind = kind;
   s->serial = c->next_serial++;
-  return (s->serial << 8) | ((uint64_t)kind << 4) | (uint64_t)s->index;
+  return (s->serial << 16) | ((uint64_t)kind << 8) | (uint64_t)s->index;
 }
 
 Slot* ticket_slot(lsg_ctx* c, uint64_t t, int kind) {
-  int k = (int)((t >> 4) & 15), i = (int)(t & 15);
+  int k = (int)((t >> 8) & 255), i = (int)(t & 255);
   if (k != kind) return nullptr;
   Slot* s = nullptr;
   if (kind == SLOT_FINAL) {
@@ -1181,7 +1183,7 @@ Slot* ticket_slot(lsg_ctx* c, uint64_t t, int kind) {
   } else if (i < LSG_SLOTS) {
     s = &c->slots[i];
   }
-  if (!s || s->kind != kind || s->serial != (t >> 8)) return nullptr;
+  if (!s || s->kind != kind || s->serial != (t >> 16)) return nullptr;
   return s;
 }
 
@@ -1481,7 +1483,9 @@ int lsg_init(int device_ordinal, lsg_ctx** out) {
   bool ok = hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&c->s_final, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < LSG_SLOTS && ok; i++) ok = slot_create(c, &c->slots[i], i, nullptr) == LSG_OK;
   // each final exponentiation entry has its own stream: consecutive batches' FEs overlap
-  for (int i = 0; i < LSG_FINALS && ok; i++) ok = slot_create(c, &c->finals[i], i, nullptr) == LSG_OK;
+  for (int i = 0; i < LSG_FE_STREAMS && ok; i++)
+    ok = hipStreamCreateWithFlags(&c->s_fe[i], hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < LSG_FINALS && ok; i++) ok = slot_create(c, &c->finals[i], i, c->s_fe[i % LSG_FE_STREAMS]) == LSG_OK;
   if (ok) ok = slot_create(c, &c->util, 0, c->s_final) == LSG_OK;
   if (!ok) {
     lsg_destroy(c);
@@ -1498,6 +1502,8 @@ int lsg_destroy(lsg_ctx* c) {
   for (Slot& s : c->finals) slot_destroy(&s);
   slot_destroy(&c->util);
   if (c->s_final) (void)hipStreamDestroy(c->s_final);
+  for (hipStream_t st : c->s_fe)
+    if (st) (void)hipStreamDestroy(st);
   delete c;
   return LSG_OK;
 }
@@ -1565,7 +1571,7 @@ int lsg_pipeline_slots(lsg_ctx* c, int32_t* n) {
 int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
   if (!c || !done) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
-  Slot* s = ticket_slot(c, ticket, (int)((ticket >> 4) & 15));
+  Slot* s = ticket_slot(c, ticket, (int)((ticket >> 8) & 255));
   if (!s) return LSG_ERR_INVALID_ARG;
   hipError_t e = hipEventQuery(s->ev_done);
   if (e == hipErrorNotReady) {

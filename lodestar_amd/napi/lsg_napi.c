@@ -277,7 +277,7 @@ static napi_value js_submit_jobs(napi_env env, napi_callback_info info) {
     } else if (rc != LSG_OK) {
       throw_lsg(env, ctx, "lsg_submit_jobs", rc);
     } else {
-      /* tickets are serial << 8 | kind << 4 | slot: exact in a double for 2^45 submissions */
+      /* tickets are serial << 16 | kind << 8 | slot: exact in a double for 2^37 submissions */
       napi_value o;
       napi_create_object(env, &o);
       set_int(env, o, "ticket", (int64_t)t);
