@@ -153,3 +153,38 @@ def sign(sk, msg):
 
 def sk_to_pk(sk):
     return E1.mul(G1_GEN, sk)
+
+
+def batch_partial(sets, rands):
+    """Per-shard half of verify_multiple for the node-sharded path, with the
+    device's conventions (lodestar_amd/csrc/lsg_bls.hip submit_batch): sets whose signature
+    does not decode (or whose key is infinite) contribute 1 and are reported by error code.
+    sets: list of (pk_bytes, msg, sig_bytes).  Returns (partial Fp12, [error codes])."""
+    from .curves import BlstError as _BE
+    gt = F12_ONE
+    S = None
+    errs = []
+    for (pkb, msg, sigb), r in zip(sets, rands):
+        try:
+            sig = signature_from_bytes(sigb, True)
+            pk = public_key_from_bytes(pkb)
+            if pk is None:
+                raise _BE(BLST_PK_IS_INFINITY)
+        except _BE as e:
+            errs.append(e.code)
+            continue
+        errs.append(0)
+        if sig is not None:
+            S = E2.add(S, E2.mul(sig, r))
+        gt = f12_mul(gt, miller_loop_fast(E1.mul(pk, r), hash_to_g2(msg)))
+    if S is not None:
+        gt = f12_mul(gt, f12_conj(miller_loop_fast(G1_GEN, S)))
+    return gt, errs
+
+
+def final_verify_partials(partials):
+    """prod(partials) -> final exponentiation == 1 (one FE for the whole node)."""
+    gt = F12_ONE
+    for p in partials:
+        gt = f12_mul(gt, p)
+    return bool(partials) and f12_is_one(final_exp_fast(gt))

@@ -152,16 +152,33 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
   lsg_mul_count = 0;
   g1_deserialize(pk, inf, pk96, 96);
   counts[2] = lsg_mul_count;
+  g1a_t P = proj_to_aff(proj_mul_u64(proj_from_aff(pk), r));  // value (inversion not counted:)
   lsg_mul_count = 0;
-  g1a_t P = proj_to_aff(proj_mul_u64(proj_from_aff(pk), r));
-  counts[3] = lsg_mul_count;
+  {  // device: projective [r]PK, 1/Z from the batched inversion (3 M per element), 2 M to affine
+    g1p_t Pp = proj_mul_u64(proj_from_aff(pk), r);
+    fp_t zi = fp_one();
+    (void)fp_mul(Pp.X, zi);
+    (void)fp_mul(Pp.Y, zi);
+  }
+  counts[3] = lsg_mul_count + 3;
   uint8_t ub[256];
   expand_message_xmd_256(ub, msg32, 32, (const uint8_t*)"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_", 43);
-  lsg_mul_count = 0;
   fp2_t u0 = fp2_make(fp_from_be64_mod(ub), fp_from_be64_mod(ub + 64));
   fp2_t u1 = fp2_make(fp_from_be64_mod(ub + 128), fp_from_be64_mod(ub + 192));
   g2a_t H = proj_to_aff(clear_cofactor_g2(g2_add(iso_map3(map_to_curve_sswu(u0)), iso_map3(map_to_curve_sswu(u1)))));
-  counts[4] = lsg_mul_count;
+  lsg_mul_count = 0;
+  {  // device stages k_h2c_prep / k_h2c_map / k_h2c_affine; the three inversions per set are
+     // batched (3 M per inverted element)
+    fp2_t v0 = fp2_make(fp_from_be64_mod(ub), fp_from_be64_mod(ub + 64));
+    fp2_t v1 = fp2_make(fp_from_be64_mod(ub + 128), fp_from_be64_mod(ub + 192));
+    fp_t n0 = fp2_norm(sswu_tv1(v0)), n1 = fp2_norm(sswu_tv1(v1));
+    g2p_t q = clear_cofactor_g2(g2_add(iso_map3(map_to_curve_sswu_ni(v0, n0)), iso_map3(map_to_curve_sswu_ni(v1, n1))));
+    fp_t zn = fp2_norm(q.Z);
+    fp2_t zi = fp2_inv_with_norm_inv(q.Z, zn);
+    (void)fp2_mul(q.X, zi);
+    (void)fp2_mul(q.Y, zi);
+  }
+  counts[4] = lsg_mul_count + 9;
   lsg_mul_count = 0;
   g2p_t rs = proj_mul_u64(proj_from_aff(s), r);
   counts[5] = lsg_mul_count;

@@ -312,3 +312,24 @@ def test_grouped_batch_submission(ctx):
             assert ctx.final_verify([whole]) == all(expect)
         finally:
             staged.free()
+
+
+def test_sharded_verifier_gpu_backend(ctx):
+    """lodestar_amd/sharded.py on one GPU: node check passes for a valid package; a corrupted
+    set localises to this rank and the per-job fallback matches the worker.ts verdicts."""
+    from lodestar_amd.sharded import ShardedVerifier, GpuBackend
+    sv = ShardedVerifier(GpuBackend(ctx))
+    jobs = [([bd.single_set(800 + 3 * j + k, tag="sv") for k in range(1 + j % 3)], 1) for j in range(6)]
+    ok = sv.verify_jobs(jobs, seed=5)
+    assert ok.combined_ok and [r[0] for r in ok.results] == [1] * 6
+    bad = list(jobs)
+    s = list(bad[4][0])
+    s[0] = bd.corrupt_wrong_message(s[0])
+    bad[4] = (s, 1)
+    t = list(bad[1][0])
+    t[1] = bd.corrupt_truncate(t[1])
+    bad[1] = (t, 1)
+    out = sv.verify_jobs(bad, seed=5)
+    exp, _ = oracle_job_results(bad)
+    assert not out.combined_ok and out.retried_ranks == [0]
+    assert [r[0] for r in out.results] == [e[0] for e in exp]
