@@ -360,7 +360,7 @@ class Context:
         self._check(self.lib.lsg_probe_fp_mul_rate(self.h, ctypes.byref(a), ctypes.byref(b)), "lsg_probe_fp_mul_rate")
         return a.value, b.value
 
-    def last_kernel_times(self, max_entries=64):
+    def last_kernel_times(self, max_entries=1024):
         names = (ctypes.c_char_p * max_entries)()
         ms = (ctypes.c_double * max_entries)()
         n = self.lib.lsg_last_kernel_times(self.h, names, ms, max_entries)
