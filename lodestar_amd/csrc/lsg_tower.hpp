@@ -22,19 +22,40 @@ LSG_INL fp_t fp_to_mont(const fp_t& a) { return fp_mul(a, fp_t(FP_R2)); }
 LSG_INL fp_t fp_from_mont(const fp_t& a) { return fp_mul(a, fp_t(FP_ONE_CANON)); }
 LSG_INL fp_t fp_from_be48(const uint8_t* b) { return fp_from_be_bytes(b, 12); }
 
-// a^e for a fixed public exponent (MSB-first square-and-multiply; uniform branches)
+// a^e for a fixed public exponent e (12 little-endian words): left-to-right sliding window
+// of width 4 over the odd powers a, a^3, ..., a^15.  For the 379-381-bit exponents of the
+// square roots and inversions that is ~380 squarings and ~75 multiplications instead of
+// ~380 + popcount(e) (~190).  The window schedule depends on e only, so every lane of a
+// wave takes the same branches; the table entry is picked with selects (no indexed
+// register access).
 LSG_BIGFN fp_t fp_pow_fixed(fp_t a, const uint32_t* e) {
+  fp_t T[8];  // T[k] = a^(2k+1)
+  T[0] = a;
+  const fp_t a2 = fp_sqr(a);
+#pragma unroll
+  for (int k = 1; k < 8; k++) T[k] = fp_mul(T[k - 1], a2);
+  int i = 383;
+  while (i >= 0 && !((e[i >> 5] >> (i & 31)) & 1u)) i--;
   fp_t r = fp_one();
   bool started = false;
-  for (int w = 11; w >= 0; w--) {
-    uint32_t word = e[w];
-    for (int b = 31; b >= 0; b--) {
-      if (started) r = fp_sqr(r);
-      if ((word >> b) & 1u) {
-        r = started ? fp_mul(r, a) : a;
-        started = true;
-      }
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {  // started: the top bit is a window
+      r = fp_sqr(r);
+      i--;
+      continue;
     }
+    int j = i - 3 < 0 ? 0 : i - 3;  // window e[i..j] ends in a set bit
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) j++;
+    uint32_t v = 0;
+    for (int t = i; t >= j; t--) v = (v << 1) | ((e[t >> 5] >> (t & 31)) & 1u);
+    if (started)
+      for (int t = i; t >= j; t--) r = fp_sqr(r);
+    fp_t tv = T[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) tv = fp_select(v == (uint32_t)(2 * k + 1), T[k], tv);
+    r = started ? fp_mul(r, tv) : tv;
+    started = true;
+    i = j - 1;
   }
   return r;
 }
