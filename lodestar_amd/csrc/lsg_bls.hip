@@ -281,7 +281,8 @@ __global__ void LSG_KERNEL_ATTR k_miller_multi(int n_items, const int32_t* __res
   lane_store(f, item, miller_loop_multi<K>(Pk, Qk, use));
 }
 
-// one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy)
+// one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy;
+// ia < 0: the identity, for an empty group)
 template <int OP>
 __global__ void LSG_KERNEL_ATTR k_tree_level(int n, const int32_t* __restrict__ ia,
                                                          const int32_t* __restrict__ ib, const uint32_t* __restrict__ src,
@@ -289,18 +290,39 @@ __global__ void LSG_KERNEL_ATTR k_tree_level(int n, const int32_t* __restrict__ 
   LANE_ITEM(n);
   int32_t a = ia[item], b = ib[item];
   if (OP == 0) {
-    g1p_t x = lane_load<g1p_t>(src, a);
+    g1p_t x = a >= 0 ? lane_load<g1p_t>(src, a) : proj_inf<fp_t>();
     if (b >= 0) x = g1_add(x, lane_load<g1p_t>(src, b));
     lane_store(dst, item, x);
   } else if (OP == 1) {
-    g2p_t x = lane_load<g2p_t>(src, a);
+    g2p_t x = a >= 0 ? lane_load<g2p_t>(src, a) : proj_inf<fp2_t>();
     if (b >= 0) x = g2_add(x, lane_load<g2p_t>(src, b));
     lane_store(dst, item, x);
   } else {
-    fp12_t x = lane_load<fp12_t>(src, a);
+    fp12_t x = a >= 0 ? lane_load<fp12_t>(src, a) : fp12_one();
     if (b >= 0) x = fp12_mul(x, lane_load<fp12_t>(src, b));
     lane_store(dst, item, x);
   }
+}
+
+// Signature points for the bucket MSM: projective sig_i, or the identity for a set whose
+// signature did not decode or is the point at infinity (same contribution as k_sig_scale's)
+__global__ void LSG_KERNEL_ATTR k_sig_proj(int n, const uint32_t* __restrict__ sig_aff,
+                                                       const uint8_t* __restrict__ inf, const int32_t* __restrict__ err,
+                                                       uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  g2p_t r = proj_inf<fp2_t>();
+  if (err[item] == 0 && !inf[item]) r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
+  lane_store(out, item, r);
+}
+
+// S_g = sum_k 2^k C[64 g + k]: Horner over the 64 per-bit partial sums of one RLC group
+// (63 doublings and 63 additions, complete formulas)
+__global__ void LSG_KERNEL_ATTR k_msm_horner(int ng, const uint32_t* __restrict__ C, uint32_t* __restrict__ S) {
+  LANE_ITEM(ng);
+  g2p_t acc = lane_load<g2p_t>(C, 64 * item + 63);
+#pragma unroll 1
+  for (int k = 62; k >= 0; k--) acc = g2_add(g2_dbl(acc), lane_load<g2p_t>(C, 64 * item + k));
+  lane_store(S, item, acc);
 }
 
 // partials: canonical big-endian 576-byte Fp12 blobs -> lane form (one item each)
@@ -488,6 +510,65 @@ struct TreeSlot {
   std::vector<int32_t> host;  // index pairs of the last reduction (alive until the slot completes)
 };
 
+// Index plan of a segmented pairwise reduction (see tree_reduce): per level, the pairs
+// (ia[k], ib[k]) of the level's inputs; the last level gathers one value per group.
+struct TreePlan {
+  std::vector<int32_t> idx;                       // per level: ia[cnt] then ib[cnt]
+  std::vector<std::pair<size_t, size_t>> levels;  // (offset into idx, cnt)
+  size_t max_level = 0;
+};
+
+TreePlan plan_tree(const std::vector<std::vector<int32_t>>& groups) {
+  TreePlan P;
+  size_t ng = groups.size();
+  std::vector<std::vector<int32_t>> cur = groups;
+  for (;;) {
+    bool done = true;
+    for (auto& g : cur)
+      if (g.size() > 1) done = false;
+    size_t cnt = 0;
+    std::vector<int32_t> ia, ib;
+    std::vector<std::vector<int32_t>> nxt(ng);
+    if (done) {  // final gather into out[g] (an empty group gets the identity)
+      for (size_t g = 0; g < ng; g++) {
+        ia.push_back(!cur[g].empty() ? cur[g][0] : -1);
+        ib.push_back(-1);
+      }
+      cnt = ng;
+    } else {
+      for (size_t g = 0; g < ng; g++) {
+        for (size_t k = 0; k < cur[g].size(); k += 2) {
+          ia.push_back(cur[g][k]);
+          ib.push_back(k + 1 < cur[g].size() ? cur[g][k + 1] : -1);
+          nxt[g].push_back((int32_t)cnt++);
+        }
+      }
+    }
+    P.levels.push_back({P.idx.size(), cnt});
+    P.idx.insert(P.idx.end(), ia.begin(), ia.end());
+    P.idx.insert(P.idx.end(), ib.begin(), ib.end());
+    P.max_level = std::max(P.max_level, cnt);
+    if (done) break;
+    cur.swap(nxt);
+  }
+  return P;
+}
+
+// Bucket MSM plan of the RLC signature sums of one staged package split into groups of
+// group_size consecutive sets (Pippenger, 8-bit windows, planned on the host from the
+// known randomizers r_i):
+//   bucket (g, w, d), d = 1..255: the sets i of group g whose w-th byte of r_i is d
+//   bit (g, k = 8w + j): the buckets (g, w, d) whose digit d has bit j set
+// so that sum_i r_i sig_i = sum_k 2^k bit(g, k) (k_msm_horner).  Device copies of the index
+// plans are kept with the package and shared by every ticket that submits it.
+struct MsmPlan {
+  size_t group_size = 0, ng = 0;
+  bool valid = false;
+  TreePlan buckets, bits;
+  DevBuf d_buckets, d_bits;
+};
+constexpr int MSM_WINDOWS = 8, MSM_DIGITS = 255, MSM_BITS = 64;
+
 // chunkifyMaximizeChunkSize (multithread/utils.ts:4-19)
 std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk) {
   std::vector<std::pair<size_t, size_t>> out;
@@ -510,6 +591,8 @@ struct lsg_staged {
   size_t n_sets = 0, n_pks = 0;
   std::vector<uint32_t> pk_cnt;
   std::vector<std::vector<int32_t>> sets_pks;  // per set: indices of its pubkeys
+  std::vector<uint64_t> rnd;                   // per set: the RLC randomizer r_i
+  mutable MsmPlan msm;                         // bucket plan of the last grouping submitted
 };
 
 namespace {
@@ -545,7 +628,11 @@ struct Slot {
   // projective hashes and their norms; inverses; product-tree scratch per stream
   DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi;
   DevBuf binv_lv[2], binv_iv[2];
-  TreeSlot tree[3];
+  // tree scratch: [0] Fp12 products (main stream), [1] pubkey aggregation, [2] signature sums,
+  // [3] [4] MSM buckets and bit sums (side stream)
+  TreeSlot tree[5];
+  DevBuf d_bkt, d_bits;  // MSM buckets and per-bit partial sums (lane-form G2, projective)
+  bool msm = false;      // signature sums of this package by bucket MSM (else per-set [r_i] sig_i)
   // Miller items: <= LSG_MILLER_K consecutive sets of one job share one multi-Miller loop
   std::vector<int32_t> item_host;  // [first..., count...]
   std::vector<int32_t> set_item;   // set -> item
@@ -710,6 +797,9 @@ void free_host(HostBuf& b) {
 void staged_free(lsg_staged* in) {
   DevBuf* bufs[] = {&in->d_sig, &in->d_siglen, &in->d_msg, &in->d_msgoff, &in->d_msglen, &in->d_pk, &in->d_pklen, &in->d_rnd};
   for (DevBuf* b : bufs) free_dev(*b);
+  free_dev(in->msm.d_buckets);
+  free_dev(in->msm.d_bits);
+  in->msm.valid = false;
   free_host(in->h_arena);
 }
 
@@ -722,7 +812,7 @@ void slot_destroy(Slot* s) {
                     &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
                     &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux, &s->d_Sb, &s->d_fgb, &s->d_Fb,
                     &s->d_Pp,  &s->d_zP, &s->d_zPi, &s->d_U, &s->d_nrm, &s->d_nrmi, &s->d_Hp, &s->d_zN, &s->d_zNi,
-                    &s->binv_lv[0], &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1]};
+                    &s->binv_lv[0], &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_bkt, &s->d_bits};
   for (DevBuf* b : bufs) free_dev(*b);
   free_dev(s->d_items);
   for (TreeSlot& t : s->tree) {
@@ -775,6 +865,8 @@ int stage_sets(Slot* s, lsg_staged* in, const lsg_set* const* sets, size_t n, ui
   rnd[0] = 0;
   in->pk_cnt.assign(n, 0);
   in->sets_pks.assign(n, {});
+  in->rnd.assign(n, 0);
+  in->msm.valid = false;
   size_t mo = 0, po = 0;
   uint64_t sd = seed;
   FILE* ur = nullptr;
@@ -807,6 +899,7 @@ int stage_sets(Slot* s, lsg_staged* in, const lsg_set* const* sets, size_t n, ui
       } while (r == 0);
     }
     rnd[i] = r;
+    in->rnd[i] = r;
   }
   if (ur) fclose(ur);
   if ((rc = ensure(s, in->d_sig, 192 * nn)) || (rc = ensure(s, in->d_siglen, 4 * nn)) ||
@@ -901,62 +994,107 @@ int launch_hash(Slot* s, int n) {
 // out[g].  All levels' index pairs are built on the host and uploaded once; each level is
 // one launch over all pairs of all groups.  `ts` selects private scratch so that trees on
 // different streams can run concurrently.
+// Runs a planned reduction (plan_tree) on the current stream: each level is one launch over
+// all pairs of all groups; d_idx holds the plan's index pairs on the device.
 template <int OP>
-int tree_reduce(Slot* s, int ts, const char* name, const uint32_t* src,
-                const std::vector<std::vector<int32_t>>& groups, uint32_t* out) {
-  size_t ng = groups.size();
-  if (ng == 0) return LSG_OK;
+int run_tree(Slot* s, int ts, const char* name, const TreePlan& P, const int32_t* d_idx, const uint32_t* src,
+             uint32_t* out) {
   TreeSlot& T = s->tree[ts];
   size_t W = OP == 0 ? W_G1P : (OP == 1 ? W_G2P : W_F12);
-  std::vector<std::vector<int32_t>> cur = groups;
-  std::vector<int32_t>& idx = T.host;
-  idx.clear();
-  std::vector<std::pair<size_t, size_t>> levels;  // (offset into idx, count)
-  size_t max_level = 0;
-  for (;;) {
-    bool done = true;
-    for (auto& g : cur)
-      if (g.size() > 1) done = false;
-    size_t cnt = 0;
-    std::vector<int32_t> ia, ib;
-    std::vector<std::vector<int32_t>> nxt(ng);
-    if (done) {  // final gather into out[g]
-      for (size_t g = 0; g < ng; g++) {
-        ia.push_back(!cur[g].empty() ? cur[g][0] : -1);
-        ib.push_back(-1);
-      }
-      cnt = ng;
-    } else {
-      for (size_t g = 0; g < ng; g++) {
-        for (size_t k = 0; k < cur[g].size(); k += 2) {
-          ia.push_back(cur[g][k]);
-          ib.push_back(k + 1 < cur[g].size() ? cur[g][k + 1] : -1);
-          nxt[g].push_back((int32_t)cnt++);
-        }
-      }
-    }
-    levels.push_back({idx.size(), cnt});
-    idx.insert(idx.end(), ia.begin(), ia.end());
-    idx.insert(idx.end(), ib.begin(), ib.end());
-    max_level = std::max(max_level, cnt);
-    if (done) break;
-    cur.swap(nxt);
-  }
   int rc;
-  if ((rc = ensure(s, T.idx, 4 * idx.size())) || (rc = ensure(s, T.tA, 4 * W * max_level)) ||
-      (rc = ensure(s, T.tB, 4 * W * max_level)))
-    return rc;
-  LSG_HIP(s, hipMemcpyAsync(T.idx.p, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, S_(s)));
+  if ((rc = ensure(s, T.tA, 4 * W * P.max_level)) || (rc = ensure(s, T.tB, 4 * W * P.max_level))) return rc;
   const uint32_t* in = src;
   uint32_t* bufs[2] = {P_<uint32_t>(T.tA), P_<uint32_t>(T.tB)};
-  for (size_t L = 0; L < levels.size(); L++) {
-    size_t off = levels[L].first, cnt = levels[L].second;
-    bool last = L + 1 == levels.size();
+  for (size_t L = 0; L < P.levels.size(); L++) {
+    size_t off = P.levels[L].first, cnt = P.levels[L].second;
+    bool last = L + 1 == P.levels.size();
     uint32_t* dst = last ? out : bufs[L & 1];
-    const int32_t* ia = P_<int32_t>(T.idx) + off;
+    const int32_t* ia = d_idx + off;
     LAUNCH_T(s, name, k_tree_level<OP>, lane_blocks(cnt), LSG_TPB, (int)cnt, ia, ia + cnt, in, dst);
     in = dst;
   }
+  return LSG_OK;
+}
+
+// Segmented pairwise reduction of lane-form values on the current stream: for each group,
+// combine the slots groups[g] of `src` (OP 0: G1 add, 1: G2 add, 2: Fp12 mul) into dense
+// out[g].  All levels' index pairs are built on the host and uploaded once; each level is
+// one launch over all pairs of all groups.  `ts` selects private scratch so that trees on
+// different streams can run concurrently.
+template <int OP>
+int tree_reduce(Slot* s, int ts, const char* name, const uint32_t* src,
+                const std::vector<std::vector<int32_t>>& groups, uint32_t* out) {
+  if (groups.empty()) return LSG_OK;
+  TreeSlot& T = s->tree[ts];
+  TreePlan P = plan_tree(groups);
+  T.host.swap(P.idx);  // the async upload reads it; kept until the slot's next reduction
+  int rc;
+  if ((rc = ensure(s, T.idx, 4 * T.host.size()))) return rc;
+  LSG_HIP(s, hipMemcpyAsync(T.idx.p, T.host.data(), 4 * T.host.size(), hipMemcpyHostToDevice, S_(s)));
+  return run_tree<OP>(s, ts, name, P, P_<int32_t>(T.idx), src, out);
+}
+
+// Minimum RLC group size for the bucket MSM (env LSG_MSM_MIN_GROUP, read per submission):
+// below ~150 sets the fixed cost of 2040 buckets and 64 bit sums per group exceeds the
+// per-set scalar multiplications it replaces.
+size_t msm_min_group() {
+  const char* e = getenv("LSG_MSM_MIN_GROUP");
+  long v = e ? atol(e) : 256;
+  return v < 1 ? 1 : (size_t)v;
+}
+
+// The staged package's MSM plan for groups of group_size consecutive sets (built once per
+// package and grouping; the device index copies are shared by every ticket that uses it)
+int msm_plan(Slot* s, const lsg_staged* in, size_t group_size, size_t ng) {
+  MsmPlan& M = in->msm;
+  if (M.valid && M.group_size == group_size && M.ng == ng) return LSG_OK;
+  M.valid = false;
+  const size_t n = in->n_sets;
+  const size_t nb = (size_t)MSM_WINDOWS * MSM_DIGITS;
+  std::vector<std::vector<int32_t>> buckets(ng * nb), bits(ng * MSM_BITS);
+  for (size_t i = 0; i < n; i++) {
+    size_t g = i / group_size;
+    uint64_t r = in->rnd[i];
+    for (int w = 0; w < MSM_WINDOWS; w++) {
+      uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
+      if (d) buckets[g * nb + (size_t)w * MSM_DIGITS + d - 1].push_back((int32_t)i);
+    }
+  }
+  for (size_t g = 0; g < ng; g++)
+    for (int w = 0; w < MSM_WINDOWS; w++)
+      for (int j = 0; j < 8; j++)
+        for (uint32_t d = 1; d <= 255; d++)
+          if ((d >> j) & 1u) bits[g * MSM_BITS + 8 * w + j].push_back((int32_t)(g * nb + (size_t)w * MSM_DIGITS + d - 1));
+  M.buckets = plan_tree(buckets);
+  M.bits = plan_tree(bits);
+  int rc;
+  if ((rc = ensure(s, M.d_buckets, 4 * M.buckets.idx.size())) || (rc = ensure(s, M.d_bits, 4 * M.bits.idx.size())))
+    return rc;
+  LSG_HIP(s, hipMemcpy(M.d_buckets.p, M.buckets.idx.data(), 4 * M.buckets.idx.size(), hipMemcpyHostToDevice));
+  LSG_HIP(s, hipMemcpy(M.d_bits.p, M.bits.idx.data(), 4 * M.bits.idx.size(), hipMemcpyHostToDevice));
+  M.group_size = group_size;
+  M.ng = ng;
+  M.valid = true;
+  return LSG_OK;
+}
+
+// S_g = sum_{i in g} r_i sig_i for the planned groups, from the projective sig_i in d_rs
+// (k_sig_proj), on the current stream: bucket tree, bit tree, Horner.  About 8 point
+// additions per set (one per nonzero window digit) plus ~8.2k per group, against ~60
+// doublings and 16 additions per set for [r_i] sig_i.
+int msm_sum(Slot* s, const MsmPlan& M, uint32_t* out) {
+  const size_t ng = M.ng;
+  int rc;
+  if ((rc = ensure(s, s->d_bkt, 4 * W_G2P * ng * MSM_WINDOWS * MSM_DIGITS)) ||
+      (rc = ensure(s, s->d_bits, 4 * W_G2P * ng * MSM_BITS)))
+    return rc;
+  if ((rc = run_tree<1>(s, 3, "msm_buckets", M.buckets, P_<int32_t>(M.d_buckets), P_<uint32_t>(s->d_rs),
+                        P_<uint32_t>(s->d_bkt))))
+    return rc;
+  if ((rc = run_tree<1>(s, 4, "msm_bits", M.bits, P_<int32_t>(M.d_bits), P_<uint32_t>(s->d_bkt),
+                        P_<uint32_t>(s->d_bits))))
+    return rc;
+  LAUNCH(s, k_msm_horner, ng, (int)ng, P_<uint32_t>(s->d_bits), out);
   return LSG_OK;
 }
 
@@ -1030,8 +1168,12 @@ int launch_set_stages(Slot* s) {
          P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
   LAUNCH(s, k_sig_subgroup, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
   LSG_HIP(s, hipEventRecord(s->ev_sig, s->st[1]));  // pubkeys scaled, signature errors known
-  LAUNCH(s, k_sig_scale, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr),
-         P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_rs));
+  if (s->msm)  // the groups' sums come from the bucket MSM over the unscaled points
+    LAUNCH(s, k_sig_proj, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr),
+           P_<uint32_t>(s->d_rs));
+  else
+    LAUNCH(s, k_sig_scale, n, n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr),
+           P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_rs));
   s->cur = 0;
   LAUNCH_T(s, "k_expand_msg", k_expand_msg, (n + 63) / 64, 64, n, P_<uint8_t>(in->d_msg), P_<uint32_t>(in->d_msgoff),
            P_<uint32_t>(in->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN, P_<uint8_t>(s->d_ub));
@@ -1086,7 +1228,11 @@ int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool
   if ((rc = ensure(s, s->d_Sb, 288 * ng)) || (rc = ensure(s, s->d_fgb, 576 * ng)) || (rc = ensure(s, s->d_Fb, 576 * ng)))
     return rc;
   s->cur = 1;
-  if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) return rc;
+  if (s->msm) {  // planned by submit_batch for exactly these groups
+    if ((rc = msm_sum(s, s->in->msm, P_<uint32_t>(s->d_S)))) return rc;
+  } else if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) {
+    return rc;
+  }
   // f_g = ML(-G1, S_g) on the row backend, written at d_fall slot n_items + g
   LAUNCH(s, k_g2p_to_canon, ng, (int)ng, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_Sb));
   LAUNCH_ROW(s, "k_row_miller_neg_g1",
@@ -1258,6 +1404,7 @@ int submit_jobs(lsg_ctx* c, Slot* s, const lsg_job* jobs, size_t n_jobs, uint64_
     P.group_is_chunk.push_back(false);
   }
   s->in = &s->own;
+  s->msm = false;  // job groups are small (<= 128 sets) and are re-summed per job on retry
   int rc;
   if ((rc = stage_sets(s, &s->own, flat.data(), flat.size(), seed, true, s->st[0]))) return rc;
   if ((rc = size_state(s, std::max(P.groups.size(), n_jobs)))) return rc;
@@ -1360,6 +1507,8 @@ int submit_batch(Slot* s, size_t group_size) {
     for (size_t i = a; i < b; i++) groups[g].push_back((int32_t)i);
   }
   plan_items(s, ranges);
+  s->msm = n > 0 && std::min(group_size, n - (ng - 1) * group_size) >= msm_min_group();
+  if (s->msm && (rc = msm_plan(s, s->in, group_size, ng))) return rc;
   if ((rc = launch_set_stages(s))) return rc;
   if ((rc = launch_groups(s, groups, false))) return rc;
   if ((rc = ensure(s, s->d_blob, 576 * ng)) || (rc = ensure_host(s, s->h_blob, 576 * ng))) return rc;

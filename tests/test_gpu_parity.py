@@ -333,3 +333,60 @@ def test_sharded_verifier_gpu_backend(ctx):
     exp, _ = oracle_job_results(bad)
     assert not out.combined_ok and out.retried_ranks == [0]
     assert [r[0] for r in out.results] == [e[0] for e in exp]
+
+
+def _splitmix_rands(seed, n):
+    """The randomizers lsg_stage / lsg_batch_partial derive from a nonzero seed
+    (lsg_bls.hip stage_sets: splitmix64, zero draws skipped)."""
+    M = (1 << 64) - 1
+    s, out = seed, []
+    while len(out) < n:
+        s = (s + 0x9E3779B97F4A7C15) & M
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        if z:
+            out.append(z)
+    return out
+
+
+def _f12_bytes(f):
+    from oracle.fields import f12_coeffs
+    return b"".join(int(c[0]).to_bytes(48, "big") + int(c[1]).to_bytes(48, "big") for c in f12_coeffs(f))
+
+
+def test_msm_signature_sums_match_scalar_path(ctx, monkeypatch):
+    """Bucket MSM (lsg_bls.hip msm_sum) vs per-set [r_i] sig_i: identical partials per group,
+    including an infinite and an undecodable signature (identity contributions)."""
+    sets = [bd.single_set(700 + i, tag="msm") for i in range(40)]
+    sets[5] = bd.corrupt_infinity(sets[5])
+    sets[22] = bd.corrupt_truncate(sets[22])
+    sets[31] = bd.corrupt_wrong_message(sets[31])
+    staged = ctx.stage(sets, seed=1234)
+    try:
+        out = {}
+        for mode, thr in (("msm", "1"), ("scalar", "1000000")):
+            monkeypatch.setenv("LSG_MSM_MIN_GROUP", thr)
+            parts, errs, anyerr = ctx.batch_wait(ctx.batch_submit(staged, group_size=20))
+            out[mode] = parts
+            assert anyerr and errs[22] == 10 and errs[5] == 0
+        assert out["msm"] == out["scalar"]
+        assert [ctx.final_verify([p]) for p in out["msm"]] == [False, False]  # 5: infinity sig; 31: wrong msg
+    finally:
+        staged.free()
+
+
+def test_batch_partial_bit_exact_vs_oracle(ctx, monkeypatch):
+    """The per-shard Miller product (SURVEY 8e partial) equals the oracle's, byte for byte,
+    with the same randomizers, through the MSM signature sum."""
+    monkeypatch.setenv("LSG_MSM_MIN_GROUP", "1")
+    sets = [bd.single_set(760 + i, tag="msm") for i in range(7)]
+    sets[2] = bd.corrupt_infinity(sets[2])
+    sets[4] = bd.corrupt_not_in_group(sets[4])
+    seed = 4242
+    part, errs, anyerr = ctx.batch_partial(sets, seed=seed)
+    rands = _splitmix_rands(seed, len(sets))
+    exp, exp_errs = ov.batch_partial([(p[0], m, s) for p, m, s in sets], rands)
+    assert errs == exp_errs and anyerr
+    assert part == _f12_bytes(exp)
