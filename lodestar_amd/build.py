@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
 SOURCES = ["lsg_bls.hip", "lsg_serial.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
-           "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_quad.hpp", "lsg_io.hpp", "lsg_serial.h"]
+           "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_quad.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp", "lsg_serial.h"]
 
 
 def hipcc():

@@ -45,10 +45,12 @@
 // The math headers go into an anonymous namespace: lsg_serial.hip instantiates the same
 // generic code over the row backend, and the two fp_t must never be merged at link time.
 namespace {
-#ifdef LSG_BACKEND_ROW
+#if defined(LSG_BACKEND_ROW)
 #include "lsg_fp_lane.hpp"  // one element per 16-lane DPP row
+#elif defined(LSG_BACKEND_QUAD)
+#include "lsg_fp_quad.hpp"  // one element per 4-lane quad, fully reduced 32-bit limbs
 #else
-#include "lsg_fp_quad.hpp"  // one element per 4-lane quad (default)
+#include "lsg_fp_pair.hpp"  // one element per lane pair, lazy radix-2^29 limbs (default)
 #endif
 #include "lsg_h2c.hpp"
 #include "lsg_io.hpp"
@@ -58,7 +60,11 @@ namespace {
 // Register budget of the lane kernels: waves per SIMD the compiler must leave room for
 // (it spills beyond that).  See DESIGN.md section 4 for the measured trade-off.
 #ifndef LSG_WAVES_PER_EU
+#ifdef LSG_PAIR_MODE
+#define LSG_WAVES_PER_EU 2  // pair: 256 VGPRs (1.32M vs 1.15M sets/s at 3, 1.06M at 4)
+#else
 #define LSG_WAVES_PER_EU 4
+#endif
 #endif
 #define LSG_KERNEL_ATTR __launch_bounds__(LSG_TPB) __attribute__((amdgpu_waves_per_eu(LSG_WAVES_PER_EU)))
 #define LSG_ITEMS_PER_BLOCK (LSG_TPB / LSG_GROUP)

@@ -57,6 +57,7 @@ LSG_INL fp_t fp_sub(const fp_t& a, const fp_t& b) {
 }
 
 LSG_INL fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
+LSG_INL fp_t fp_canonical(const fp_t& a) { return a; }  // values are kept fully reduced
 
 #ifdef LSG_COUNT_MULS  // host build only: exact Fp-multiplication counts per stage
 extern unsigned long long lsg_mul_count;

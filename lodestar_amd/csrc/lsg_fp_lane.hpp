@@ -205,6 +205,7 @@ LSG_DEVI fp_t fp_select(bool c, const fp_t& a, const fp_t& b) { return fp_t(c ? 
 LSG_DEVI fp_t fp_add(const fp_t& a, const fp_t& b) { return fp_t(lane_add(a.v, b.v)); }
 LSG_DEVI fp_t fp_sub(const fp_t& a, const fp_t& b) { return fp_t(lane_sub(a.v, b.v)); }
 LSG_DEVI fp_t fp_neg(const fp_t& a) { return fp_t(lane_sub(0u, a.v)); }
+LSG_DEVI fp_t fp_canonical(const fp_t& a) { return a; }  // values are kept fully reduced
 LSG_DEVI fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_t(lane_mont_mul(a.v, b.v)); }
 LSG_DEVI void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
   lsg_u32x16 x, y;

@@ -1,0 +1,384 @@
+// Pair backend: 381-bit Montgomery arithmetic with one Fp element per lane PAIR.
+//
+// Representation: 14 signed limbs of 29 bits (radix 2^29, Montgomery R = 2^406); lane h
+// (0/1) of a pair holds limbs 7h..7h+6, so a wave64 carries 32 field elements.  Values are
+// LAZY: an fp_t is any integer congruent to the element, |v| < 2^12 p, with every limb in
+// [-8, 2^29 + 8) except the signed top limb (limb 13).  Nothing is reduced mod p except
+// where a canonical value is needed (equality, zero tests, serialisation), so
+//   fp_add / fp_sub / fp_neg  = one limb-wise add + one parallel carry round (no carry
+//                               chains, no comparisons, no cross-lane lookahead)
+//   fp_mul                    = CIOS over radix 2^29: the 64-bit accumulators never carry
+//                               (|t| < 28 * 2^58 < 2^63), so every partial product is one
+//                               v_mad_i64_i32; per step one DPP broadcast of b_i, one of m,
+//                               and one 32-bit DPP move of the retiring limb.  For inputs
+//                               |a|, |b| < 2^12.6 p the output satisfies |w| < 2p.
+// Measured (tools/micro/probe_fpmul.hip, profiles/r01_fpmul_probe.txt): 4.26e10 Fp-mul/s on
+// MI355X at 4 waves/SIMD against 2.86e10 for the quad backend (lsg_fp_quad.hpp): about 760
+// lane-instructions per product instead of 1360, and an addition costs ~30 per lane.
+//
+// LSG_PAIR_G = 1 builds the same arithmetic for one "lane" holding all 14 limbs (no DPP):
+// the host build (tests/native/hostcheck.hip) runs it on the CPU so the lazy bounds, the
+// radix-2^29 constants and the byte conversions are checked against the oracle without a GPU.
+#pragma once
+#include "lsg_constants_r29.hpp"
+
+#ifndef LSG_PAIR_G
+#define LSG_PAIR_G 2
+#endif
+#define LSG_GROUP LSG_PAIR_G
+#define LSG_PAIR_MODE 1
+#define LSG_QUAD_MODE 1  // register-lean (narrow-issue) tower formulas, see lsg_tower.hpp
+constexpr int LSG_PL = 14 / LSG_GROUP;  // limbs per lane
+constexpr uint32_t LSG_M29 = (1u << 29) - 1;
+
+#if LSG_PAIR_G == 2
+// the generic layers built on this backend are device-only code
+#undef LSG_INL
+#define LSG_INL __device__ __forceinline__
+#undef LSG_NOINL
+#define LSG_NOINL __device__ __noinline__
+#define LSG_PFN __device__ __forceinline__
+#define LSG_PLEAF __device__ __noinline__
+LSG_PFN uint32_t pair_h() { return __lane_id() & 1u; }
+template <int CTRL>
+LSG_PFN uint32_t pdpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+// value of pair-lane S (quad_perm [0,0,2,2] / [1,1,3,3])
+template <int S>
+LSG_PFN uint32_t pbcast(uint32_t x) {
+  return S == 0 ? pdpp<0xA0>(x) : pdpp<0xF5>(x);
+}
+LSG_PFN uint32_t pswap(uint32_t x) { return pdpp<0xB1>(x); }  // the other lane of the pair
+LSG_PFN uint32_t pdown(uint32_t x) {                           // lane 0 <- lane 1, lane 1 <- 0
+  const uint32_t v = pdpp<0xF5>(x);
+  return pair_h() ? 0u : v;
+}
+LSG_PFN uint32_t pup(uint32_t x) {  // lane 1 <- lane 0, lane 0 <- 0
+  const uint32_t v = pdpp<0xA0>(x);
+  return pair_h() ? v : 0u;
+}
+#else
+#define LSG_PFN LSG_INL
+#define LSG_PLEAF LSG_NOINL
+LSG_PFN uint32_t pair_h() { return 0u; }
+template <int S>
+LSG_PFN uint32_t pbcast(uint32_t x) {
+  return x;
+}
+LSG_PFN uint32_t pswap(uint32_t x) { return x; }
+LSG_PFN uint32_t pdown(uint32_t) { return 0u; }
+LSG_PFN uint32_t pup(uint32_t) { return 0u; }
+#endif
+LSG_PFN bool pair_top() { return pair_h() == (uint32_t)(LSG_GROUP - 1); }
+// this lane's k-th limb of a 14-limb literal
+LSG_PFN uint32_t pair_pick(const uint32_t* c, int k) {
+  return (LSG_GROUP == 2 && pair_h()) ? c[LSG_PL + k] : c[k];
+}
+
+struct fp_t {
+  uint32_t l[LSG_PL];  // two's-complement limbs
+  fp_t() = default;
+  LSG_PFN fp_t(const fpc_t& c) {
+#pragma unroll
+    for (int k = 0; k < LSG_PL; k++) l[k] = pair_pick(c.l, k);
+  }
+};
+LSG_PFN fp_t fp_from_arr(const uint32_t* c) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = pair_pick(c, k);
+  return r;
+}
+
+// ---- carries
+// One parallel carry round: limb k keeps its low 29 bits plus the (signed) carry of limb
+// k-1; the top limb keeps everything above.  Value-preserving; inputs with |limb| < 2^31
+// come out with limbs in [-4, 2^29 + 4).
+LSG_PFN fp_t pair_carry(const fp_t& a) {
+  const bool top = pair_top();
+  int32_t c[LSG_PL];
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) c[k] = (int32_t)a.l[k] >> 29;
+  const uint32_t cin = pup((uint32_t)c[LSG_PL - 1]);
+  fp_t o;
+  o.l[0] = (a.l[0] & LSG_M29) + cin;
+#pragma unroll
+  for (int k = 1; k < LSG_PL - 1; k++) o.l[k] = (a.l[k] & LSG_M29) + (uint32_t)c[k - 1];
+  o.l[LSG_PL - 1] = (top ? a.l[LSG_PL - 1] : (a.l[LSG_PL - 1] & LSG_M29)) + (uint32_t)c[LSG_PL - 2];
+  return o;
+}
+// Full normalisation: limbs 0..12 in [0, 2^29), the signed top limb holds the rest.
+LSG_PFN fp_t pair_full_norm(const fp_t& a) {
+  int32_t v[LSG_PL];
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) v[k] = (int32_t)a.l[k];
+#pragma unroll
+  for (int k = 0; k < LSG_PL - 1; k++) {
+    v[k + 1] += v[k] >> 29;
+    v[k] &= (int32_t)LSG_M29;
+  }
+#if LSG_PAIR_G == 2
+  const uint32_t cin = pup((uint32_t)(v[LSG_PL - 1] >> 29));
+  if (!pair_top()) v[LSG_PL - 1] &= (int32_t)LSG_M29;
+  v[0] += (int32_t)cin;
+#pragma unroll
+  for (int k = 0; k < LSG_PL - 1; k++) {
+    v[k + 1] += v[k] >> 29;
+    v[k] &= (int32_t)LSG_M29;
+  }
+#endif
+  fp_t o;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) o.l[k] = (uint32_t)v[k];
+  return o;
+}
+// sign of a fully normalised value (pair-uniform)
+LSG_PFN bool pair_is_neg(const fp_t& n) {
+  const uint32_t s = (int32_t)n.l[LSG_PL - 1] < 0 ? 1u : 0u;
+  return pbcast<LSG_GROUP - 1>(s) != 0u;
+}
+
+#ifdef LSG_COUNT_MULS  // host build only: exact Fp-multiplication counts per stage
+extern unsigned long long lsg_mul_count;
+#define LSG_COUNT_MUL() (lsg_mul_count++)
+#else
+#define LSG_COUNT_MUL() ((void)0)
+#endif
+
+// ---- Montgomery product (CIOS over the 14 radix-2^29 limbs, i-loop over time)
+LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
+  LSG_COUNT_MUL();
+  const bool top = pair_top();
+  uint32_t p[LSG_PL];
+#pragma unroll
+  for (int j = 0; j < LSG_PL; j++) p[j] = pair_pick(LSG_P, j);
+  int64_t t[LSG_PL];
+#pragma unroll
+  for (int j = 0; j < LSG_PL; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t bs = b.l[i % LSG_PL];
+    const int32_t bi = (int32_t)(i / LSG_PL == 0 ? pbcast<0>(bs) : pbcast<LSG_GROUP - 1>(bs));
+#pragma unroll
+    for (int j = 0; j < LSG_PL; j++) t[j] += (int64_t)(int32_t)a.l[j] * bi;
+    const uint32_t m = pbcast<0>(((uint32_t)t[0] * LSG_N0P) & LSG_M29);
+#pragma unroll
+    for (int j = 0; j < LSG_PL; j++) t[j] += (int64_t)(int32_t)m * (int32_t)p[j];
+    // retire limb 0 (its low 29 bits are zero on lane 0): the high part carries into the
+    // next accumulator of the same lane, lane 1's low 29 bits move down to lane 0's top
+    const int64_t c = t[0] >> 29;
+    const uint32_t mv = pdown((uint32_t)t[0] & LSG_M29);
+#pragma unroll
+    for (int j = 0; j < LSG_PL - 1; j++) t[j] = t[j + 1];
+    t[0] += c;
+    t[LSG_PL - 1] = (int64_t)mv;
+  }
+#pragma unroll
+  for (int j = 0; j < LSG_PL - 1; j++) {
+    t[j + 1] += t[j] >> 29;
+    t[j] &= (int64_t)LSG_M29;
+  }
+#if LSG_PAIR_G == 2
+  const int64_t ct = t[LSG_PL - 1] >> 29;
+  const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
+  if (!top) t[LSG_PL - 1] &= (int64_t)LSG_M29;
+  t[0] += (int64_t)(((uint64_t)chi << 32) | clo);
+#pragma unroll
+  for (int j = 0; j < LSG_PL - 1; j++) {
+    t[j + 1] += t[j] >> 29;
+    t[j] &= (int64_t)LSG_M29;
+  }
+#else
+  (void)top;
+#endif
+  fp_t r;
+#pragma unroll
+  for (int j = 0; j < LSG_PL; j++) r.l[j] = (uint32_t)t[j];
+  return r;
+}
+
+// ------------------------------------------------------------------ Fp API
+LSG_PFN fp_t fp_zero() {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = 0u;
+  return r;
+}
+LSG_PFN fp_t fp_select(bool c, const fp_t& a, const fp_t& b) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = c ? a.l[k] : b.l[k];
+  return r;
+}
+LSG_PFN fp_t fp_add(const fp_t& a, const fp_t& b) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = a.l[k] + b.l[k];
+  return pair_carry(r);
+}
+LSG_PFN fp_t fp_sub(const fp_t& a, const fp_t& b) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = a.l[k] - b.l[k];
+  return pair_carry(r);
+}
+LSG_PFN fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
+LSG_PFN fp_t fp_mul(const fp_t& a, const fp_t& b) { return pair_mont_mul(a, b); }
+LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+  fp_t t = pair_mont_mul(a0, b0);
+  r1 = pair_mont_mul(a1, b1);
+  r0 = t;
+}
+LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
+                     const fp_t& a2, const fp_t& b2) {
+  fp_t t0 = pair_mont_mul(a0, b0);
+  fp_t t1 = pair_mont_mul(a1, b1);
+  r2 = pair_mont_mul(a2, b2);
+  r0 = t0;
+  r1 = t1;
+}
+LSG_PFN void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
+#pragma unroll
+  for (int g = 0; g < 9; g += 3) fp_mul3(r[g], r[g + 1], r[g + 2], a[g], b[g], a[g + 1], b[g + 1], a[g + 2], b[g + 2]);
+}
+
+// ---- canonical values
+// v in (-p, 2p) -> the representative in [0, p), fully normalised
+LSG_PFN fp_t pair_canon_small(const fp_t& v0) {
+  const fp_t p = fp_from_arr(LSG_P);
+  fp_t v = pair_full_norm(v0);
+  v = fp_select(pair_is_neg(v), pair_full_norm(fp_add(v, p)), v);
+  fp_t d = pair_full_norm(fp_sub(v, p));
+  return fp_select(pair_is_neg(d), v, d);
+}
+// any lazy value -> [0, p): one product by mont(1) lands it in (-p, 2p)
+LSG_PFN fp_t pair_canon(const fp_t& a) { return pair_canon_small(pair_mont_mul(a, fp_t(FP_ONE))); }
+// fp_from_mont's result (lsg_tower.hpp) is made canonical here, so serialisation and the
+// canonical predicates below see plain integers in [0, p)
+LSG_PFN fp_t fp_canonical(const fp_t& a) { return pair_canon_small(a); }
+
+// |result| < 2p for any lazy value (for loop-carried values that are not products)
+LSG_PFN fp_t fp_tame(const fp_t& a) { return pair_mont_mul(a, fp_t(FP_ONE)); }
+
+LSG_PFN bool fp_is_zero(const fp_t& a) {
+  const fp_t c = pair_canon(a);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) nz |= c.l[k];
+  nz |= pswap(nz);
+  return nz == 0u;
+}
+LSG_PFN bool fp_eq(const fp_t& a, const fp_t& b) { return fp_is_zero(fp_sub(a, b)); }
+
+// predicates on canonical (non-Montgomery) values
+LSG_PFN bool fp_canon_gt_half(const fp_t& c) {
+  return pair_is_neg(pair_full_norm(fp_sub(fp_from_arr(LSG_HALF_P_CANON), pair_canon_small(c))));
+}
+// c = a raw decoded integer (not reduced): c < p
+LSG_PFN bool fp_canon_lt_p(const fp_t& c) { return pair_is_neg(pair_full_norm(fp_sub(c, fp_from_arr(LSG_P)))); }
+LSG_PFN uint32_t fp_canon_parity(const fp_t& c) { return pbcast<0>(pair_canon_small(c).l[0] & 1u); }
+
+// ---- bytes
+LSG_PFN uint32_t pair_be32(const uint8_t* q) {
+  return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+}
+// the number formed by the 4*nwords big-endian bytes at b (nwords <= 12)
+LSG_PFN fp_t fp_from_be_bytes(const uint8_t* b, int nwords) {
+  uint32_t w[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) w[k] = k < nwords ? pair_be32(b + 4 * (nwords - 1 - k)) : 0u;
+  uint32_t L[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const int bit = 29 * k, wi = bit / 32, off = bit % 32;
+    uint32_t x = w[wi] >> off;
+    if (off > 3 && wi + 1 < 12) x |= w[wi + 1] << (32 - off);
+    L[k] = x & LSG_M29;
+  }
+  return fp_from_arr(L);
+}
+// all 14 limbs of a value in every lane of its pair
+LSG_PFN void pair_gather(uint32_t* L, const fp_t& a) {
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) {
+    const uint32_t o = pswap(a.l[k]);
+    if (LSG_GROUP == 2) {
+      L[k] = pair_h() ? o : a.l[k];
+      L[LSG_PL + k] = pair_h() ? a.l[k] : o;
+    } else {
+      L[k] = a.l[k];
+    }
+  }
+}
+LSG_PFN void pair_put_be32(uint8_t* q, uint32_t v) {
+  q[0] = (uint8_t)(v >> 24);
+  q[1] = (uint8_t)(v >> 16);
+  q[2] = (uint8_t)(v >> 8);
+  q[3] = (uint8_t)v;
+}
+// 48 big-endian bytes of a canonical (or flag-carrying raw) value; lane h writes 24 of them
+LSG_PFN void fp_to_be48(uint8_t* b, const fp_t& a) {
+  uint32_t L[14];
+  pair_gather(L, pair_full_norm(a));
+  uint32_t w[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    const int bit = 32 * k, li = bit / 29, off = bit % 29;
+    uint64_t x = (uint64_t)L[li] >> off;
+    int got = 29 - off;
+    if (li + 1 < 14) x |= (uint64_t)L[li + 1] << got;
+    got += 29;
+    if (got < 32 && li + 2 < 14) x |= (uint64_t)L[li + 2] << got;
+    w[k] = (uint32_t)x;
+  }
+  constexpr int PW = 12 / LSG_GROUP;
+#pragma unroll
+  for (int j = 0; j < PW; j++) {
+    const int k = PW * (int)pair_h() + j;
+    const uint32_t v = (LSG_GROUP == 2 && pair_h()) ? w[(PW + j) % 12] : w[j];
+    pair_put_be32(b + 44 - 4 * k, v);
+  }
+}
+// the 3 ZCash flag bits are bits 381..383 = bits 4..6 of limb 13 (top lane, last register)
+LSG_PFN fp_t fp_mask_flags(const fp_t& a) {
+  fp_t r = a;
+  if (pair_top()) r.l[LSG_PL - 1] &= 0xfu;
+  return r;
+}
+// flags: the ZCash flag byte (bits 5..7), placed at bits 381..383 of a canonical value
+LSG_PFN fp_t fp_or_flags(const fp_t& a, uint32_t flags) {
+  fp_t r = pair_full_norm(a);
+  if (pair_top()) r.l[LSG_PL - 1] |= flags >> 1;
+  return r;
+}
+
+// kernels call this once (the quad backend stages p in LDS; here p is a literal)
+LSG_PFN void lsg_lane_setup() {}
+
+// ---- item-major global storage: a value of type T (a struct of W words per lane) for item
+// i lives at mem[(i*W + k)*G + h], k = 0..W-1 (one 8-byte segment per pair and word)
+template <class T>
+LSG_PFN T lane_load(const uint32_t* __restrict__ mem, size_t item) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  const uint32_t* p = mem + item * W * LSG_GROUP + pair_h();
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = p[k * LSG_GROUP];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+template <class T>
+LSG_PFN void lane_store(uint32_t* __restrict__ mem, size_t item, const T& v) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+  uint32_t* p = mem + item * W * LSG_GROUP + pair_h();
+#pragma unroll
+  for (int k = 0; k < W; k++) p[k * LSG_GROUP] = w[k];
+}
+template <class T>
+constexpr size_t lane_words() {
+  return sizeof(T) / 4 * LSG_GROUP;  // u32 words per item in global memory
+}

@@ -255,6 +255,7 @@ LSG_DEVNOINL fp_t quad_sub(fp_t a, fp_t b) {
 
 // ------------------------------------------------------------------ Fp API
 LSG_DEVI fp_t fp_zero() { return fp_t(0u, 0u, 0u); }
+LSG_INL fp_t fp_canonical(const fp_t& a) { return a; }  // values are kept fully reduced
 LSG_DEVI bool fp_is_zero(const fp_t& a) { return quad_none(!lane_all_zero(a)); }
 LSG_DEVI bool fp_eq(const fp_t& a, const fp_t& b) {
   return quad_none(((a.l0 ^ b.l0) | (a.l1 ^ b.l1) | (a.l2 ^ b.l2)) != 0u);

@@ -19,7 +19,9 @@ LSG_INL fp_t fp_one() { return fp_t(FP_ONE); }
 LSG_INL fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
 LSG_INL fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
 LSG_INL fp_t fp_to_mont(const fp_t& a) { return fp_mul(a, fp_t(FP_R2)); }
-LSG_INL fp_t fp_from_mont(const fp_t& a) { return fp_mul(a, fp_t(FP_ONE_CANON)); }
+// canonical plain integer in [0, p) (fp_canonical is the identity for the fully reduced
+// backends; the lazy pair backend reduces here)
+LSG_INL fp_t fp_from_mont(const fp_t& a) { return fp_canonical(fp_mul(a, fp_t(FP_ONE_CANON))); }
 LSG_INL fp_t fp_from_be48(const uint8_t* b) { return fp_from_be_bytes(b, 12); }
 
 // a^e for a fixed public exponent e (12 little-endian words): left-to-right sliding window
@@ -426,6 +428,12 @@ LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
   z2 = fp2_add(fp2_add(z2, z2), t0);
   z3 = fp2_sub(t2, z3);
   z3 = fp2_add(fp2_add(z3, z3), t2);
+#ifdef LSG_PAIR_MODE
+  // the output carries 2x the input additively (3t - 2z): bound lazy values so chains of
+  // squarings (exp by x) do not grow them without limit
+  fp2_t* zs[6] = {&z0, &z1, &z2, &z3, &z4, &z5};
+  for (int k = 0; k < 6; k++) *zs[k] = fp2_t(fp_tame(zs[k]->c0), fp_tame(zs[k]->c1));
+#endif
   return fp12_make(fp6_make(z0, z4, z3), fp6_make(z2, z1, z5));
 }
 

@@ -17,8 +17,13 @@
 #define LSG_DEVNOINL __device__ __noinline__
 #define LSG_CONST static constexpr
 
+// limbs per constant literal: 12 x 32-bit (quad / row / element backends) or 14 x 29-bit
+// (pair backend; lsg_constants_r29.hpp defines LSG_NLIMBS before including this file)
+#ifndef LSG_NLIMBS
+#define LSG_NLIMBS 12
+#endif
 struct fpc_t {
-  uint32_t l[12];
+  uint32_t l[LSG_NLIMBS];
 };
 struct fp2c_t {
   fpc_t c0, c1;

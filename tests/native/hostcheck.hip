@@ -9,7 +9,14 @@
 #include <string.h>
 
 #define LSG_COUNT_MULS 1
+#ifdef LSG_HOSTCHECK_PAIR
+// the pair backend's arithmetic (lazy signed radix-2^29 limbs) with all 14 limbs in one
+// "lane": same representation, bounds and byte conversions as the gfx950 build
+#define LSG_PAIR_G 1
+#include "lsg_fp_pair.hpp"
+#else
 #include "lsg_fp_elem.hpp"
+#endif
 #include "lsg_h2c.hpp"
 #include "lsg_pairing.hpp"
 

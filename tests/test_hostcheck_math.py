@@ -21,26 +21,34 @@ from oracle.pairing import miller_loop_fast, final_exp_fast
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB = os.path.join(HERE, "native", "libhostcheck.so")
 SRC = os.path.join(HERE, "native", "hostcheck.hip")
+# host builds of the generic math over two Fp backends: "elem" (12 x 32-bit limbs, fully
+# reduced, lsg_fp_elem.hpp) and "pair" (the pair backend's lazy signed 14 x 29-bit limbs,
+# lsg_fp_pair.hpp with all limbs in one lane)
+LIBS = {"elem": (os.path.join(HERE, "native", "libhostcheck.so"), []),
+        "pair": (os.path.join(HERE, "native", "libhostcheck_pair.so"), ["-DLSG_HOSTCHECK_PAIR"])}
 
 
-def _build():
+def _build(backend):
+    lib, defs = LIBS[backend]
     hdrs = [os.path.join(ROOT, "lodestar_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "lodestar_amd", "csrc"))]
     newest = max(os.path.getmtime(p) for p in hdrs + [SRC])
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
-        return
-    subprocess.check_call(["hipcc", "-x", "hip", "--cuda-host-only", "-O2", "-std=c++17", "-fPIC", "-shared",
-                           "-I", os.path.join(ROOT, "lodestar_amd", "csrc"), SRC, "-o", LIB])
+    if os.path.exists(lib) and os.path.getmtime(lib) >= newest:
+        return lib
+    subprocess.check_call(["hipcc", "-x", "hip", "--cuda-host-only", "-O2", "-std=c++17", "-fPIC", "-shared"] + defs +
+                          ["-I", os.path.join(ROOT, "lodestar_amd", "csrc"), SRC, "-o", lib])
+    return lib
 
 
-@pytest.fixture(scope="module")
-def hc():
+@pytest.fixture(scope="module", params=["elem", "pair"])
+def hc(request):
     try:
-        _build()
+        lib = _build(request.param)
     except (OSError, subprocess.CalledProcessError) as e:  # pragma: no cover
         pytest.skip(f"hipcc unavailable: {e}")
-    return ctypes.CDLL(LIB)
+    h = ctypes.CDLL(lib)
+    h.backend = request.param
+    return h
 
 
 def be(v):

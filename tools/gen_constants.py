@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
-"""Build tool: emits lodestar_amd/csrc/lsg_constants.hpp (Montgomery-form constants for the
-gfx950 kernels: 12 x 32-bit little-endian limbs, R = 2^384).
+"""Build tool: emits the Montgomery-form constants of the gfx950 kernels for the two limb
+layouts:
+  lodestar_amd/csrc/lsg_constants.hpp      12 x 32-bit little-endian limbs, R = 2^384
+                                           (quad and row backends, host element backend)
+  lodestar_amd/csrc/lsg_constants_r29.hpp  14 x 29-bit little-endian limbs, R = 2^406
+                                           (radix-2^29 thread-per-set backend)
 
 Standalone on purpose -- it does not import oracle/ (the checker); tests/test_constants.py
 cross-checks every emitted value against the oracle.  The 3-isogeny coefficients are the
@@ -13,6 +17,8 @@ import sys
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 X_ABS = 0xD201000000010000
+# limb layout (set by main): bits per limb, limbs, Montgomery radix R = 2^(bits*limbs)
+BITS, NL = 32, 12
 RM = 1 << 384
 N0P = (-pow(P, -1, 1 << 32)) % (1 << 32)
 
@@ -36,8 +42,8 @@ def f2inv(a):
     return (a[0] * n % P, -a[1] * n % P)
 
 
-def limbs(v, n=12):
-    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
+def limbs(v, n=12, bits=32):
+    return [(v >> (bits * i)) & ((1 << bits) - 1) for i in range(n)]
 
 
 def mont(v):
@@ -45,7 +51,13 @@ def mont(v):
 
 
 def arr(v, n=12):
+    """a 32-bit-word array (exponents: bit-scanned by fp_pow_fixed in every layout)"""
     return "{" + ", ".join("0x%08xu" % x for x in limbs(v, n)) + "}"
+
+
+def arrl(v):
+    """a field element in the current limb layout"""
+    return "{" + ", ".join("0x%08xu" % x for x in limbs(v, NL, BITS)) + "}"
 
 
 XI = (1, 1)
@@ -99,29 +111,40 @@ G1_Y = 0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC74
 
 
 def fp_decl(name, v):
-    return f"LSG_CONST fpc_t {name} = {{{arr(mont(v))}}};\n"
+    return f"LSG_CONST fpc_t {name} = {{{arrl(mont(v))}}};\n"
 
 
 def fp2_decl(name, v):
-    return f"LSG_CONST fp2c_t {name} = {{{{{arr(mont(v[0]))}}}, {{{arr(mont(v[1]))}}}}};\n"
+    return f"LSG_CONST fp2c_t {name} = {{{{{arrl(mont(v[0]))}}}, {{{arrl(mont(v[1]))}}}}};\n"
 
 
-def main(out):
+def main(out, bits=32):
+    global BITS, NL, RM, N0P
+    BITS, NL = bits, (12 if bits == 32 else 14)
+    RM = 1 << (BITS * NL)
+    N0P = (-pow(P, -1, 1 << BITS)) % (1 << BITS)
     s = []
     s.append("// GENERATED by tools/gen_constants.py -- do not edit.\n")
-    s.append("// Montgomery form (R = 2^384), 12 x u32 little-endian limbs.\n#pragma once\n#include \"lsg_types.hpp\"\n\n")
-    s.append(f"LSG_CONST uint32_t LSG_P[12] = {arr(P)};\n")
+    s.append(f"// Montgomery form (R = 2^{BITS * NL}), {NL} x {BITS}-bit little-endian limbs"
+             f"{'' if BITS == 32 else ' (one u32 word each)'}.\n#pragma once\n")
+    if BITS != 32:
+        s.append(f"#define LSG_NLIMBS {NL}\n")
+    s.append("#include \"lsg_types.hpp\"\n\n")
+    s.append(f"LSG_CONST uint32_t LSG_P[{NL}] = {arrl(P)};\n")
     s.append(f"LSG_CONST uint32_t LSG_N0P = 0x{N0P:08x}u;\n")
     s.append(f"LSG_CONST uint32_t LSG_EXP_P_MINUS_2[12] = {arr(P - 2)};\n")
     s.append(f"LSG_CONST uint32_t LSG_EXP_P_PLUS_1_DIV_4[12] = {arr((P + 1) // 4)};\n")
     s.append(f"LSG_CONST uint32_t LSG_EXP_P_MINUS_3_DIV_4[12] = {arr((P - 3) // 4)};\n")
-    s.append(f"LSG_CONST uint32_t LSG_HALF_P_CANON[12] = {arr((P - 1) // 2)};  // (p-1)/2, canonical\n")
+    s.append(f"LSG_CONST uint32_t LSG_HALF_P_CANON[{NL}] = {arrl((P - 1) // 2)};  // (p-1)/2, canonical\n")
     s.append(f"LSG_CONST uint32_t LSG_X_ABS_LO = 0x{X_ABS & 0xFFFFFFFF:08x}u, LSG_X_ABS_HI = 0x{X_ABS >> 32:08x}u;\n\n")
     s.append(fp_decl("FP_ONE", 1))
     s.append(fp_decl("FP_R2", RM % P))  # mont(R) = R^2
-    s.append(fp_decl("FP_R3", RM * RM % P))  # mont(R^2) = R^3 mod p
+    s.append(fp_decl("FP_R3", (1 << 384) * RM % P))  # mont(2^384 R) (= R^3 for R = 2^384)
     s.append(fp_decl("FP_R2_SHL256", (1 << 256) * RM % P))  # mont(2^256 R) = 2^256 R^2 mod p
-    s.append(f"LSG_CONST fpc_t FP_ONE_CANON = {{{arr(1)}}};  // plain 1 (for from_mont)\n")
+    s.append(f"LSG_CONST fpc_t FP_ONE_CANON = {{{arrl(1)}}};  // plain 1 (for from_mont)\n")
+    if BITS != 32:  # plain multipliers between this layout and the 12 x 32-bit (R = 2^384) one
+        s.append(f"LSG_CONST fpc_t FP_FROM_R384 = {{{arrl((1 << (2 * BITS * NL - 384)) % P)}}};  // x R^2 / 2^384\n")
+        s.append(f"LSG_CONST fpc_t FP_TO_R384 = {{{arrl((1 << 384) % P)}}};  // x 2^384 / R\n")
     s.append(fp_decl("FP_HALF", pow(2, -1, P)))
     s.append(fp_decl("FP_B_G1", 4))
     s.append(fp_decl("FP_B3_G1", 12))
@@ -157,3 +180,4 @@ if __name__ == "__main__":
     here = os.path.dirname(os.path.abspath(__file__))
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(here, "..", "lodestar_amd", "csrc", "lsg_constants.hpp")
     main(out)
+    main(os.path.join(os.path.dirname(out), "lsg_constants_r29.hpp"), bits=29)

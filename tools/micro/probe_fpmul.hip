@@ -158,6 +158,88 @@ __device__ __noinline__ f14 mul_r29(f14 a, f14 b) {
   return r;
 }
 
+
+// ---------------------------------------------------------------- pair29
+// 14 x 29-bit limbs over a lane PAIR: lane h (0/1) holds limbs 7h..7h+6 and the matching
+// seven 64-bit CIOS accumulators.  Per step: b_i and m are DPP broadcasts inside the pair;
+// the retiring accumulator is split into its carry (into the next accumulator, same lane)
+// and its low 29 bits (moved one lane down by DPP), so only one 32-bit value crosses lanes
+// per step and no carry bookkeeping is needed.
+struct h7 {
+  uint32_t l[7];
+};
+template <int CTRL>
+__device__ __forceinline__ uint32_t pdpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+__device__ __noinline__ h7 mul_pair(h7 a, h7 b) {
+  const bool hi = __lane_id() & 1u;
+  uint32_t p[7];
+#pragma unroll
+  for (int j = 0; j < 7; j++) p[j] = hi ? P29.l[7 + j] : P29.l[j];
+  uint64_t t[7];
+#pragma unroll
+  for (int j = 0; j < 7; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t bs = b.l[i % 7];
+    const uint32_t bi = i < 7 ? pdpp<0xA0>(bs) : pdpp<0xF5>(bs);
+#pragma unroll
+    for (int j = 0; j < 7; j++) t[j] += (uint64_t)a.l[j] * bi;
+    const uint32_t m = pdpp<0xA0>(((uint32_t)t[0] * N0P29) & M29);
+#pragma unroll
+    for (int j = 0; j < 7; j++) t[j] += (uint64_t)m * p[j];
+    const uint64_t c = t[0] >> 29;
+    uint32_t mv = pdpp<0xF5>((uint32_t)t[0] & M29);
+    mv = hi ? 0u : mv;
+#pragma unroll
+    for (int j = 0; j < 6; j++) t[j] = t[j + 1];
+    t[0] += c;
+    t[6] = mv;
+  }
+  // normalise: in-lane carries, lane 0's carry-out into lane 1, in-lane carries again
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    t[j + 1] += t[j] >> 29;
+    t[j] &= M29;
+  }
+  uint32_t co = pdpp<0xA0>((uint32_t)(t[6] >> 29));
+  t[6] = hi ? t[6] : (t[6] & M29);
+  t[0] += hi ? co : 0u;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    t[j + 1] += t[j] >> 29;
+    t[j] &= M29;
+  }
+  h7 r;
+#pragma unroll
+  for (int j = 0; j < 7; j++) r.l[j] = (uint32_t)t[j];
+  return r;
+}
+
+template <int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_rate_pair(int iters, const f14* __restrict__ in, f14* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t e = t >> 1;
+  const int h = (int)(t & 1);
+  h7 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int j = 0; j < 7; j++) v[k].l[j] = in[4 * e + k].l[7 * h + j];
+  for (int k = 0; k < iters; k++) {
+    v[0] = mul_pair(v[0], v[1]);
+    v[1] = mul_pair(v[1], v[2]);
+    v[2] = mul_pair(v[2], v[3]);
+    v[3] = mul_pair(v[3], v[0]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int j = 0; j < 7; j++) out[4 * e + k].l[7 * h + j] = v[k].l[j];
+}
+
 // ---------------------------------------------------------------- rate kernels: 4 chains/thread
 template <class F, F (*MUL)(F, F), int WPE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
@@ -190,20 +272,31 @@ static void fill(F* h, size_t n, int limbs, int bits) {
 }
 
 template <class F, F (*MUL)(F, F), int WPE>
+struct LaunchElem {
+  static constexpr int lanes = 1;
+  static void go(int blocks, int iters, const F* i, F* o) { k_rate<F, MUL, WPE><<<blocks, 64>>>(iters, i, o); }
+};
+template <int WPE>
+struct LaunchPair {
+  static constexpr int lanes = 2;
+  static void go(int blocks, int iters, const f14* i, f14* o) { k_rate_pair<WPE><<<blocks, 64>>>(iters, i, o); }
+};
+
+template <class F, class L>
 static void run(const char* name, int limbs, int bits, int iters, int waves_per_simd) {
   int dev;
   CHECK(hipGetDevice(&dev));
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, dev));
   const int blocks = prop.multiProcessorCount * 4 * waves_per_simd;  // one wave per block
-  const size_t threads = (size_t)blocks * 64, n = 4 * threads;
+  const size_t threads = (size_t)blocks * 64 / L::lanes, n = 4 * threads;  // threads = elements per chain
   F* h = (F*)malloc(n * sizeof(F));
   fill(h, n, limbs, bits);
   F *din, *dout;
   CHECK(hipMalloc(&din, n * sizeof(F)));
   CHECK(hipMalloc(&dout, n * sizeof(F)));
   CHECK(hipMemcpy(din, h, n * sizeof(F), hipMemcpyHostToDevice));
-  k_rate<F, MUL, WPE><<<blocks, 64>>>(1, din, dout);  // correctness sample: one iteration
+  L::go(blocks, 1, din, dout);  // correctness sample: one iteration
   CHECK(hipDeviceSynchronize());
   F* o = (F*)malloc(n * sizeof(F));
   CHECK(hipMemcpy(o, dout, n * sizeof(F), hipMemcpyDeviceToHost));
@@ -219,12 +312,12 @@ static void run(const char* name, int limbs, int bits, int iters, int waves_per_
     }
     printf("\n");
   }
-  k_rate<F, MUL, WPE><<<blocks, 64>>>(iters, din, dout);  // warm
+  L::go(blocks, iters, din, dout);  // warm
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   CHECK(hipEventRecord(e0));
-  k_rate<F, MUL, WPE><<<blocks, 64>>>(iters, din, dout);
+  L::go(blocks, iters, din, dout);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms;
@@ -241,12 +334,16 @@ static void run(const char* name, int limbs, int bits, int iters, int waves_per_
 
 int main(int argc, char** argv) {
   int iters = argc > 1 ? atoi(argv[1]) : 256;
-  run<f12, mul_c, 2>("elem_c", 12, 32, iters, 2);
-  run<f12, mul_c, 4>("elem_c", 12, 32, iters, 4);
-  run<f12, mul_ps, 1>("elem_ps", 12, 32, iters, 1);
-  run<f12, mul_ps, 2>("elem_ps", 12, 32, iters, 2);
-  run<f12, mul_ps, 4>("elem_ps", 12, 32, iters, 4);
-  run<f14, mul_r29, 2>("r29", 14, 29, iters, 2);
-  run<f14, mul_r29, 4>("r29", 14, 29, iters, 4);
+  run<f12, LaunchElem<f12, mul_c, 2>>("elem_c", 12, 32, iters, 2);
+  run<f12, LaunchElem<f12, mul_c, 4>>("elem_c", 12, 32, iters, 4);
+  run<f12, LaunchElem<f12, mul_ps, 1>>("elem_ps", 12, 32, iters, 1);
+  run<f12, LaunchElem<f12, mul_ps, 2>>("elem_ps", 12, 32, iters, 2);
+  run<f12, LaunchElem<f12, mul_ps, 4>>("elem_ps", 12, 32, iters, 4);
+  run<f14, LaunchElem<f14, mul_r29, 2>>("r29", 14, 29, iters, 2);
+  run<f14, LaunchElem<f14, mul_r29, 4>>("r29", 14, 29, iters, 4);
+  run<f14, LaunchPair<1>>("pair29", 14, 29, iters, 1);
+  run<f14, LaunchPair<2>>("pair29", 14, 29, iters, 2);
+  run<f14, LaunchPair<4>>("pair29", 14, 29, iters, 4);
+  run<f14, LaunchPair<8>>("pair29", 14, 29, iters, 8);
   return 0;
 }
