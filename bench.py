@@ -220,7 +220,9 @@ def main():
             "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
     total_sets = n * world * steps
     value = total_sets / elapsed
-    per_set_muls = opc["batched_single_set_fp_muls"]
+    # whole-path work per set: the per-set stages with the bucket-MSM signature sums (groups of
+    # n >= 256 sets take the MSM path) plus each group's share of its per-group stages
+    per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / n
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:
         cpu = None

@@ -8,9 +8,9 @@
 //   packages/beacon-node/src/chain/bls/utils.ts:5-26               (pubkey aggregation)
 //   + the un-vendored @chainsafe/blst@0.2.8 arithmetic underneath.
 //
-// Execution model: every field element is limb-parallel over a 16-lane DPP row
-// (lsg_fp_lane.hpp), so one work item (a set, a pubkey, a group) is one row and a wave64
-// carries four items.  Per work package:
+// Execution model: every field element is limb-parallel over a lane pair (lsg_fp_pair.hpp,
+// the default build; lsg_fp_quad.hpp / lsg_fp_lane.hpp are alternative builds), so one work
+// item (a set, a pubkey, a group) is one pair and a wave64 carries 32 items.  Per package:
 //   k_expand_msg      expand_message_xmd (SHA-256), one thread per set          [M3]
 //   k_sig_decode      96/192-byte signature -> affine G2                         [M2]
 //   k_sig_subgroup    psi(P) == [x]P                                             [M2]
@@ -19,13 +19,13 @@
 //   k_pk_scale        P_i = [r_i] agg_i; batched 1/Z; k_pk_affine               [M4]
 //   k_h2c_prep/map/affine  hash_to_field -> SSWU x2 -> 3-isogeny -> add ->
 //                     clear_cofactor -> affine, inversions batched per stage       [M3]
-//   k_sig_scale       [r_i] sig_i                                                [M4]
-//   k_miller_sets     f_i = ML(P_i, H(m_i))                                      [M5]
+//   k_sig_proj        sig_i for the bucket MSM (k_sig_scale [r_i] sig_i for small groups) [M4]
+//   k_miller_multi    f_item = prod of ML(P_i, H(m_i)) over <= K sets            [M5]
 // then per group (an RLC batch = a chunk of batchable jobs, or one job):
-//   tree(G2 add)      S_g = sum [r_i] sig_i
-//   k_miller_groups   f_g = ML(-G1, S_g)
-//   tree(Fp12 mul)    F_g = f_g prod f_i
-//   k_final_exp_check FE(F_g) == 1                                               [M6]
+//   msm_buckets/msm_bits/k_msm_horner   S_g = sum r_i sig_i (8-bit windows)
+//   k_row_miller_neg_g1                 f_g = ML(-G1, S_g)        (row backend, lsg_serial.hip)
+//   tree(Fp12 mul)    F_g = f_g prod f_item
+//   k_row_final_exp   FE(F_g) == 1                                               [M6]
 // Per-set values stay resident between the batch attempt and the per-job retry.
 #include <hip/hip_runtime.h>
 

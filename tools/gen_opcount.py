@@ -28,12 +28,23 @@ def main():
     per_set = (c["sig_decode"] + c["sig_subgroup"] + c["pk_decode"] + c["pk_scale"] + c["hash_map"] + c["sig_scale"]
                + c["miller_multi2_per_set"] + c["g2_add"] + c["fp12_mul"] // 2)
     per_batch = c["miller"] + c["fp12_mul"] + c["final_exp"]  # group sig term + product + FE
+    # the device sums sum_i r_i sig_i per group by a bucket MSM (lsg_bls.hip msm_sum: 8-bit
+    # windows of the 64-bit r_i) instead of per-set [r_i] sig_i: per set one G2 addition per
+    # window digit (8, an upper bound: zero digits are skipped); per group the 64 bit sums over
+    # 128 buckets each (64 * 127 additions) and the Horner pass (63 doublings + 63 additions,
+    # a doubling counted as an addition)
+    msm_per_set = 8 * c["g2_add"]
+    msm_per_group = (64 * 127 + 126) * c["g2_add"]
+    per_set_msm = per_set - c["sig_scale"] - c["g2_add"] + msm_per_set
     out = {
         "unit": "Fp multiplications (381-bit Montgomery); 1 = 300 v_mad_u64_u32",
         "mads_per_fp_mul": 300,
         "stage_fp_muls": c,
         "batched_single_set_fp_muls": per_set,
         "per_batch_fp_muls": per_batch,
+        "msm": {"per_set_fp_muls": msm_per_set, "per_group_fp_muls": msm_per_group},
+        "batched_single_set_msm_fp_muls": per_set_msm,
+        "per_batch_msm_fp_muls": per_batch + msm_per_group,
         "aggregate_extra_per_pubkey_fp_muls": c["g1_add"],
         "survey_estimate_blst_equivalent": {"batched_single_set": 16000, "per_batch": 15000, "per_pubkey": 11},
         "source": "tools/gen_opcount.py over tests/native/hostcheck.hip (LSG_COUNT_MULS)",
