@@ -67,6 +67,15 @@ namespace {
 #endif
 #endif
 #define LSG_KERNEL_ATTR __launch_bounds__(LSG_TPB) __attribute__((amdgpu_waves_per_eu(LSG_WAVES_PER_EU)))
+// per-kernel register budget (waves per SIMD) for the kernels whose live state does not fit
+// 256 registers: at 1 wave per SIMD a wave owns 512 (VGPRs + AGPRs) instead of spilling
+#define LSG_KERNEL_ATTR_W(w) __launch_bounds__(LSG_TPB) __attribute__((amdgpu_waves_per_eu(w)))
+#ifndef LSG_H2C_WAVES
+#define LSG_H2C_WAVES LSG_WAVES_PER_EU
+#endif
+#ifndef LSG_SUBGROUP_WAVES
+#define LSG_SUBGROUP_WAVES LSG_WAVES_PER_EU
+#endif
 #define LSG_ITEMS_PER_BLOCK (LSG_TPB / LSG_GROUP)
 
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
@@ -119,7 +128,7 @@ __global__ void LSG_KERNEL_ATTR k_sig_decode(int n, const uint8_t* __restrict__ 
   }
 }
 
-__global__ void LSG_KERNEL_ATTR k_sig_subgroup(int n, const uint32_t* __restrict__ sig_aff,
+__global__ void LSG_KERNEL_ATTR_W(LSG_SUBGROUP_WAVES) k_sig_subgroup(int n, const uint32_t* __restrict__ sig_aff,
                                                            const uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
   LANE_ITEM(n);
   if (err[item] != 0 || inf[item]) return;
@@ -222,7 +231,7 @@ __global__ void LSG_KERNEL_ATTR k_h2c_prep(int n, const uint8_t* __restrict__ ub
 }
 // stage 2: SSWU x2 (with the batched 1/N(tv1)) -> 3-isogeny -> add -> clear_cofactor,
 // projective; zN_i = N(Z) (0 at infinity) for the second batched inversion
-__global__ void LSG_KERNEL_ATTR k_h2c_map(int n, const uint32_t* __restrict__ U,
+__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_map(int n, const uint32_t* __restrict__ U,
                                                       const uint32_t* __restrict__ ninv, uint32_t* __restrict__ Hp,
                                                       uint32_t* __restrict__ zN, uint8_t* __restrict__ hinf) {
   LANE_ITEM(n);
@@ -287,10 +296,69 @@ __global__ void LSG_KERNEL_ATTR k_miller_multi(int n_items, const int32_t* __res
   lane_store(f, item, miller_loop_multi<K>(Pk, Qk, use));
 }
 
+// ---- split Miller loop (lsg_pairing.hpp: miller_lines / miller_accum_multi)
+// Line storage is word-major over sets: word k (of the W per lane of a line_t) of step st of
+// set i lives at lines[((st * W + k) * n + i) * G + h], so one store or load instruction of a
+// wave touches one contiguous 256-byte run.  ML_STEPS lines = 68 x 6 Fp per set (~22.8 KB).
+constexpr int W_LINE = (int)(sizeof(line_t) / 4);
+LSG_DEVI void line_store(uint32_t* __restrict__ lines, size_t n, size_t i, int st, const line_t& L) {
+  uint32_t w[W_LINE];
+  __builtin_memcpy(w, &L, sizeof(line_t));
+  uint32_t* p = lines + (((size_t)st * W_LINE) * n + i) * LSG_GROUP + (threadIdx.x % LSG_GROUP);
+#pragma unroll
+  for (int k = 0; k < W_LINE; k++) p[(size_t)k * n * LSG_GROUP] = w[k];
+}
+LSG_DEVI line_t line_load(const uint32_t* __restrict__ lines, size_t n, size_t i, int st) {
+  uint32_t w[W_LINE];
+  const uint32_t* p = lines + (((size_t)st * W_LINE) * n + i) * LSG_GROUP + (threadIdx.x % LSG_GROUP);
+#pragma unroll
+  for (int k = 0; k < W_LINE; k++) w[k] = p[(size_t)k * n * LSG_GROUP];
+  line_t L;
+  __builtin_memcpy(&L, w, sizeof(line_t));
+  return L;
+}
+
+// the G2 half: the 68 unevaluated lines of Q_i = H(m_i) for every set (no dependency on the
+// pubkey side, so it runs as soon as hash_to_G2 is done).  Sets whose point is unusable still
+// run the chain on whatever Q holds: every lane pair follows one control path.
+__global__ void LSG_KERNEL_ATTR k_miller_lines(int n, const uint32_t* __restrict__ H, uint32_t* __restrict__ lines) {
+  LANE_ITEM(n);
+  const g2a_t Q = lane_load<g2a_t>(H, item);
+  miller_lines(Q, [&](int st, const line_t& L) { line_store(lines, (size_t)n, item, st, L); });
+}
+
+// the Fp12 half: f_item = prod over the item's <= K sets of their lines evaluated at P_i,
+// with shared squarings -- the value k_miller_multi computes
+#ifndef LSG_ACCUM_WAVES
+#define LSG_ACCUM_WAVES 1  // 512 registers: f, the line and the products stay out of scratch (1.33M -> 1.43M sets/s)
+#endif
+template <int K>
+__global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES) k_miller_accum(int n_items, const int32_t* __restrict__ item_first,
+                                               const int32_t* __restrict__ item_cnt, const uint32_t* __restrict__ P,
+                                               const uint8_t* __restrict__ pinf, const uint8_t* __restrict__ hinf,
+                                               const int32_t* __restrict__ err, int n_sets,
+                                               const uint32_t* __restrict__ lines, uint32_t* __restrict__ f) {
+  LANE_ITEM(n_items);
+  const int first = item_first[item], cnt = item_cnt[item];
+  g1a_t Pk[K];
+  bool use[K];
+  int idx[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = first + (k < cnt ? k : cnt - 1);
+    idx[k] = i;
+    use[k] = k < cnt && err[i] == 0 && !pinf[i] && !hinf[i];
+    Pk[k] = lane_load<g1a_t>(P, i);
+  }
+  lane_store(f, item, miller_accum_multi<K>(Pk, use, [&](int k, int st) {
+               return line_load(lines, (size_t)n_sets, (size_t)idx[k], st);
+             }));
+}
+
 // one level of a segmented pairwise reduction: dst[k] = src[ia[k]] (+) src[ib[k]]  (ib < 0: copy;
 // ia < 0: the identity, for an empty group)
-template <int OP>
-__global__ void LSG_KERNEL_ATTR k_tree_level(int n, const int32_t* __restrict__ ia,
+template <int OP>  // OP 2 (Fp12 products) gets 1 wave per SIMD: its operands do not fit 256 registers
+__global__ void LSG_KERNEL_ATTR_W(OP == 2 ? 1 : LSG_WAVES_PER_EU) k_tree_level(int n, const int32_t* __restrict__ ia,
                                                          const int32_t* __restrict__ ib, const uint32_t* __restrict__ src,
                                                          uint32_t* __restrict__ dst) {
   LANE_ITEM(n);
@@ -637,6 +705,7 @@ struct Slot {
   // tree scratch: [0] Fp12 products (main stream), [1] pubkey aggregation, [2] signature sums,
   // [3] [4] MSM buckets and bit sums (side stream)
   TreeSlot tree[5];
+  DevBuf d_lines;        // split Miller loop: ML_STEPS unevaluated lines per set
   DevBuf d_bkt, d_bits;  // MSM buckets and per-bit partial sums (lane-form G2, projective)
   bool msm = false;      // signature sums of this package by bucket MSM (else per-set [r_i] sig_i)
   // Miller items: <= LSG_MILLER_K consecutive sets of one job share one multi-Miller loop
@@ -818,7 +887,7 @@ void slot_destroy(Slot* s) {
                     &s->d_agg, &s->d_P,  &s->d_pinf,   &s->d_H,      &s->d_hinf,   &s->d_rs,  &s->d_fall,
                     &s->d_S,   &s->d_F,  &s->d_verdict, &s->d_blob,  &s->d_aux, &s->d_Sb, &s->d_fgb, &s->d_Fb,
                     &s->d_Pp,  &s->d_zP, &s->d_zPi, &s->d_U, &s->d_nrm, &s->d_nrmi, &s->d_Hp, &s->d_zN, &s->d_zNi,
-                    &s->binv_lv[0], &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_bkt, &s->d_bits};
+                    &s->binv_lv[0], &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_bkt, &s->d_bits, &s->d_lines};
   for (DevBuf* b : bufs) free_dev(*b);
   free_dev(s->d_items);
   for (TreeSlot& t : s->tree) {
@@ -1114,6 +1183,16 @@ int miller_k() {
   return k;
 }
 
+// Miller loop as two kernels (k_miller_lines + k_miller_accum, default) or one
+// (k_miller_multi): env LSG_MILLER_SPLIT=0 selects the fused kernel (A/B)
+bool miller_split() {
+  static bool v = [] {
+    const char* e = getenv("LSG_MILLER_SPLIT");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 // Items of <= LSG_MILLER_K consecutive sets that never cross a range (a job): per-job Miller
 // products, needed by the per-job retry, stay products of whole items.
 void plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges) {
@@ -1187,6 +1266,12 @@ int launch_set_stages(Slot* s) {
     int rc = launch_hash(s, n);
     if (rc) return rc;
   }
+  const bool split = miller_split();
+  if (split) {  // the G2 half needs only the hashes
+    int rc = ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * LSG_GROUP * (size_t)n);
+    if (rc) return rc;
+    LAUNCH(s, k_miller_lines, n, n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines));
+  }
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
   int ni = (int)s->n_items;
   if (ni <= 0 || s->item_host.size() != 2 * (size_t)ni) {
@@ -1204,6 +1289,19 @@ int launch_set_stages(Slot* s) {
   const uint8_t* mhi = P_<uint8_t>(s->d_hinf);
   const int32_t* merr = P_<int32_t>(s->d_seterr);
   uint32_t* mf = P_<uint32_t>(s->d_fall);
+  if (split) {
+    const uint32_t* ml = P_<uint32_t>(s->d_lines);
+    if (miller_k() == 1)
+      LAUNCH_T(s, "k_miller_accum", k_miller_accum<1>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mhi,
+               merr, n, ml, mf);
+    else if (miller_k() == 2)
+      LAUNCH_T(s, "k_miller_accum", k_miller_accum<2>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mhi,
+               merr, n, ml, mf);
+    else
+      LAUNCH_T(s, "k_miller_accum", k_miller_accum<4>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mhi,
+               merr, n, ml, mf);
+    return LSG_OK;
+  }
   if (miller_k() == 1)
     LAUNCH_T(s, "k_miller_multi", k_miller_multi<1>, lane_blocks(ni), LSG_TPB, ni, items, items + ni, mP, mpi, mH, mhi,
              merr, mf);

@@ -12,17 +12,17 @@ struct line_t {
   fp2_t l00, l01, l11;
 };
 
-// T <- 2T; line = (3b'Z^2 - Y^2, 3X^2 xP, -2YZ yP)
-LSG_BIGFN line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
+// T <- 2T; returns the line unevaluated: (3b'Z^2 - Y^2, 3X^2, -2YZ); at P it is
+// (l00, l01 xP, l11 yP) (line_eval)
+LSG_BIGFN line_t ml_dbl_step_raw(g2p_t& T) {
   fp2_t t0 = fp2_sqr(T.Y);
   fp2_t t1 = fp2_mul(T.Y, T.Z);
   fp2_t t2 = fp2_mul_b3(fp2_sqr(T.Z));
   fp2_t XX = fp2_sqr(T.X);
   line_t L;
   L.l00 = fp2_sub(t2, t0);
-  fp2_t XX3 = fp2_add(fp2_add(XX, XX), XX);
-  L.l01 = fp2_mul_fp(XX3, xP);
-  L.l11 = fp2_mul_fp(fp2_neg(fp2_add(t1, t1)), yP);
+  L.l01 = fp2_add(fp2_add(XX, XX), XX);
+  L.l11 = fp2_neg(fp2_add(t1, t1));
   fp2_t Z3 = fp2_add(t0, t0);
   Z3 = fp2_add(Z3, Z3);
   Z3 = fp2_add(Z3, Z3);
@@ -43,14 +43,15 @@ LSG_BIGFN line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) {
   return L;
 }
 
-// T <- T + Q; theta = Y - yQ Z, delta = X - xQ Z; line = (delta yQ - theta xQ, theta xP, -delta yP)
-LSG_BIGFN line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
+// T <- T + Q; theta = Y - yQ Z, delta = X - xQ Z; unevaluated line (delta yQ - theta xQ,
+// theta, -delta); at P: (l00, theta xP, -delta yP)
+LSG_BIGFN line_t ml_add_step_raw(g2p_t& T, g2a_t Q) {
   fp2_t theta = fp2_sub(T.Y, fp2_mul(Q.y, T.Z));
   fp2_t delta = fp2_sub(T.X, fp2_mul(Q.x, T.Z));
   line_t L;
   L.l00 = fp2_sub(fp2_mul(delta, Q.y), fp2_mul(theta, Q.x));
-  L.l01 = fp2_mul_fp(theta, xP);
-  L.l11 = fp2_mul_fp(fp2_neg(delta), yP);
+  L.l01 = theta;
+  L.l11 = fp2_neg(delta);
   fp2_t C = fp2_sqr(theta);
   fp2_t D = fp2_sqr(delta);
   fp2_t E = fp2_mul(D, delta);
@@ -64,6 +65,21 @@ LSG_BIGFN line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
   T.Y = Y3;
   T.Z = Z3;
   return L;
+}
+
+// an unevaluated line at the G1 point P = (xP, yP)
+LSG_INL line_t line_eval(line_t L, const fp_t& xP, const fp_t& yP) {
+  L.l01 = fp2_mul_fp(L.l01, xP);
+  L.l11 = fp2_mul_fp(L.l11, yP);
+  return L;
+}
+
+// T <- 2T; line = (3b'Z^2 - Y^2, 3X^2 xP, -2YZ yP)
+LSG_INL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) { return line_eval(ml_dbl_step_raw(T), xP, yP); }
+
+// T <- T + Q; line = (delta yQ - theta xQ, theta xP, -delta yP)
+LSG_INL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
+  return line_eval(ml_add_step_raw(T, Q), xP, yP);
 }
 
 // f_{|x|,Q}(P) conjugated (x < 0).  P affine G1, Q affine G2, both finite.
@@ -137,6 +153,62 @@ LSG_INL fp12_t miller_loop_multi(const g1a_t (&P)[K], const g2a_t (&Q)[K], const
 #pragma unroll
       for (int k = 0; k < K; k++) {
         line_t L = ml_add_step(T[k], Q[k], P[k].x, P[k].y);
+        f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
+      }
+    }
+  }
+  return fp12_conj(f);
+}
+
+// ---- Split Miller loop (device path): the G2 side and the Fp12 side run as two kernels.
+// miller_lines writes the ML_STEPS unevaluated lines of one Q in loop order (step 0: the
+// first doubling, step 1: the addition for bit 62, then per bit b = 61..0 a doubling and,
+// for set bits, an addition); miller_accum_multi evaluates them at the P_k and accumulates
+// f with the same operation order as miller_loop_multi, so the result is the same field
+// element.  Each kernel then holds only its own half of the state (T and a line, or f and a
+// line) instead of f, K points and the line together.
+constexpr int ML_STEPS = 68;  // 63 doublings + 5 additions for |x| = 0xd201000000010000
+
+template <class Put>
+LSG_INL void miller_lines(const g2a_t& Q, Put&& put) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  g2p_t T = proj_from_aff(Q);
+  int s = 0;
+  put(s++, ml_dbl_step_raw(T));
+  put(s++, ml_add_step_raw(T, Q));
+#pragma unroll 1
+  for (int b = 61; b >= 0; b--) {
+    put(s++, ml_dbl_step_raw(T));
+    if ((xa >> b) & 1u) put(s++, ml_add_step_raw(T, Q));
+  }
+}
+
+// get(k, step) -> the unevaluated line of pair k at that step
+template <int K, class Get>
+LSG_INL fp12_t miller_accum_multi(const g1a_t (&P)[K], const bool (&use)[K], Get&& get) {
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  fp12_t f = fp12_one();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    line_t L = line_eval(get(k, 0), P[k].x, P[k].y);
+    fp12_t g = k > 0 ? fp12_mul_line(f, L.l00, L.l01, L.l11) : fp12_from_line(L);
+    f = fp12_select(use[k], g, f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    line_t L = line_eval(get(k, 1), P[k].x, P[k].y);
+    f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
+  }
+  int s = 2;
+#pragma unroll 1
+  for (int b = 61; b >= 0; b--) {
+    f = fp12_sqr(f);
+    const int n_steps = 1 + (int)((xa >> b) & 1u);
+#pragma unroll 1
+    for (int j = 0; j < n_steps; j++, s++) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        line_t L = line_eval(get(k, s), P[k].x, P[k].y);
         f = fp12_select(use[k], fp12_mul_line(f, L.l00, L.l01, L.l11), f);
       }
     }

@@ -146,6 +146,28 @@ void hc_miller_multi4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t
   wr12(out576, miller_loop_multi<4>(P, Q, use));
 }
 
+// the split multi-Miller loop over 4 pairs: miller_lines per Q, then miller_accum_multi
+// (lsg_pairing.hpp; the device kernels k_miller_lines / k_miller_accum)
+void hc_miller_split4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t* use4, uint8_t* out576) {
+  g1a_t P[4];
+  bool use[4];
+  static line_t lines[4][ML_STEPS];
+  for (int k = 0; k < 4; k++) {
+    bool inf;
+    g2a_t Q;
+    g1_deserialize(P[k], inf, p96x4 + 96 * k, 96);
+    g2_deserialize_uncompressed(Q, inf, q192x4 + 192 * k);
+    use[k] = use4[k] != 0;
+    int cnt = 0;
+    miller_lines(Q, [&](int st, const line_t& L) {
+      lines[k][st] = L;
+      cnt++;
+    });
+    if (cnt != ML_STEPS) abort();
+  }
+  wr12(out576, miller_accum_multi<4>(P, use, [&](int k, int st) { return lines[k][st]; }));
+}
+
 void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32, uint64_t r, unsigned long long* counts) {
   g2a_t s;
   g1a_t pk;
@@ -199,6 +221,17 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
     lsg_mul_count = 0;
     (void)miller_loop_multi<2>(P2, H2, use2);
     counts[11] = lsg_mul_count / 2;
+  }
+  {  // split device path: line schedule per set, then the accumulation over K = 2 pairs
+    line_t lines[ML_STEPS];
+    lsg_mul_count = 0;
+    miller_lines(H, [&](int st, const line_t& L) { lines[st] = L; });
+    counts[12] = lsg_mul_count;
+    g1a_t P2[2] = {P, P};
+    bool use2[2] = {true, true};
+    lsg_mul_count = 0;
+    (void)miller_accum_multi<2>(P2, use2, [&](int, int st) { return lines[st]; });
+    counts[13] = lsg_mul_count / 2;
   }
   lsg_mul_count = 0;
   (void)g2_add(rs, rs);

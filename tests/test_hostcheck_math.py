@@ -247,3 +247,22 @@ def test_miller_loop_multi_is_product_of_single_loops(hc):
             if u:
                 exp = f12_mul(exp, f)
         assert ub12(o.raw) == exp, use
+
+
+def test_split_miller_loop_equals_multi_loop(hc):
+    """lsg_pairing.hpp:miller_lines + miller_accum_multi (the device's k_miller_lines /
+    k_miller_accum split) give the same field element as the product of single Miller loops
+    (oracle/pairing.py:miller_loop_fast); dropped pairs contribute 1."""
+    from oracle.fields import f12_mul, F12_ONE
+    pairs = [(E1.mul(G1_GEN, 5 + 3 * k), E2.mul(G2_GEN, 17 + 11 * k)) for k in range(4)]
+    pb = b"".join(g1_serialize(p) for p, _ in pairs)
+    qb = b"".join(g2_serialize(q) for _, q in pairs)
+    singles = [miller_loop_fast(p, q) for p, q in pairs]
+    for use in ([1, 1, 1, 1], [0, 1, 1, 1], [1, 0, 0, 1], [0, 0, 0, 0]):
+        o = buf(576)
+        hc.hc_miller_split4(pb, qb, (ctypes.c_int32 * 4)(*use), o)
+        exp = F12_ONE
+        for u, f in zip(use, singles):
+            if u:
+                exp = f12_mul(exp, f)
+        assert ub12(o.raw) == exp, use
