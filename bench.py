@@ -52,6 +52,30 @@ def make_shard(ctx, rank, n):
     return [([pks[(base + i) % keys]], msgs[i], sigs[i]) for i in range(n)]
 
 
+def make_block(ctx, rank, n):
+    """SURVEY 8(d) config C, "full mainnet block body": n aggregate-attestation sets of 440-460
+    signers each (~450), distinct messages.  Keys live in the device pubkey table (8f(1),
+    lsg_pubkey_table_set over the 1024 interop keys) and sets name their signers by index,
+    as the node's index2pubkey cache does; signatures are (sum sk) * H(m)."""
+    from lodestar_amd._native import PkIndices
+    keys = 1024
+    sks = [interop_sk(i) for i in range(keys)]
+    errs = ctx.pubkey_table_set(0, ctx.sk_to_pk(sks))
+    if any(errs):
+        raise SystemExit("pubkey table load failed")
+    idx, agg_sk, msgs = [], [], []
+    for i in range(n):
+        g = rank * n + i
+        size = 440 + (g * 7) % 21
+        start = (g * 53) % keys
+        ix = [(start + j) % keys for j in range(size)]
+        idx.append(PkIndices(ix))
+        agg_sk.append(sum(sks[k] for k in ix) % R_ORDER)
+        msgs.append(hashlib.sha256(b"lodestar-mi355x" + b"block" + g.to_bytes(8, "little")).digest())
+    sigs = ctx.sign(agg_sk, msgs)
+    return [(idx[i], msgs[i], sigs[i]) for i in range(n)]
+
+
 def host_cores():
     """Host threads this job may use: the box's CPU share (OMP_NUM_THREADS is set to it on the
     GPU box; os.cpu_count() there shows the whole machine), else the affinity mask."""
@@ -102,11 +126,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=192)
     ap.add_argument("--warmup", type=int, default=24)
-    ap.add_argument("--sets-per-gpu", type=int, default=4096)
+    ap.add_argument("--workload", choices=["firehose", "block"], default="firehose",
+                    help="firehose: config D shard (default, the headline line); block: config C")
+    ap.add_argument("--sets-per-gpu", type=int, default=None, help="sets per step (4096 firehose, 128 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=4, help="submissions in flight (<= library pipeline slots)")
-    ap.add_argument("--groups", type=int, default=6, help="batches (steps) per submission, verified as separate RLC groups")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="batches (steps) per submission, verified as separate RLC groups (6 firehose, 32 block)")
     args = ap.parse_args()
+    block = args.workload == "block"
+    if args.sets_per_gpu is None:
+        args.sets_per_gpu = 128 if block else 4096
+    if args.groups is None:
+        args.groups = 32 if block else 6
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -122,7 +154,7 @@ def main():
     ctx = Context(local)
     n = args.sets_per_gpu
     M = max(1, args.groups)
-    sets = make_shard(ctx, rank, n * M)
+    sets = make_block(ctx, rank, n * M) if block else make_shard(ctx, rank, n * M)
     # M steps' shards staged as one package; each ticket verifies them as M separate RLC
     # batches (groups of n sets, one Miller partial and one final exponentiation each)
     staged = ctx.stage(sets, seed=0x5EED + rank)
@@ -170,15 +202,16 @@ def main():
                 parts = [parts]
             if capture:  # HIP-event kernel times of this ticket (recorded on the kernels' own streams)
                 times.append(ctx.last_kernel_times())
-            fts = [ctx.final_submit(pg) for pg in gather(parts)]
-            pend_f.append((fts, t_sub, anyerr))
+            ft = ctx.final_submit_groups(gather(parts))  # the M batches' final checks in one ticket
+            if ft is None:
+                raise SystemExit("final-exponentiation entries exhausted")
+            pend_f.append((ft, t_sub, anyerr))
             if submitted < k_tickets:
                 pend_b.append((submit(), time.perf_counter()))
                 submitted += 1
             while pend_f and (len(pend_f) > 1 or not pend_b):
-                fts0, t0, ae = pend_f.popleft()
-                for tf0 in fts0:
-                    check(ae, ctx.final_wait(tf0))
+                ft0, t0, ae = pend_f.popleft()
+                check(ae, all(ctx.final_wait_groups(ft0)))
                 lat.append(time.perf_counter() - t0)
         return lat, times
 
@@ -208,7 +241,8 @@ def main():
     for ticket_times in ktimes:
         for name, ms in ticket_times:
             agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
-    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_h2c_map": "hash_map", "k_sig_scale": "sig_scale",
+    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_miller_accum": "miller_accum2_per_set",
+                "k_miller_lines": "miller_lines", "k_h2c_map": "hash_map", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
     per_set = {k: v for k, v in agg.items() if k in stage_of}
     dom = max(per_set, key=per_set.get)
@@ -221,21 +255,36 @@ def main():
     total_sets = n * world * steps
     value = total_sets / elapsed
     # whole-path work per set: the per-set stages with the bucket-MSM signature sums (groups of
-    # n >= 256 sets take the MSM path) plus each group's share of its per-group stages
-    per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / n
+    # n >= 256 sets take the MSM path, smaller ones per-set [r_i] sig_i) plus each group's share
+    # of its per-group stages, plus one G1 addition per extra signer of an aggregate set
+    if n >= 256:
+        per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / n
+    else:
+        per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / n
+    pks_per_set = sum(len(p) for p, _, _ in sets) / len(sets)
+    per_set_muls += (pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_oracle(sets)
+            if block:  # the CPU path gets the aggregated keys for free (favours the CPU)
+                cpu = cpu_baseline_oracle([([ctx.aggregate_pubkeys(p)[0]], m, sg) for p, m, sg in sets[:256]])
+                cpu["sample"] += "; pubkey aggregation (main thread in the reference) excluded"
+            else:
+                cpu = cpu_baseline_oracle(sets)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "firehose-32k shard (SURVEY 8d config D): single-pubkey gossip sets, RLC batch "
-                                   "per GPU, RCCL all-gather of Fp12 partials, one final exponentiation",
-                       "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
-                       "parallelism": f"shard{world}"},
+            "config": ({"workload": "block-body (SURVEY 8d config C): aggregate-attestation sets of 440-460 "
+                                    "signers named by index into the device pubkey table, distinct messages, one "
+                                    "RLC multi-pairing per block",
+                        "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
+                        "pubkeys_per_set": round(pks_per_set, 1), "parallelism": f"shard{world}"} if block else
+                       {"workload": "firehose-32k shard (SURVEY 8d config D): single-pubkey gossip sets, RLC batch "
+                                    "per GPU, RCCL all-gather of Fp12 partials, one final exponentiation",
+                        "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
+                        "parallelism": f"shard{world}"}),
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
             "pipeline_depth": args.depth, "batches_per_submission": M,

@@ -57,6 +57,11 @@ extern "C" {
 /* non-blst job errors */
 #define LSG_ERR_EMPTY_SET 100        /* maybeBatch.ts:29-31 "Empty signature set" */
 #define LSG_ERR_EMPTY_AGGREGATE 101  /* PublicKey.aggregate([]) "EMPTY_AGGREGATE_ARRAY" */
+#define LSG_ERR_BAD_INDEX 102        /* a pubkey index outside the loaded table (index2pubkey[i] undefined) */
+
+/* lsg_set.pk_len value for keys given by validator index into the context's pubkey table
+ * (lsg_pubkey_table_set): pks then points at n_pks uint32 indices (host byte order). */
+#define LSG_PK_INDEX 4u
 
 /* ---- job verdicts (WorkResult<boolean>, multithread/types.ts:21-24) */
 #define LSG_INVALID 0 /* {code: success, result: false} */
@@ -139,7 +144,8 @@ int lsg_verify_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t s
 int lsg_verify_sets(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_job_result* result);
 
 /* PublicKey.aggregate(pks).toBytes(uncompressed): out96 receives the 96-byte affine sum.
- * *err_code = BLST_* for a bad input key, LSG_ERR_EMPTY_AGGREGATE for n == 0. */
+ * *err_code = BLST_* for a bad input key, LSG_ERR_EMPTY_AGGREGATE for n == 0.  With
+ * pk_len == LSG_PK_INDEX, pks holds n uint32 indices into the pubkey table. */
 int lsg_aggregate_pubkeys(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96,
                           int32_t* err_code);
 
@@ -174,6 +180,36 @@ int lsg_batch_submit_groups(lsg_ctx* ctx, const lsg_staged* staged, size_t group
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
 int lsg_final_submit(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket);
 int lsg_final_wait(lsg_ctx* ctx, lsg_ticket ticket, int32_t* valid);
+/* Several RLC batches' final checks in one ticket (one launch per stage instead of one
+ * ticket per batch): n_groups groups of per_group partials each, group g being partials
+ * g*per_group .. g*per_group+per_group-1 (e.g. one per rank); lsg_final_wait_groups writes
+ * n_groups verdicts.  lsg_final_submit(p, n) is lsg_final_submit_groups(p, 1, n). */
+int lsg_final_submit_groups(lsg_ctx* ctx, const uint8_t* partials576, size_t n_groups, size_t per_group,
+                            lsg_ticket* ticket);
+int lsg_final_wait_groups(lsg_ctx* ctx, lsg_ticket ticket, int32_t* valid /* [n_groups] */);
+
+/* ---- Validator pubkey table resident in HBM.  Replaces the per-call
+ * PublicKey -> bytes hand-off of the pool (multithread/index.ts:177, utils.ts:11) with the
+ * node's index2pubkey cache held on the GPU (state-transition/src/cache/pubkeyCache.ts:60-75
+ * syncPubkeys, cache/epochContext.ts:701-704 addPubkey): keys are decoded once, as
+ * PublicKey.fromBytes(pk, jacobian) does there (on-curve check, no subgroup check: cached
+ * keys were validated at deposit time), and sets then name their keys by index
+ * (lsg_set.pk_len = LSG_PK_INDEX); aggregation gathers them on the device.
+ *   lsg_pubkey_table_set  keys first_index .. first_index+n-1 <- pks (48 or 96 bytes each);
+ *                         the table grows as needed (growth waits for in-flight work).
+ *                         err[k] (may be NULL) = BLST_* of key k; a key that does not decode
+ *                         leaves its index unset, and a set naming an unset index fails
+ *                         its package with LSG_ERR_BAD_INDEX (as deserializeSet throws).
+ *   lsg_pubkey_table_size number of indices (highest set index + 1). */
+int lsg_pubkey_table_set(lsg_ctx* ctx, size_t first_index, const uint8_t* pks, uint32_t pk_len, size_t n,
+                         int32_t* err);
+int lsg_pubkey_table_size(lsg_ctx* ctx, size_t* n);
+
+/* Batched KeyValidate: PublicKey.fromBytes(pk, affine, validate=true) of
+ * processDeposit.ts:57-65 for n keys of pk_len (48/96) bytes -- decode, not the point at
+ * infinity (BLST_PK_IS_INFINITY), in the r-torsion subgroup (BLST_POINT_NOT_IN_GROUP).
+ * err[i] = BLST_* (0 = valid); out96 (may be NULL) = the uncompressed affine key. */
+int lsg_pubkey_validate(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96, int32_t* err);
 
 /* Test/bench input generation (not on the verify path): sig_i = sk_i * H(m_i) compressed,
  * pk_i = sk_i * G1 uncompressed; sks are 32-byte big-endian secret keys. */

@@ -29,6 +29,8 @@ BLST_NAMES = {
 }
 LSG_ERR_EMPTY_SET = 100
 LSG_ERR_EMPTY_AGGREGATE = 101
+LSG_ERR_BAD_INDEX = 102
+LSG_PK_INDEX = 4  # lsg_set.pk_len for keys named by pubkey-table index
 
 
 def error_message(code):
@@ -38,11 +40,24 @@ def error_message(code):
         return "Empty signature set"
     if code == LSG_ERR_EMPTY_AGGREGATE:
         return "EMPTY_AGGREGATE_ARRAY"
+    if code == LSG_ERR_BAD_INDEX:
+        return "Unknown pubkey index"
     return "BLST_ERROR: " + BLST_NAMES.get(code, f"BLST_UNKNOWN_{code}")
 
 
 class NativeUnavailable(RuntimeError):
     pass
+
+
+class PkIndices(list):
+    """A set's pubkeys given as validator indices into the context's pubkey table
+    (Context.pubkey_table_set; lsg_set.pk_len = LSG_PK_INDEX) instead of encoded bytes."""
+
+    def tobytes(self):
+        import array
+        a = array.array("I", self)
+        assert a.itemsize == 4
+        return a.tobytes()
 
 
 class LsgSet(ctypes.Structure):
@@ -78,6 +93,8 @@ EXPORTS = [
     "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
     "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
     "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups", "lsg_probe_mad_peak",
+    "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
+    "lsg_final_submit_groups", "lsg_final_wait_groups",
 ]
 
 
@@ -118,6 +135,11 @@ def load_library(path=LIB_PATH):
         lib.lsg_staged_free.argtypes = [vp, vp]
         lib.lsg_batch_submit.argtypes = [vp, vp, pu64]
         lib.lsg_batch_submit_groups.argtypes = [vp, vp, sz, pu64]
+        lib.lsg_pubkey_table_set.argtypes = [vp, sz, ctypes.c_char_p, u32, sz, pi32]
+        lib.lsg_pubkey_table_size.argtypes = [vp, ctypes.POINTER(sz)]
+        lib.lsg_final_submit_groups.argtypes = [vp, ctypes.c_char_p, sz, sz, pu64]
+        lib.lsg_final_wait_groups.argtypes = [vp, u64, pi32]
+        lib.lsg_pubkey_validate.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
         lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
@@ -140,10 +162,13 @@ class SetBuffer:
         sets = list(sets)
         self.arr = (LsgSet * max(len(sets), 1))()
         for i, (pks, msg, sig) in enumerate(sets):
-            pk_len = len(pks[0]) if pks else 96
-            if any(len(p) != pk_len for p in pks):
-                raise ValueError("all pubkeys of one set must share one encoding length")
-            pkb = b"".join(pks)
+            if isinstance(pks, PkIndices):
+                pk_len, pkb = LSG_PK_INDEX, pks.tobytes()
+            else:
+                pk_len = len(pks[0]) if pks else 96
+                if any(len(p) != pk_len for p in pks):
+                    raise ValueError("all pubkeys of one set must share one encoding length")
+                pkb = b"".join(pks)
             for b in (pkb, msg, sig):
                 self._keep.append(b)
             s = self.arr[i]
@@ -253,12 +278,41 @@ class Context:
         return res.status, res.err_code
 
     def aggregate_pubkeys(self, pks):
-        pk_len = len(pks[0]) if pks else 96
+        """pks: list of encoded keys, or PkIndices into the pubkey table."""
+        if isinstance(pks, PkIndices):
+            pk_len, pkb = LSG_PK_INDEX, pks.tobytes()
+        else:
+            pk_len, pkb = (len(pks[0]) if pks else 96), b"".join(pks)
         out = ctypes.create_string_buffer(96)
         err = ctypes.c_int32()
-        self._check(self.lib.lsg_aggregate_pubkeys(self.h, b"".join(pks), pk_len, len(pks), out, ctypes.byref(err)),
+        self._check(self.lib.lsg_aggregate_pubkeys(self.h, pkb, pk_len, len(pks), out, ctypes.byref(err)),
                     "lsg_aggregate_pubkeys")
         return out.raw, err.value
+
+    def pubkey_table_set(self, first_index, pks):
+        """index2pubkey[first_index + k] = pks[k] on the device; returns per-key BLST codes."""
+        n = len(pks)
+        pk_len = len(pks[0]) if pks else 96
+        err = (ctypes.c_int32 * max(n, 1))()
+        self._check(self.lib.lsg_pubkey_table_set(self.h, first_index, b"".join(pks), pk_len, n, err),
+                    "lsg_pubkey_table_set")
+        return list(err[:n])
+
+    def pubkey_table_size(self):
+        n = ctypes.c_size_t()
+        self._check(self.lib.lsg_pubkey_table_size(self.h, ctypes.byref(n)), "lsg_pubkey_table_size")
+        return n.value
+
+    def pubkey_validate(self, pks):
+        """Batched KeyValidate: [(uncompressed 96 B, BLST code)] per key."""
+        n = len(pks)
+        if n == 0:
+            return []
+        pk_len = len(pks[0])
+        out = ctypes.create_string_buffer(96 * n)
+        err = (ctypes.c_int32 * n)()
+        self._check(self.lib.lsg_pubkey_validate(self.h, b"".join(pks), pk_len, n, out, err), "lsg_pubkey_validate")
+        return [(out.raw[96 * k:96 * k + 96], err[k]) for k in range(n)]
 
     def hash_to_g2(self, msgs, dst=b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"):
         if not msgs:
@@ -336,6 +390,27 @@ class Context:
         v = ctypes.c_int32()
         self._check(self.lib.lsg_final_wait(self.h, ticket, ctypes.byref(v)), "lsg_final_wait")
         return bool(v.value)
+
+    def final_submit_groups(self, groups):
+        """groups: list of equal-length lists of 576-byte partials -> one ticket, one final
+        exponentiation per group."""
+        ng = len(groups)
+        pg = len(groups[0]) if groups else 0
+        if any(len(g) != pg for g in groups):
+            raise ValueError("every group needs the same number of partials")
+        t = ctypes.c_uint64()
+        rc = self.lib.lsg_final_submit_groups(self.h, b"".join(b"".join(g) for g in groups), ng, pg, ctypes.byref(t))
+        if rc == LSG_ERR_BUSY:
+            return None
+        self._check(rc, "lsg_final_submit_groups")
+        t_ng = ng
+        return (t.value, t_ng)
+
+    def final_wait_groups(self, ticket):
+        t, ng = ticket
+        v = (ctypes.c_int32 * max(ng, 1))()
+        self._check(self.lib.lsg_final_wait_groups(self.h, t, v), "lsg_final_wait_groups")
+        return [bool(x) for x in v[:ng]]
 
     def sign(self, sks, msgs):
         """sks: list of ints (< r); msgs: equal-length bytes.  Returns compressed signatures."""

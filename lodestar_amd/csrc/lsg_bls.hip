@@ -136,19 +136,50 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_SUBGROUP_WAVES) k_sig_subgroup(int n, cons
   if (lead && !ok) err[item] = LSG_BLST_POINT_NOT_IN_GROUP;
 }
 
-// pubkey -> projective G1 (infinity and undecodable keys become (0:1:0))
+// pubkey -> projective G1 (infinity and undecodable keys become (0:1:0)).  A key given by
+// index (len == LSG_PK_INDEX: the slot's first 4 bytes) is gathered from the resident table
+// (tab, tab_ok: decoded keys of lsg_pubkey_table_set; tab_n indices).
 __global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ pk,
                                                         const uint32_t* __restrict__ pk_len, uint32_t* __restrict__ pkp,
-                                                        int32_t* __restrict__ err) {
+                                                        int32_t* __restrict__ err, const uint32_t* __restrict__ tab,
+                                                        const uint8_t* __restrict__ tab_ok, uint32_t tab_n) {
   LANE_ITEM(n);
   uint32_t len = pk_len[item];
+  g1p_t p = proj_inf<fp_t>();
+  int e;
+  if (len == LSG_PK_INDEX) {
+    const uint8_t* b = pk + 96 * item;
+    const uint32_t idx = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+    const bool ok = idx < tab_n && tab_ok[idx];
+    e = ok ? 0 : LSG_ERR_BAD_INDEX;
+    if (ok) p = lane_load<g1p_t>(tab, idx);
+  } else {
+    g1a_t a;
+    a.x = fp_zero();
+    a.y = fp_zero();
+    bool is_inf = false;
+    e = (len == 48 || len == 96) ? g1_deserialize(a, is_inf, pk + 96 * item, (int)len) : LSG_BLST_INVALID_SIZE;
+    if (e == 0 && !is_inf) p = proj_from_aff(a);
+  }
+  lane_store(pkp, item, p);
+  if (lead) err[item] = e;
+}
+
+// KeyValidate (lsg_pubkey_validate): decode, reject infinity and points outside G1; pts
+// receives the key as a projective point (the identity for rejected keys); keys sit in the
+// staging arena's 96-byte slots
+__global__ void LSG_KERNEL_ATTR k_pk_validate(int n, const uint8_t* __restrict__ pk, uint32_t len,
+                                              uint32_t* __restrict__ pts, int32_t* __restrict__ err) {
+  LANE_ITEM(n);
   g1a_t a;
   a.x = fp_zero();
   a.y = fp_zero();
   bool is_inf = false;
-  int e = (len == 48 || len == 96) ? g1_deserialize(a, is_inf, pk + 96 * item, (int)len) : LSG_BLST_INVALID_SIZE;
-  g1p_t p = (e == 0 && !is_inf) ? proj_from_aff(a) : proj_inf<fp_t>();
-  lane_store(pkp, item, p);
+  int e = g1_deserialize(a, is_inf, pk + 96 * item, (int)len);
+  if (e == 0 && is_inf) e = LSG_BLST_PK_IS_INFINITY;
+  const g1p_t p = e == 0 ? proj_from_aff(a) : proj_inf<fp_t>();
+  if (e == 0 && !g1_in_group(p)) e = LSG_BLST_POINT_NOT_IN_GROUP;
+  lane_store(pts, item, e == 0 ? p : proj_inf<fp_t>());
   if (lead) err[item] = e;
 }
 
@@ -667,6 +698,10 @@ struct lsg_staged {
   std::vector<std::vector<int32_t>> sets_pks;  // per set: indices of its pubkeys
   std::vector<uint64_t> rnd;                   // per set: the RLC randomizer r_i
   mutable MsmPlan msm;                         // bucket plan of the last grouping submitted
+  // pubkey-aggregation tree plan of sets_pks, built and uploaded by the first submission
+  mutable TreePlan pk_plan;
+  mutable DevBuf d_pk_plan;
+  mutable bool pk_plan_valid = false;
 };
 
 namespace {
@@ -737,6 +772,9 @@ struct lsg_ctx {
   Slot util;
   uint64_t next_serial = 1;
   const Slot* last = nullptr;  // slot whose timers lsg_last_kernel_times reports
+  // validator pubkey table (lsg_pubkey_table_set): projective lane-form keys + validity bytes
+  DevBuf d_pktab, d_pktab_ok;
+  size_t pktab_n = 0, pktab_cap = 0;
 };
 
 namespace {
@@ -872,6 +910,8 @@ void free_host(HostBuf& b) {
 void staged_free(lsg_staged* in) {
   DevBuf* bufs[] = {&in->d_sig, &in->d_siglen, &in->d_msg, &in->d_msgoff, &in->d_msglen, &in->d_pk, &in->d_pklen, &in->d_rnd};
   for (DevBuf* b : bufs) free_dev(*b);
+  free_dev(in->d_pk_plan);
+  in->pk_plan_valid = false;
   free_dev(in->msm.d_buckets);
   free_dev(in->msm.d_bits);
   in->msm.valid = false;
@@ -942,6 +982,7 @@ int stage_sets(Slot* s, lsg_staged* in, const lsg_set* const* sets, size_t n, ui
   in->sets_pks.assign(n, {});
   in->rnd.assign(n, 0);
   in->msm.valid = false;
+  in->pk_plan_valid = false;
   size_t mo = 0, po = 0;
   uint64_t sd = seed;
   FILE* ur = nullptr;
@@ -958,7 +999,8 @@ int stage_sets(Slot* s, lsg_staged* in, const lsg_set* const* sets, size_t n, ui
     // a set without keys points at pk 0 and is reported as an empty aggregate
     for (uint32_t k = 0; k < q->n_pks; k++) {
       pklen[po] = q->pk_len;
-      if (q->pk_len == 48 || q->pk_len == 96) memcpy(A + o_pk + 96 * po, q->pks + (size_t)q->pk_len * k, q->pk_len);
+      if (q->pk_len == 48 || q->pk_len == 96 || q->pk_len == LSG_PK_INDEX)
+        memcpy(A + o_pk + 96 * po, q->pks + (size_t)q->pk_len * k, q->pk_len);
       in->sets_pks[i].push_back((int32_t)po);
       po++;
     }
@@ -1238,8 +1280,21 @@ int launch_set_stages(Slot* s) {
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
   if (np > 0) {
     LAUNCH(s, k_pk_decode, np, np, P_<uint8_t>(in->d_pk), P_<uint32_t>(in->d_pklen), P_<uint32_t>(s->d_pkp),
-           P_<int32_t>(s->d_pkerr));
-    int rc = tree_reduce<0>(s, 1, "tree_g1_aggregate", P_<uint32_t>(s->d_pkp), in->sets_pks, P_<uint32_t>(s->d_agg));
+           P_<int32_t>(s->d_pkerr), P_<uint32_t>(s->c->d_pktab), P_<uint8_t>(s->c->d_pktab_ok),
+           (uint32_t)s->c->pktab_n);
+    // the package's aggregation plan is built once (an aggregate-heavy package has ~450 keys
+    // per set) and reused by every ticket that submits it
+    if (!in->pk_plan_valid) {
+      in->pk_plan = plan_tree(in->sets_pks);
+      int rc = ensure(s, in->d_pk_plan, 4 * in->pk_plan.idx.size());
+      if (rc) return rc;
+      // synchronous: other slots may submit the same package before this stream runs
+      LSG_HIP(s, hipMemcpy(in->d_pk_plan.p, in->pk_plan.idx.data(), 4 * in->pk_plan.idx.size(),
+                           hipMemcpyHostToDevice));
+      in->pk_plan_valid = true;
+    }
+    int rc = run_tree<0>(s, 1, "tree_g1_aggregate", in->pk_plan, P_<int32_t>(in->d_pk_plan), P_<uint32_t>(s->d_pkp),
+                         P_<uint32_t>(s->d_agg));
     if (rc) return rc;
   }
   LAUNCH(s, k_pk_scale, n, n, P_<uint32_t>(s->d_agg), P_<uint64_t>(in->d_rnd), P_<uint32_t>(s->d_Pp),
@@ -1637,35 +1692,39 @@ int wait_batch(Slot* s, uint8_t* out576, int32_t* set_err, int32_t* any_error) {
   return LSG_OK;
 }
 
-int submit_final(Slot* s, const uint8_t* partials576, size_t n) {
+// ng groups of pg partials each (group g: partials g*pg .. g*pg+pg-1) -> per group the
+// product of its partials and one final exponentiation; all groups in one launch per stage
+int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg) {
   timer_reset(s);
   s->n_verdicts = 0;
   int rc;
-  size_t np = std::max(n, (size_t)1);
+  const size_t n = ng * pg, np = std::max(n, (size_t)1), gq = std::max(ng, (size_t)1);
   if ((rc = ensure_host(s, s->h_blob, 576 * np)) || (rc = ensure(s, s->d_blob, 576 * np)) ||
-      (rc = ensure(s, s->d_aux, 4 * W_F12 * np)) || (rc = ensure(s, s->d_F, 4 * W_F12)) ||
-      (rc = ensure(s, s->d_verdict, 4)) || (rc = ensure_host(s, s->h_verdict, 4)))
+      (rc = ensure(s, s->d_aux, 4 * W_F12 * np)) || (rc = ensure(s, s->d_F, 4 * W_F12 * gq)) ||
+      (rc = ensure(s, s->d_verdict, 4 * gq)) || (rc = ensure_host(s, s->h_verdict, 4 * gq)))
     return rc;
   if (n) {
     hipStream_t S = s->st[0];
     memcpy(s->h_blob.p, partials576, 576 * n);
     LSG_HIP(s, hipMemcpyAsync(s->d_blob.p, s->h_blob.p, 576 * n, hipMemcpyHostToDevice, S));
     LAUNCH(s, k_blobs_to_fp12, n, (int)n, P_<uint8_t>(s->d_blob), P_<uint32_t>(s->d_aux));
-    std::vector<std::vector<int32_t>> g(1);
-    for (size_t k = 0; k < n; k++) g[0].push_back((int32_t)k);
+    std::vector<std::vector<int32_t>> g(ng);
+    for (size_t k = 0; k < n; k++) g[k / pg].push_back((int32_t)k);
     if ((rc = tree_reduce<2>(s, 0, "tree_fp12_product", P_<uint32_t>(s->d_aux), g, P_<uint32_t>(s->d_F)))) return rc;
-    LAUNCH(s, k_fp12_to_canon, 1, 1, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
-    LAUNCH_ROW(s, "k_row_final_exp", lsg_row_final_exp(S, 1, P_<uint8_t>(s->d_blob), P_<int32_t>(s->d_verdict)));
-    LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4, hipMemcpyDeviceToHost, S));
-    s->n_verdicts = 1;
+    LAUNCH(s, k_fp12_to_canon, ng, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_blob));
+    LAUNCH_ROW(s, "k_row_final_exp", lsg_row_final_exp(S, (int)ng, P_<uint8_t>(s->d_blob), P_<int32_t>(s->d_verdict)));
+    LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
+    s->n_verdicts = ng;
   }
   LSG_HIP(s, hipEventRecord(s->ev_done, s->st[0]));
   return LSG_OK;
 }
 
+// valid[0 .. max(n_verdicts, 1)) (0 for a ticket without partials)
 int wait_final(Slot* s, int32_t* valid) {
   LSG_HIP(s, hipEventSynchronize(s->ev_done));
-  *valid = s->n_verdicts ? H_<int32_t>(s->h_verdict)[0] : 0;
+  if (!s->n_verdicts) valid[0] = 0;
+  for (size_t g = 0; g < s->n_verdicts; g++) valid[g] = H_<int32_t>(s->h_verdict)[g];
   return LSG_OK;
 }
 
@@ -1754,6 +1813,8 @@ int lsg_destroy(lsg_ctx* c) {
   for (Slot& s : c->slots) slot_destroy(&s);
   for (Slot& s : c->finals) slot_destroy(&s);
   slot_destroy(&c->util);
+  free_dev(c->d_pktab);
+  free_dev(c->d_pktab_ok);
   if (c->s_final) (void)hipStreamDestroy(c->s_final);
   for (hipStream_t st : c->s_fe)
     if (st) (void)hipStreamDestroy(st);
@@ -1923,15 +1984,16 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
   return lsg_batch_wait(c, t, out576, set_err, any_error);
 }
 
-int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket) {
-  if (!c || !ticket || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+int lsg_final_submit_groups(lsg_ctx* c, const uint8_t* partials576, size_t n_groups, size_t per_group,
+                            lsg_ticket* ticket) {
+  if (!c || !ticket || (n_groups && per_group && !partials576) || (n_groups && !per_group)) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
   Slot* s = free_slot(c, c->finals, LSG_FINALS);
   if (!s) {
     c->err = "all final-exponentiation entries are busy";
     return LSG_ERR_BUSY;
   }
-  int rc = submit_final(s, partials576, n_partials);
+  int rc = submit_final(s, partials576, n_groups, per_group);
   if (rc) {
     sync_slot(s);
     return rc;
@@ -1940,12 +2002,32 @@ int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, 
   return LSG_OK;
 }
 
+int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+  return lsg_final_submit_groups(c, partials576, n_partials ? 1 : 0, n_partials, ticket);
+}
+
+int lsg_final_wait_groups(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) {
+  if (!c || !valid) return LSG_ERR_INVALID_ARG;
+  if (int prc = presync(c, ticket, SLOT_FINAL)) return prc;
+  LSG_ENTER(c);
+  Slot* s = ticket_slot(c, ticket, SLOT_FINAL);
+  if (!s) return LSG_ERR_INVALID_ARG;
+  int rc = wait_final(s, valid);
+  release(c, s);
+  return rc;
+}
+
 int lsg_final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) {
   if (!c || !valid) return LSG_ERR_INVALID_ARG;
   if (int prc = presync(c, ticket, SLOT_FINAL)) return prc;
   LSG_ENTER(c);
   Slot* s = ticket_slot(c, ticket, SLOT_FINAL);
   if (!s) return LSG_ERR_INVALID_ARG;
+  if (s->n_verdicts > 1) {
+    c->err = "ticket carries several groups: use lsg_final_wait_groups";
+    return LSG_ERR_INVALID_ARG;
+  }
   int rc = wait_final(s, valid);
   release(c, s);
   return rc;
@@ -1982,7 +2064,7 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
   if ((rc = size_state(s, 0))) return rc;
   int np = (int)n;
   LAUNCH(s, k_pk_decode, np, np, P_<uint8_t>(s->own.d_pk), P_<uint32_t>(s->own.d_pklen), P_<uint32_t>(s->d_pkp),
-         P_<int32_t>(s->d_pkerr));
+         P_<int32_t>(s->d_pkerr), P_<uint32_t>(c->d_pktab), P_<uint8_t>(c->d_pktab_ok), (uint32_t)c->pktab_n);
   if ((rc = tree_reduce<0>(s, 1, "tree_g1_aggregate", P_<uint32_t>(s->d_pkp), s->own.sets_pks, P_<uint32_t>(s->d_agg))))
     return rc;
   LAUNCH(s, k_g1p_to_bytes, 1, 1, P_<uint32_t>(s->d_agg), P_<uint8_t>(s->d_blob));
@@ -1996,6 +2078,102 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
       *err_code = pkerr[k];
       break;
     }
+  return LSG_OK;
+}
+
+// pubkey table: keys decoded once on the device, gathered by index
+int lsg_pubkey_table_set(lsg_ctx* c, size_t first, const uint8_t* pks, uint32_t pk_len, size_t n, int32_t* err) {
+  if (!c || (n && !pks) || (pk_len != 48 && pk_len != 96) || first + n > 0xffffffffull) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  const size_t need = first + n, WG = lane_words<g1p_t>();
+  if (need > c->pktab_cap) {
+    // tickets in flight read the table: drain the device before moving it
+    LSG_HIPC(c, hipDeviceSynchronize());
+    size_t cap = std::max(std::max(need, 2 * c->pktab_cap), (size_t)1024);
+    DevBuf nt, nok;
+    LSG_HIPC(c, hipMalloc(&nt.p, 4 * WG * cap));
+    nt.cap = 4 * WG * cap;
+    hipError_t e = hipMalloc(&nok.p, cap);
+    if (e != hipSuccess) {
+      free_dev(nt);
+      return fail_c(c, "hipMalloc", e);
+    }
+    nok.cap = cap;
+    LSG_HIPC(c, hipMemset(nok.p, 0, cap));
+    if (c->pktab_n) {
+      LSG_HIPC(c, hipMemcpy(nt.p, c->d_pktab.p, 4 * WG * c->pktab_n, hipMemcpyDeviceToDevice));
+      LSG_HIPC(c, hipMemcpy(nok.p, c->d_pktab_ok.p, c->pktab_n, hipMemcpyDeviceToDevice));
+    }
+    free_dev(c->d_pktab);
+    free_dev(c->d_pktab_ok);
+    c->d_pktab = nt;
+    c->d_pktab_ok = nok;
+    c->pktab_cap = cap;
+  }
+  lsg_set q;
+  memset(&q, 0, sizeof(q));
+  q.pks = pks;
+  q.pk_len = pk_len;
+  q.n_pks = (uint32_t)n;
+  const lsg_set* qp = &q;
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, &qp, 1, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, 0))) return rc;
+  // decode straight into the table rows first .. first + n - 1
+  LAUNCH(s, k_pk_decode, n, (int)n, P_<uint8_t>(s->own.d_pk), P_<uint32_t>(s->own.d_pklen),
+         P_<uint32_t>(c->d_pktab) + WG * first, P_<int32_t>(s->d_pkerr), (const uint32_t*)nullptr,
+         (const uint8_t*)nullptr, 0u);
+  std::vector<int32_t> pkerr(n);
+  LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  std::vector<uint8_t> ok(n);
+  for (size_t k = 0; k < n; k++) {
+    ok[k] = pkerr[k] == 0 ? 1 : 0;
+    if (err) err[k] = pkerr[k];
+  }
+  LSG_HIP(s, hipMemcpy(P_<uint8_t>(c->d_pktab_ok) + first, ok.data(), n, hipMemcpyHostToDevice));
+  c->pktab_n = std::max(c->pktab_n, need);
+  c->last = s;
+  return LSG_OK;
+}
+
+int lsg_pubkey_table_size(lsg_ctx* c, size_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *n = c->pktab_n;
+  return LSG_OK;
+}
+
+// batched KeyValidate
+int lsg_pubkey_validate(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96, int32_t* err) {
+  if (!c || !err || (n && !pks) || (pk_len != 48 && pk_len != 96) || n > 0x7fffffffull) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  lsg_set q;
+  memset(&q, 0, sizeof(q));
+  q.pks = pks;
+  q.pk_len = pk_len;
+  q.n_pks = (uint32_t)n;
+  const lsg_set* qp = &q;
+  s->in = &s->own;
+  int rc;
+  if ((rc = stage_sets(s, &s->own, &qp, 1, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, 0))) return rc;
+  if ((rc = ensure(s, s->d_ub, 96 * n))) return rc;
+  LAUNCH(s, k_pk_validate, n, (int)n, P_<uint8_t>(s->own.d_pk), pk_len, P_<uint32_t>(s->d_pkp), P_<int32_t>(s->d_pkerr));
+  LSG_HIP(s, hipMemcpyAsync(err, s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  if (out96) {
+    LAUNCH(s, k_g1p_to_bytes, n, (int)n, P_<uint32_t>(s->d_pkp), P_<uint8_t>(s->d_ub));
+    LSG_HIP(s, hipMemcpyAsync(out96, s->d_ub.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  }
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
   return LSG_OK;
 }
 

@@ -326,6 +326,23 @@ LSG_BIGFN bool g2_in_group(g2p_t p) {
   return proj_eq(g2_psi(p), xp);
 }
 
+// G1 membership by definition, [r]P == O: double-and-add over the 255-bit group order
+// (KeyValidate of batched pubkey validation; not on the verify path, where keys are trusted)
+LSG_BIGFN bool g1_in_group(g1p_t p) {
+  const uint32_t rw[8] = {0x73eda753u, 0x299d7d48u, 0x3339d808u, 0x09a1d805u,
+                          0x53bda402u, 0xfffe5bfeu, 0xffffffffu, 0x00000001u};
+  g1p_t acc = proj_inf<fp_t>();
+#pragma unroll 1
+  for (int w = 0; w < 8; w++) {
+#pragma unroll 1
+    for (int b = 31; b >= 0; b--) {
+      acc = g1_dbl(acc);
+      if ((rw[w] >> b) & 1u) acc = g1_add(acc, p);
+    }
+  }
+  return proj_is_inf(acc);
+}
+
 LSG_INL bool g1_on_curve_aff(const g1a_t& a) {
   fp_t rhs = fp_add(fp_mul(fp_sqr(a.x), a.x), FP_B_G1);
   return fp_eq(fp_sqr(a.y), rhs);

@@ -20,7 +20,7 @@ import os
 from .fields import F12_ONE, f12_mul, f12_conj, f12_is_one
 from .curves import (
     E1, E2, G1_GEN, BlstError, BLST_INVALID_SIZE, BLST_PK_IS_INFINITY, BLST_POINT_NOT_IN_GROUP,
-    g1_deserialize, g2_deserialize, in_g2, g1_serialize, g1_compress,
+    g1_deserialize, g2_deserialize, in_g1, in_g2, g1_serialize, g1_compress,
 )
 from .hash_to_curve import hash_to_g2
 from .pairing import miller_loop_fast, final_exp_fast
@@ -43,6 +43,18 @@ def public_key_from_bytes(b):
     if len(b) not in (48, 96):
         raise BlstError(BLST_INVALID_SIZE)
     return g1_deserialize(bytes(b))
+
+
+def public_key_validate(b):
+    """PublicKey.fromBytes(bytes, CoordType.affine, validate=true) as processDeposit.ts:57-65
+    calls it (KeyValidate): decode, then blst rejects the identity (BLST_PK_IS_INFINITY) and
+    points outside the r-torsion subgroup (BLST_POINT_NOT_IN_GROUP).  SURVEY.md 8f(2)."""
+    pt = public_key_from_bytes(b)
+    if pt is None:
+        raise BlstError(BLST_PK_IS_INFINITY)
+    if not in_g1(pt):
+        raise BlstError(BLST_POINT_NOT_IN_GROUP)
+    return pt
 
 
 def aggregate_pubkeys(points):

@@ -89,3 +89,16 @@ def corrupt_infinity(s):
 
 
 CORRUPTIONS = [corrupt_wrong_message, corrupt_flip_x_bit, corrupt_truncate, corrupt_not_in_group, corrupt_infinity]
+
+
+def g1_not_in_group(seed=0):
+    """An E1 point outside the r-torsion subgroup (affine, on the curve): KeyValidate must
+    reject it with BLST_POINT_NOT_IN_GROUP (processDeposit.ts:57-65)."""
+    from oracle.curves import in_g1
+    from oracle.fields import fp_sqrt
+    x = 5 + 7 * seed
+    while True:
+        y = fp_sqrt((x * x * x + 4) % P)
+        if y is not None and not in_g1((x, y)):
+            return (x, y)
+        x += 1

@@ -168,6 +168,14 @@ void hc_miller_split4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t
   wr12(out576, miller_accum_multi<4>(P, use, [&](int k, int st) { return lines[k][st]; }));
 }
 
+// KeyValidate's subgroup test (lsg_curve.hpp:g1_in_group) on a 96-byte uncompressed point
+int hc_g1_in_group(const uint8_t* p96) {
+  g1a_t a;
+  bool inf;
+  if (g1_deserialize(a, inf, p96, 96) != 0) return -1;
+  return g1_in_group(inf ? proj_inf<fp_t>() : proj_from_aff(a)) ? 1 : 0;
+}
+
 void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32, uint64_t r, unsigned long long* counts) {
   g2a_t s;
   g1a_t pk;

@@ -308,6 +308,12 @@ def test_grouped_batch_submission(ctx):
             assert len(parts) == 3 and not anyerr and errs == [0] * 20
             assert [ctx.final_verify([p]) for p in parts] == expect
             assert ctx.final_verify(parts) == all(expect)
+            # all groups' final checks in one ticket (lsg_final_submit_groups), one and two
+            # partials per group
+            assert ctx.final_wait_groups(ctx.final_submit_groups([[p] for p in parts])) == expect
+            again = ctx.batch_wait(ctx.batch_submit(staged, group_size=8))[0]
+            pairs = [[parts[g], again[g]] for g in range(3)]  # F_g^2: the same verdicts
+            assert ctx.final_wait_groups(ctx.final_submit_groups(pairs)) == expect
             whole, _, _ = ctx.batch_wait(ctx.batch_submit(staged))  # one group: product of the three
             assert ctx.final_verify([whole]) == all(expect)
         finally:
@@ -390,3 +396,97 @@ def test_batch_partial_bit_exact_vs_oracle(ctx, monkeypatch):
     exp, exp_errs = ov.batch_partial([(p[0], m, s) for p, m, s in sets], rands)
     assert errs == exp_errs and anyerr
     assert part == _f12_bytes(exp)
+
+
+# ---- validator pubkey table resident in HBM, sets naming keys by index
+# (index2pubkey, state-transition/src/cache/pubkeyCache.ts:60-75, epochContext.ts:701-704)
+@pytest.fixture(scope="module")
+def table_ctx():
+    from lodestar_amd._native import Context
+    c = Context(0)
+    # indices 0..23 uncompressed, 24..39 compressed (two loads, the second one past the end)
+    assert c.pubkey_table_set(0, [bd.pk_bytes(i) for i in range(24)]) == [0] * 24
+    assert c.pubkey_table_set(24, [bd.pk_bytes(i, compressed=True) for i in range(24, 40)]) == [0] * 16
+    yield c
+    c.close()
+
+
+def test_pubkey_table_aggregation_by_index(table_ctx):
+    from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
+    c = table_ctx
+    assert c.pubkey_table_size() == 40
+    for idx in ([7], [0, 1, 2], list(range(40)), [39, 3, 3, 17, 24]):
+        out, err = c.aggregate_pubkeys(PkIndices(idx))
+        assert err == 0
+        assert out == g1_serialize(ov.aggregate_pubkeys([bd.pk_point(i) for i in idx])), idx
+    assert c.aggregate_pubkeys(PkIndices([1, 40]))[1] == LSG_ERR_BAD_INDEX
+    assert c.aggregate_pubkeys(PkIndices([]))[1] == 101  # EMPTY_AGGREGATE_ARRAY
+
+
+def test_pubkey_table_rejects_bad_keys_and_grows(table_ctx):
+    from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
+    c = table_ctx
+    bad = bytearray(bd.pk_bytes(1))
+    bad[50] ^= 1  # y no longer on the curve
+    errs = c.pubkey_table_set(5000, [bd.pk_bytes(41), bytes(bad), bd.pk_bytes(43)])
+    assert errs[0] == 0 and errs[1] == 2 and errs[2] == 0  # BLST_POINT_NOT_ON_CURVE
+    assert c.pubkey_table_size() == 5003
+    assert c.aggregate_pubkeys(PkIndices([5000, 5002]))[0] == g1_serialize(
+        ov.aggregate_pubkeys([bd.pk_point(41), bd.pk_point(43)]))
+    assert c.aggregate_pubkeys(PkIndices([5001]))[1] == LSG_ERR_BAD_INDEX  # undecodable key: index unset
+    assert c.aggregate_pubkeys(PkIndices([4999]))[1] == LSG_ERR_BAD_INDEX  # gap: never set
+    assert c.aggregate_pubkeys(PkIndices([0, 39]))[0] == g1_serialize(
+        ov.aggregate_pubkeys([bd.pk_point(0), bd.pk_point(39)]))  # rows kept across growth
+
+
+def test_index_sets_match_byte_sets(table_ctx):
+    """Verdicts of sets naming keys by index equal those of the same sets with encoded keys,
+    through maybeBatch (lsg_verify_sets) and the worker's batch + retry path (lsg_verify_jobs)."""
+    from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
+    c = table_ctx
+
+    def by_index(s, keys):
+        return (PkIndices(keys), s[1], s[2])
+
+    agg_keys = [list(range(3 * i, 3 * i + 4 + i)) for i in range(4)]
+    agg = [by_index(bd.aggregate_set(i, k), k) for i, k in enumerate(agg_keys)]
+    single = [by_index(bd.single_set(i), [i]) for i in range(4)]
+    assert c.verify_sets(agg + single, seed=11) == (1, 0)
+    wrong = by_index(bd.corrupt_wrong_message(bd.single_set(5)), [5])
+    assert c.verify_sets(agg + [wrong], seed=11) == (0, 0)
+    miss = (PkIndices(agg_keys[1][:-1]), agg[1][1], agg[1][2])  # one signer missing
+    assert c.verify_sets([miss], seed=11) == (0, 0)
+    jobs = [(agg[:2], 1), ([wrong], 1), (single, 1), (agg[2:], 0)]
+    got, stats = c.verify_jobs(jobs, seed=12)
+    assert [g[0] for g in got] == [1, 0, 1, 1]
+    # deserializeSet semantics (worker.ts:108-114): an unknown index rejects the package
+    got, _ = c.verify_jobs([(agg[:1], 1), ([(PkIndices([7, 4096]), agg[0][1], agg[0][2])], 1)], seed=13)
+    assert got == [(2, LSG_ERR_BAD_INDEX), (2, LSG_ERR_BAD_INDEX)]
+
+
+# ---- SURVEY.md 8f(2): batched KeyValidate (PublicKey.fromBytes(pk, affine, true),
+# processDeposit.ts:57-65) against oracle/verifier.py:public_key_validate
+def test_pubkey_validate_matches_oracle(ctx):
+    from oracle.curves import g1_compress
+    from oracle.fields import P
+    flip = bytearray(bd.pk_bytes(2, compressed=True))
+    flip[47] ^= 4
+    big_x = bytearray((P + 5).to_bytes(48, "big"))
+    big_x[0] |= 0x80
+    cases = {
+        48: [bd.pk_bytes(i, compressed=True) for i in range(3)] + [g1_compress(None), bytes(flip), bytes(big_x),
+                                                                   g1_compress(bd.g1_not_in_group(1))],
+        96: [bd.pk_bytes(i) for i in range(3, 6)] + [g1_serialize(None), g1_serialize(bd.g1_not_in_group(2)),
+                                                     bytes(96)],
+    }
+    for ln, pks in cases.items():
+        got = ctx.pubkey_validate(pks)
+        for pk, (out, err) in zip(pks, got):
+            try:
+                pt = ov.public_key_validate(pk)
+                exp = 0
+            except BlstError as e:
+                exp = e.code
+            assert err == exp, (ln, pk.hex(), err, exp)
+            if exp == 0:
+                assert out == g1_serialize(pt)

@@ -266,3 +266,14 @@ def test_split_miller_loop_equals_multi_loop(hc):
             if u:
                 exp = f12_mul(exp, f)
         assert ub12(o.raw) == exp, use
+
+
+def test_g1_subgroup_check(hc):
+    """lsg_curve.hpp:g1_in_group ([r]P == O, KeyValidate) against oracle/curves.py:in_g1 on
+    subgroup points, the identity and on-curve points outside the subgroup."""
+    from oracle.curves import in_g1
+    from tests.blsdata import g1_not_in_group
+    pts = [E1.mul(G1_GEN, k) for k in (1, 2, 12345)] + [g1_not_in_group(s) for s in range(3)]
+    for pt in pts:
+        assert hc.hc_g1_in_group(g1_serialize(pt)) == (1 if in_g1(pt) else 0)
+    assert hc.hc_g1_in_group(g1_serialize(None)) == 1
