@@ -22,8 +22,8 @@
 //   k_sig_proj        sig_i for the bucket MSM (k_sig_scale [r_i] sig_i for small groups) [M4]
 //   k_miller_multi    f_item = prod of ML(P_i, H(m_i)) over <= K sets            [M5]
 // then per group (an RLC batch = a chunk of batchable jobs, or one job):
-//   msm_buckets/msm_bits/k_msm_horner   S_g = sum r_i sig_i (8-bit windows)
-//   k_row_miller_neg_g1                 f_g = ML(-G1, S_g)        (row backend, lsg_serial.hip)
+//   msm_buckets/msm_bits   per-bit sums C_{g,k} of sum r_i sig_i (8-bit windows)
+//   k_row_horner_miller    S_g = sum_k 2^k C_{g,k}, f_g = ML(-G1, S_g)   (row backend, lsg_serial.hip)
 //   tree(Fp12 mul)    F_g = f_g prod f_item
 //   k_row_final_exp   FE(F_g) == 1                                               [M6]
 // Per-set values stay resident between the batch attempt and the per-job retry.
@@ -420,15 +420,6 @@ __global__ void LSG_KERNEL_ATTR k_sig_proj(int n, const uint32_t* __restrict__ s
   lane_store(out, item, r);
 }
 
-// S_g = sum_k 2^k C[64 g + k]: Horner over the 64 per-bit partial sums of one RLC group
-// (63 doublings and 63 additions, complete formulas)
-__global__ void LSG_KERNEL_ATTR k_msm_horner(int ng, const uint32_t* __restrict__ C, uint32_t* __restrict__ S) {
-  LANE_ITEM(ng);
-  g2p_t acc = lane_load<g2p_t>(C, 64 * item + 63);
-#pragma unroll 1
-  for (int k = 62; k >= 0; k--) acc = g2_add(g2_dbl(acc), lane_load<g2p_t>(C, 64 * item + k));
-  lane_store(S, item, acc);
-}
 
 // partials: canonical big-endian 576-byte Fp12 blobs -> lane form (one item each)
 __global__ void LSG_KERNEL_ATTR k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs,
@@ -664,7 +655,7 @@ TreePlan plan_tree(const std::vector<std::vector<int32_t>>& groups) {
 // known randomizers r_i):
 //   bucket (g, w, d), d = 1..255: the sets i of group g whose w-th byte of r_i is d
 //   bit (g, k = 8w + j): the buckets (g, w, d) whose digit d has bit j set
-// so that sum_i r_i sig_i = sum_k 2^k bit(g, k) (k_msm_horner).  Device copies of the index
+// so that sum_i r_i sig_i = sum_k 2^k bit(g, k) (Horner in k_row_horner_miller).  Device copies of the index
 // plans are kept with the package and shared by every ticket that submits it.
 struct MsmPlan {
   size_t group_size = 0, ng = 0;
@@ -1195,11 +1186,12 @@ int msm_plan(Slot* s, const lsg_staged* in, size_t group_size, size_t ng) {
   return LSG_OK;
 }
 
-// S_g = sum_{i in g} r_i sig_i for the planned groups, from the projective sig_i in d_rs
-// (k_sig_proj), on the current stream: bucket tree, bit tree, Horner.  About 8 point
-// additions per set (one per nonzero window digit) plus ~8.2k per group, against ~60
-// doublings and 16 additions per set for [r_i] sig_i.
-int msm_sum(Slot* s, const MsmPlan& M, uint32_t* out) {
+// Per-bit sums C_{g,k} (d_bits) of S_g = sum_{i in g} r_i sig_i for the planned groups, from
+// the projective sig_i in d_rs (k_sig_proj), on the current stream: bucket tree, bit tree
+// (the Horner pass runs on a row, k_row_horner_miller).  About 8 point additions per set (one
+// per nonzero window digit) plus ~8.2k per group, against ~60 doublings and 16 additions per
+// set for [r_i] sig_i.
+int msm_bit_sums(Slot* s, const MsmPlan& M) {
   const size_t ng = M.ng;
   int rc;
   if ((rc = ensure(s, s->d_bkt, 4 * W_G2P * ng * MSM_WINDOWS * MSM_DIGITS)) ||
@@ -1208,11 +1200,7 @@ int msm_sum(Slot* s, const MsmPlan& M, uint32_t* out) {
   if ((rc = run_tree<1>(s, 3, "msm_buckets", M.buckets, P_<int32_t>(M.d_buckets), P_<uint32_t>(s->d_rs),
                         P_<uint32_t>(s->d_bkt))))
     return rc;
-  if ((rc = run_tree<1>(s, 4, "msm_bits", M.bits, P_<int32_t>(M.d_bits), P_<uint32_t>(s->d_bkt),
-                        P_<uint32_t>(s->d_bits))))
-    return rc;
-  LAUNCH(s, k_msm_horner, ng, (int)ng, P_<uint32_t>(s->d_bits), out);
-  return LSG_OK;
+  return run_tree<1>(s, 4, "msm_bits", M.bits, P_<int32_t>(M.d_bits), P_<uint32_t>(s->d_bkt), P_<uint32_t>(s->d_bits));
 }
 
 constexpr int LSG_MILLER_KMAX = 4;  // pairs per multi-Miller item: 1, 2 or 4 (env LSG_MILLER_K)
@@ -1388,14 +1376,22 @@ int launch_groups(Slot* s, const std::vector<std::vector<int32_t>>& groups, bool
     return rc;
   s->cur = 1;
   if (s->msm) {  // planned by submit_batch for exactly these groups
-    if ((rc = msm_sum(s, s->in->msm, P_<uint32_t>(s->d_S)))) return rc;
-  } else if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) {
-    return rc;
+    // buckets and per-bit sums on the pair backend, then Horner + ML(-G1, S_g) in one row
+    // chain per group (k_row_horner_miller), written at d_fall slot n_items + g
+    if ((rc = msm_bit_sums(s, s->in->msm))) return rc;
+    if ((rc = ensure(s, s->d_Sb, (size_t)288 * MSM_BITS * ng))) return rc;
+    LAUNCH(s, k_g2p_to_canon, (size_t)MSM_BITS * ng, (int)(MSM_BITS * ng), P_<uint32_t>(s->d_bits),
+           P_<uint8_t>(s->d_Sb));
+    LAUNCH_ROW(s, "k_row_horner_miller",
+               lsg_row_horner_miller(S_(s), (int)ng, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
+  } else {
+    if ((rc = tree_reduce<1>(s, 2, "tree_g2_sigsum", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S))))
+      return rc;
+    // f_g = ML(-G1, S_g) on the row backend, written at d_fall slot n_items + g
+    LAUNCH(s, k_g2p_to_canon, ng, (int)ng, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_Sb));
+    LAUNCH_ROW(s, "k_row_miller_neg_g1",
+               lsg_row_miller_neg_g1(S_(s), (int)ng, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
   }
-  // f_g = ML(-G1, S_g) on the row backend, written at d_fall slot n_items + g
-  LAUNCH(s, k_g2p_to_canon, ng, (int)ng, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_Sb));
-  LAUNCH_ROW(s, "k_row_miller_neg_g1",
-             lsg_row_miller_neg_g1(S_(s), (int)ng, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
   LAUNCH(s, k_blobs_to_fp12, ng, (int)ng, P_<uint8_t>(s->d_fgb), P_<uint32_t>(s->d_fall) + W_F12 * n);
   LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
   s->cur = 0;

@@ -9,3 +9,6 @@
 hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict);
 // out576[g] = ML(-G1, S_g) for ng canonical 288-byte projective G2 points (1 if S_g = O)
 hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576);
+// out576[g] = ML(-G1, sum_k 2^k C_{g,k}) for ng groups of 64 canonical 288-byte projective G2
+// points each (the bucket MSM's per-bit sums): Horner and the Miller loop in one row chain
+hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576);

@@ -43,6 +43,28 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_miller_neg_g1(int ng, const
   fp12_to_canon_bytes(out576 + 576 * (size_t)item, r);
 }
 
+// The bucket MSM's last step fused with the signature Miller loop: S_g = sum_k 2^k C_{g,k}
+// by Horner over the group's 64 per-bit sums (63 doublings + 63 additions, complete
+// formulas), then ML(-G1, S_g).  Both are single dependency chains, so they run on rows.
+__global__ void __launch_bounds__(LSG_ROW_TPB) k_row_horner_miller(int ng, const uint8_t* __restrict__ C288,
+                                                                   uint8_t* __restrict__ out576) {
+  lsg_lane_setup();
+  const int item = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 16);
+  if (item >= ng) return;
+  const uint8_t* c = C288 + (size_t)288 * 64 * item;
+  g2p_t s = g2p_from_canon_bytes(c + 288 * 63);
+#pragma unroll 1
+  for (int k = 62; k >= 0; k--) s = g2_add(g2_dbl(s), g2p_from_canon_bytes(c + 288 * k));
+  fp12_t r = fp12_one();
+  if (!proj_is_inf(s)) {
+    g1a_t ng1;
+    ng1.x = fp_t(G1_GEN_X);
+    ng1.y = fp_t(G1_GEN_NEG_Y);
+    r = miller_loop(ng1, proj_to_aff(s));
+  }
+  fp12_to_canon_bytes(out576 + 576 * (size_t)item, r);
+}
+
 static int row_blocks(int n) { return (n * 16 + LSG_ROW_TPB - 1) / LSG_ROW_TPB; }
 
 hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
@@ -54,5 +76,11 @@ hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_
 hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
   if (ng <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_row_miller_neg_g1, dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, S288, out576);
+  return hipGetLastError();
+}
+
+hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
+  if (ng <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_row_horner_miller, dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, C288, out576);
   return hipGetLastError();
 }

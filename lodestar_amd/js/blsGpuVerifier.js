@@ -108,6 +108,12 @@ function pubkeyBytes(pk) {
 /** ISignatureSet -> the addon's set (utils.ts:5-17 getAggregatedPubkey, with the sum done on
  * the GPU instead of the main thread). */
 function serializeSet(set) {
+  // signers named by validator index into the device pubkey table (SURVEY 8f(1)):
+  // loadPubkeys() mirrors index2pubkey; the set carries its attesting indices
+  if (set.pubkeyIndices !== undefined) {
+    const ix = set.pubkeyIndices instanceof Uint32Array ? set.pubkeyIndices : Uint32Array.from(set.pubkeyIndices);
+    return {pubkeyIndices: ix, message: set.signingRoot, signature: set.signature};
+  }
   let pubkeys;
   switch (set.type) {
     case SignatureSetType.single:
@@ -125,7 +131,10 @@ function serializeSet(set) {
 /** utils.ts:19-26 */
 function getAggregatedPubkeysCount(sets) {
   let n = 0;
-  for (const set of sets) if (set.type === SignatureSetType.aggregate) n += set.pubkeys.length;
+  for (const set of sets) {
+    if (set.pubkeyIndices !== undefined) n += set.pubkeyIndices.length;
+    else if (set.type === SignatureSetType.aggregate) n += set.pubkeys.length;
+  }
   return n;
 }
 
@@ -155,6 +164,13 @@ class BlsGpuVerifier {
     this.inflight = new Set();
     this._runJob = this._runJob.bind(this);
     this._runBufferedJobs = this._runBufferedJobs.bind(this);
+  }
+
+  /** Mirror index2pubkey[firstIndex ..] into the device pubkey table (SURVEY 8f(1); call next
+   * to pubkeyCache.ts syncPubkeys / epochContext.ts addPubkey).  Sets may then carry
+   * `pubkeyIndices` instead of PublicKeys.  Returns per-key BLST codes (0 = loaded). */
+  loadPubkeys(firstIndex, pubkeys) {
+    return this.addon.pubkeyTableSet(this.ctx, firstIndex, pubkeys.map(pubkeyBytes));
   }
 
   canAcceptWork() {

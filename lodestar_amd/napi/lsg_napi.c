@@ -22,6 +22,8 @@
  *                                     batchSigsSuccess, startNs, endNs}>   lsg_wait_jobs
  *   verifySets(ctx, sets, seed) -> {status, errCode}                   lsg_verify_sets
  *   aggregatePubkeys(ctx, pubkeys[]) -> {errCode, bytes: Uint8Array(96)} lsg_aggregate_pubkeys
+ *   pubkeyTableSet(ctx, firstIndex, pubkeys[]) -> errCodes[]          lsg_pubkey_table_set
+ *       (a set may then carry pubkeyIndices: Uint32Array instead of pubkeys)
  *   hashToG2(ctx, message, dst) -> Uint8Array(192)                     lsg_hash_to_g2
  * Failures of the library itself (not verdicts) throw an Error carrying lsg_last_error().
  */
@@ -69,6 +71,19 @@ static int get_bytes(napi_env env, napi_value v, const uint8_t** data, size_t* l
   if (napi_get_typedarray_info(env, v, &t, &n, &d, &ab, &off) != napi_ok || t != napi_uint8_array) return -1;
   *data = (const uint8_t*)d;
   *len = n;
+  return 0;
+}
+
+/* Uint32Array -> pointer + element count; returns 0 on success */
+static int get_u32s(napi_env env, napi_value v, const uint32_t** data, size_t* n) {
+  bool is_ta = false;
+  if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return -1;
+  napi_typedarray_type t;
+  void* d;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, n, &d, &ab, &off) != napi_ok || t != napi_uint32_array) return -1;
+  *data = (const uint32_t*)d;
   return 0;
 }
 
@@ -126,6 +141,19 @@ static int view_sets(napi_env env, napi_value arr, set_view* out) {
     if (!g || get_bytes(env, g, &d, &len)) goto bad;
     q->sig = d;
     q->sig_len = (uint32_t)len;
+    /* signers by validator index into the device pubkey table (lsg_pubkey_table_set) */
+    napi_value pki = get_prop(env, s, "pubkeyIndices");
+    napi_valuetype pkit = napi_undefined;
+    if (pki) napi_typeof(env, pki, &pkit);
+    if (pki && pkit != napi_undefined) {
+      const uint32_t* ix;
+      size_t nix;
+      if (get_u32s(env, pki, &ix, &nix)) goto bad;
+      q->pks = (const uint8_t*)ix;
+      q->pk_len = LSG_PK_INDEX;
+      q->n_pks = (uint32_t)nix;
+      continue;
+    }
     uint32_t npk = pk ? array_len(env, pk) : UINT32_MAX;
     if (npk == UINT32_MAX) goto bad;
     q->n_pks = npk;
@@ -161,7 +189,9 @@ static int view_sets(napi_env env, napi_value arr, set_view* out) {
   return 0;
 bad:
   view_free(out);
-  napi_throw_type_error(env, NULL, "lsg_napi: a set is {pubkeys: Uint8Array[], message: Uint8Array, signature: Uint8Array}");
+  napi_throw_type_error(env, NULL,
+                        "lsg_napi: a set is {pubkeys: Uint8Array[] | pubkeyIndices: Uint32Array, message: Uint8Array, "
+                        "signature: Uint8Array}");
   return -1;
 }
 
@@ -423,6 +453,51 @@ static napi_value js_aggregate_pubkeys(napi_env env, napi_callback_info info) {
   return o;
 }
 
+/* pubkeyTableSet(ctx, firstIndex, pubkeys: Uint8Array[]) -> errCodes: number[]  (8f(1)) */
+static napi_value js_pubkey_table_set(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int64_t first = 0;
+  uint32_t n = array_len(env, argv[2]);
+  if (napi_get_value_int64(env, argv[1], &first) != napi_ok || first < 0 || n == UINT32_MAX) {
+    napi_throw_type_error(env, NULL, "lsg_napi: pubkeyTableSet(ctx, firstIndex, pubkeys: Uint8Array[])");
+    return NULL;
+  }
+  size_t len = 96;
+  uint8_t* buf = NULL;
+  for (uint32_t k = 0; k < n; k++) {
+    napi_value kk;
+    const uint8_t* d;
+    size_t l;
+    napi_get_element(env, argv[2], k, &kk);
+    if (get_bytes(env, kk, &d, &l) || (k > 0 && l != len)) {
+      free(buf);
+      napi_throw_type_error(env, NULL, "lsg_napi: pubkeys must be Uint8Arrays of one encoding");
+      return NULL;
+    }
+    if (k == 0) {
+      len = l;
+      buf = (uint8_t*)malloc((size_t)n * len);
+    }
+    memcpy(buf + (size_t)k * len, d, len);
+  }
+  int32_t* err = (int32_t*)calloc(n ? n : 1, sizeof(int32_t));
+  int rc = n ? lsg_pubkey_table_set(ctx, (size_t)first, buf, (uint32_t)len, n, err) : LSG_OK;
+  free(buf);
+  if (rc) {
+    free(err);
+    return throw_lsg(env, ctx, "lsg_pubkey_table_set", rc);
+  }
+  napi_value out;
+  NAPI_CALL(env, napi_create_array_with_length(env, n, &out));
+  for (uint32_t k = 0; k < n; k++) napi_set_element(env, out, k, make_int(env, err[k]));
+  free(err);
+  return out;
+}
+
 static napi_value js_hash_to_g2(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
@@ -456,6 +531,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"verifySets", NULL, js_verify_sets, NULL, NULL, NULL, napi_enumerable, NULL},
       {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, napi_enumerable, NULL},
       {"hashToG2", NULL, js_hash_to_g2, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pubkeyTableSet", NULL, js_pubkey_table_set, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   NAPI_CALL(env, napi_define_properties(env, exports, sizeof props / sizeof props[0], props));
   return exports;

@@ -52,6 +52,14 @@ const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
   assert.strictEqual(Buffer.from(agg.bytes).toString("hex"), cases.aggregate_pk);
   const h = pool.addon.hashToG2(pool.ctx, hex(cases.h2c.msg), Buffer.from(cases.h2c.dst, "latin1"));
   assert.strictEqual(Buffer.from(h).toString("hex"), cases.h2c.out);
+  // signers by index into the device pubkey table (SURVEY 8f(1))
+  const aggPks = cases.aggregate.pks.map(hex);
+  assert.deepStrictEqual(pool.loadPubkeys(100, aggPks), Array(aggPks.length).fill(0));
+  const ix = Uint32Array.from(aggPks.map((_, k) => 100 + k));
+  const byIndex = {type: V.SignatureSetType.aggregate, pubkeyIndices: ix, signingRoot: hex(cases.aggregate.msg),
+                   signature: hex(cases.aggregate.sig)};
+  assert.strictEqual(await pool.verifySignatureSets([byIndex, sets[0]], {batchable: true}), true);
+  assert.strictEqual(await pool.verifySignatureSets([Object.assign({}, byIndex, {pubkeyIndices: ix.slice(1)})]), false);
   await pool.close();
   console.log("node host on GPU: all checks passed");
 })().catch((e) => {
