@@ -154,6 +154,10 @@ class BlsGpuVerifier {
     this.metrics = modules.metrics || null;
     this.blsVerifyAllMultiThread = options.blsVerifyAllMultiThread === true;
     this.seed = options.seed || 0; // 0: randomizers from the OS CSPRNG (production)
+    // sigs of queued jobs drained into one GPU package (prepareWork, index.ts:400-418).  The
+    // reference's 128 suits a CPU worker; one GPU launch wants thousands of sets, so a
+    // production node sets e.g. 4096.  Per-job verdicts do not depend on it.
+    this.maxSigsPerPackage = options.maxSigsPerPackage || MAX_SIGNATURE_SETS_PER_JOB;
     this.addon = modules.addon || loadAddon();
     this.ctx = this.addon.open(options.device || 0); // throws loudly without a gfx950 device
     this.poolSize = this.addon.slots(this.ctx);
@@ -333,7 +337,7 @@ class BlsGpuVerifier {
   _prepareWork() {
     const jobs = [];
     let totalSigs = 0;
-    while (totalSigs < MAX_SIGNATURE_SETS_PER_JOB) {
+    while (totalSigs < this.maxSigsPerPackage) {
       const job = this.jobs.shift();
       if (!job) break;
       jobs.push(job);

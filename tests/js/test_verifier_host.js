@@ -187,6 +187,18 @@ test("a package holds at most 128 sigs of queued jobs (prepareWork, index.ts:400
   await pool.close();
 });
 
+test("maxSigsPerPackage widens the package (GPU sizing) without changing verdicts", async () => {
+  const a = mockAddon(1);
+  const pool = new V.BlsGpuVerifier({maxSigsPerPackage: 4096}, {addon: a});
+  const sets100 = Array.from({length: 100}, (_, i) => set(i));
+  const bad = Array.from({length: 100}, (_, i) => (i === 7 ? Object.assign({}, set(i), {signingRoot: new Uint8Array(32).fill(9)}) : set(i)));
+  const ps = [pool.verifySignatureSets(sets100), pool.verifySignatureSets(bad), pool.verifySignatureSets(sets100)];
+  assert.deepStrictEqual(await Promise.all(ps), [true, false, true]);
+  // all three jobs (300 sigs) in one package, where the reference's 128 cap makes two
+  assert.deepStrictEqual(a.packages.map((p) => p.length), [3]);
+  await pool.close();
+});
+
 test("empty set list: job error 'Empty signature set' (maybeBatch.ts:29-31)", async () => {
   const a = mockAddon();
   const pool = new V.BlsGpuVerifier({}, {addon: a});
