@@ -121,6 +121,22 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
                       f"(oracle/c, C restatement of the oracle, gcc -O3) in {dt:.1f}s"}
 
 
+def pmc_traffic(kernel, sets_per_launch):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (tools/gpu_traffic.sh ->
+    tools/pmc_traffic.py -> profiles/rNN_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE), when
+    they were measured at this launch size; None otherwise (PMC counters cannot be read from
+    inside the timed run)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = d["kernels"].get(kernel)
+    if k is None or d["sets_per_launch"] != sets_per_launch:
+        return None
+    return k["hbm_bytes_per_dispatch"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,7 +266,8 @@ def main():
     achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] * 1e-3) / 1e12
     peak = peak_mad / 1e12
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
-            "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4), "traffic": None,
+            "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
+            "traffic": pmc_traffic(dom, n * M),
             "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
     total_sets = n * world * steps
     value = total_sets / elapsed

@@ -14,6 +14,7 @@
  *   lsg_aggregate_pubkeys  <- utils.ts:11 PublicKey.aggregate (+ toBytes, index.ts:177)
  *   lsg_hash_to_g2         <- blst Hash_to_G2 inside Pairing.mul_n_aggregate
  *   lsg_sig_decode         <- maybeBatch.ts:23,36 Signature.fromBytes(bytes, affine, true)
+ *   lsg_aggregate_signatures <- opPools Signature.aggregate
  *   lsg_submit_jobs /      <- the asynchronous lsg_submit / lsg_wait pair of SURVEY.md 8b:
  *   lsg_wait_jobs             one BlsWorkReq[] package in flight per pipeline slot
  *   lsg_batch_* /          <- the per-GPU half of verifyMultipleSignatures for the
@@ -210,6 +211,19 @@ int lsg_pubkey_table_size(lsg_ctx* ctx, size_t* n);
  * infinity (BLST_PK_IS_INFINITY), in the r-torsion subgroup (BLST_POINT_NOT_IN_GROUP).
  * err[i] = BLST_* (0 = valid); out96 (may be NULL) = the uncompressed affine key. */
 int lsg_pubkey_validate(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96, int32_t* err);
+
+/* G2 signature aggregation for the op pools:
+ *   bls.Signature.aggregate(sigs.map(signatureFromBytesNoCheck)).toBytes()
+ * of opPools/attestationPool.ts:195, syncCommitteeMessagePool.ts:139,
+ * aggregatedAttestationPool.ts:322 and syncContributionAndProofPool.ts:185, with the decode of
+ * opPools/utils.ts:32-34 (Signature.fromBytes(sig, affine, validate=false): size, encoding and
+ * on-curve checks, no subgroup check).  n_groups independent aggregations in one call: group g
+ * is signatures offsets[g] .. offsets[g+1]-1 (offsets has n_groups+1 entries, offsets[0] = 0),
+ * each sig_len (96 or 192) bytes.  out96[g] = the compressed sum (zeros unless err[g] == 0);
+ * err[g] = BLST_* of the group's first signature that does not decode, or
+ * LSG_ERR_EMPTY_AGGREGATE for an empty group ("EMPTY_AGGREGATE_ARRAY"). */
+int lsg_aggregate_signatures(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, const uint32_t* offsets,
+                             size_t n_groups, uint8_t* out96, int32_t* err);
 
 /* Test/bench input generation (not on the verify path): sig_i = sk_i * H(m_i) compressed,
  * pk_i = sk_i * G1 uncompressed; sks are 32-byte big-endian secret keys. */

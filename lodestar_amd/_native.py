@@ -94,7 +94,7 @@ EXPORTS = [
     "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
     "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups", "lsg_probe_mad_peak",
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
-    "lsg_final_submit_groups", "lsg_final_wait_groups",
+    "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
 ]
 
 
@@ -140,6 +140,8 @@ def load_library(path=LIB_PATH):
         lib.lsg_final_submit_groups.argtypes = [vp, ctypes.c_char_p, sz, sz, pu64]
         lib.lsg_final_wait_groups.argtypes = [vp, u64, pi32]
         lib.lsg_pubkey_validate.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
+        lib.lsg_aggregate_signatures.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(u32), sz,
+                                                 ctypes.c_char_p, pi32]
         lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
@@ -313,6 +315,24 @@ class Context:
         err = (ctypes.c_int32 * n)()
         self._check(self.lib.lsg_pubkey_validate(self.h, b"".join(pks), pk_len, n, out, err), "lsg_pubkey_validate")
         return [(out.raw[96 * k:96 * k + 96], err[k]) for k in range(n)]
+
+    def aggregate_signatures(self, groups):
+        """Op-pool Signature.aggregate over each list of signatures in `groups` (one device
+        pass for all): [(compressed 96 B, BLST code or LSG_ERR_EMPTY_AGGREGATE)] per group."""
+        ng = len(groups)
+        if ng == 0:
+            return []
+        flat = [sg for g in groups for sg in g]
+        sl = len(flat[0]) if flat else 96
+        assert all(len(sg) == sl for sg in flat)
+        offs = (ctypes.c_uint32 * (ng + 1))()
+        for g in range(ng):
+            offs[g + 1] = offs[g] + len(groups[g])
+        out = ctypes.create_string_buffer(96 * ng)
+        err = (ctypes.c_int32 * ng)()
+        self._check(self.lib.lsg_aggregate_signatures(self.h, b"".join(flat), sl, offs, ng, out, err),
+                    "lsg_aggregate_signatures")
+        return [(out.raw[96 * g:96 * g + 96], err[g]) for g in range(ng)]
 
     def hash_to_g2(self, msgs, dst=b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"):
         if not msgs:

@@ -496,6 +496,23 @@ __global__ void LSG_KERNEL_ATTR k_sign(int n, const uint8_t* __restrict__ sks, c
   g2_compress(out96 + 96 * item, a, inf);
 }
 
+// op-pool aggregates (lsg_aggregate_signatures): projective G2 sums -> ZCash-compressed
+// 96 bytes, Signature.toBytes() of the aggregate (the identity -> 0xc0 || 0^95)
+__global__ void LSG_KERNEL_ATTR k_g2p_compress(int n, const uint32_t* __restrict__ pts,
+                                               uint8_t* __restrict__ out96) {
+  LANE_ITEM(n);
+  g2p_t p = lane_load<g2p_t>(pts, item);
+  bool inf = proj_is_inf(p);
+  g2a_t a;
+  if (inf) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    a = proj_to_aff(p);
+  }
+  g2_compress(out96 + 96 * item, a, inf);
+}
+
 // pk_i = [sk_i] G1, uncompressed 96 bytes (bench/test input generation)
 __global__ void LSG_KERNEL_ATTR k_sk_to_pk(int n, const uint8_t* __restrict__ sks,
                                                        uint8_t* __restrict__ out96) {
@@ -2218,6 +2235,68 @@ int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, 
   LSG_HIP(s, hipMemcpyAsync(err, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   c->last = s;
+  return LSG_OK;
+}
+
+// G2 signature aggregation for the op pools: n_groups independent
+// Signature.aggregate calls in one pass -- decode without the subgroup check
+// (signatureFromBytesNoCheck, opPools/utils.ts:32-34), projective sums as a segmented tree,
+// one compression per group
+int lsg_aggregate_signatures(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, const uint32_t* offsets,
+                             size_t n_groups, uint8_t* out96, int32_t* err) {
+  if (!c || !offsets || (n_groups && (!out96 || !err)) || offsets[0] != 0 || n_groups > 0x7fffffffull)
+    return LSG_ERR_INVALID_ARG;
+  for (size_t g = 0; g < n_groups; g++)
+    if (offsets[g + 1] < offsets[g]) return LSG_ERR_INVALID_ARG;
+  const size_t n = offsets[n_groups];
+  if (n && !sigs) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  std::vector<std::vector<int32_t>> groups;
+  std::vector<size_t> gid;  // groups[k] is caller group gid[k]
+  for (size_t g = 0; g < n_groups; g++) {
+    err[g] = offsets[g + 1] == offsets[g] ? LSG_ERR_EMPTY_AGGREGATE : 0;
+    memset(out96 + 96 * g, 0, 96);
+    if (offsets[g + 1] == offsets[g]) continue;
+    std::vector<int32_t> m;
+    for (uint32_t i = offsets[g]; i < offsets[g + 1]; i++) m.push_back((int32_t)i);
+    groups.push_back(std::move(m));
+    gid.push_back(g);
+  }
+  if (n == 0) return LSG_OK;
+  std::vector<lsg_set> sets(n);
+  std::vector<const lsg_set*> sp(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&sets[i], 0, sizeof(lsg_set));
+    sets[i].sig = sigs + (size_t)sig_len * i;
+    sets[i].sig_len = sig_len;
+    sp[i] = &sets[i];
+  }
+  s->in = &s->own;
+  int rc;
+  const size_t ng = groups.size();
+  if ((rc = stage_sets(s, &s->own, sp.data(), n, 0, false, s->st[0]))) return rc;
+  if ((rc = size_state(s, ng)) || (rc = ensure(s, s->d_blob, 96 * ng))) return rc;
+  int nn = (int)n;
+  LAUNCH(s, k_sig_decode, nn, nn, P_<uint8_t>(s->own.d_sig), P_<uint32_t>(s->own.d_siglen), P_<uint32_t>(s->d_sigaff),
+         P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr));
+  LAUNCH(s, k_sig_proj, nn, nn, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr),
+         P_<uint32_t>(s->d_rs));
+  if ((rc = tree_reduce<1>(s, 1, "tree_g2_aggregate", P_<uint32_t>(s->d_rs), groups, P_<uint32_t>(s->d_S)))) return rc;
+  LAUNCH(s, k_g2p_compress, ng, (int)ng, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_blob));
+  std::vector<int32_t> serr(n);
+  std::vector<uint8_t> blob(96 * ng);
+  LSG_HIP(s, hipMemcpyAsync(serr.data(), s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(blob.data(), s->d_blob.p, 96 * ng, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
+  // Signature.aggregate throws on the first signature that fails to deserialize
+  for (size_t k = 0; k < ng; k++) {
+    const size_t g = gid[k];
+    for (uint32_t i = offsets[g]; i < offsets[g + 1] && !err[g]; i++) err[g] = serr[i];
+    if (!err[g]) memcpy(out96 + 96 * g, blob.data() + 96 * k, 96);
+  }
   return LSG_OK;
 }
 

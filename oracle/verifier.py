@@ -20,7 +20,7 @@ import os
 from .fields import F12_ONE, f12_mul, f12_conj, f12_is_one
 from .curves import (
     E1, E2, G1_GEN, BlstError, BLST_INVALID_SIZE, BLST_PK_IS_INFINITY, BLST_POINT_NOT_IN_GROUP,
-    g1_deserialize, g2_deserialize, in_g1, in_g2, g1_serialize, g1_compress,
+    g1_deserialize, g2_deserialize, in_g1, in_g2, g1_serialize, g1_compress, g2_compress,
 )
 from .hash_to_curve import hash_to_g2
 from .pairing import miller_loop_fast, final_exp_fast
@@ -65,6 +65,20 @@ def aggregate_pubkeys(points):
     for pt in points:
         acc = E1.add(acc, pt)
     return acc
+
+
+def aggregate_signatures(sigs):
+    """Op-pool aggregation: bls.Signature.aggregate(sigs.map(
+    signatureFromBytesNoCheck)).toBytes() -- opPools/utils.ts:32-34 decodes with validate=false
+    (size/encoding/on-curve only), aggregatedAttestationPool.ts:322 and
+    syncContributionAndProofPool.ts:185 sum and compress.  Empty -> EMPTY_AGGREGATE_ARRAY;
+    the first undecodable signature raises its BlstError."""
+    if len(sigs) == 0:
+        raise ValueError("EMPTY_AGGREGATE_ARRAY")
+    acc = None
+    for b in sigs:
+        acc = E2.add(acc, signature_from_bytes(b, validate=False))
+    return g2_compress(acc)
 
 
 def default_rand():

@@ -6,6 +6,7 @@ packages/beacon-node/test/e2e/interop/genesisState.test.ts:49-56).
   sig_decode.json         96/192/other-byte signatures -> point or blst error code
   aggregate_pubkeys.json  pubkey lists -> uncompressed aggregate or error
   verdict_jobs.json       work packages -> per-job verdicts (worker.ts semantics)
+  aggregate_signatures.json  op-pool signature lists -> compressed aggregate or error (8f(4))
 
 Run: python tests/golden/gen_golden.py
 """
@@ -20,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle.curves import (  # noqa: E402
-    E1, g1_serialize, g1_compress, g2_serialize, g2_compress, g2_uncompress, g2_deserialize, in_g2, BlstError,
+    E1, E2, g1_serialize, g1_compress, g2_serialize, g2_compress, g2_uncompress, g2_deserialize, in_g2, BlstError,
     BLST_INVALID_SIZE, BLST_POINT_NOT_IN_GROUP,
 )
 from oracle.fields import P  # noqa: E402
@@ -91,6 +92,45 @@ def main():
     bad[95] ^= 1
     agg.append({"pks": [g1_serialize(pk).hex(), bytes(bad).hex()], "err": 2})
     json.dump({"cases": agg}, open(os.path.join(HERE, "aggregate_pubkeys.json"), "w"), indent=1)
+
+    # op-pool signature aggregation (Signature.aggregate of signatureFromBytesNoCheck)
+    json.dump({"cases": aggregate_signature_cases(rng, mainnet)},
+              open(os.path.join(HERE, "aggregate_signatures.json"), "w"), indent=1)
+
+
+def sig_agg_case(sigs):
+    try:
+        return {"sigs": [b.hex() for b in sigs], "err": 0, "out": ov.aggregate_signatures(sigs).hex()}
+    except BlstError as e:
+        return {"sigs": [b.hex() for b in sigs], "err": e.code}
+
+
+def aggregate_signature_cases(rng, mainnet):
+    cases = []
+    sigs = [bd.single_set(i)[2] for i in range(128)]
+    for n in (1, 2, 3, 16, 128):                                  # committee-shaped aggregates
+        cases.append(sig_agg_case(sigs[:n]))
+    real = []
+    for hx in mainnet:                                            # the reference's mainnet G2 points
+        b = bytes.fromhex(hx)
+        try:
+            ov.signature_from_bytes(b, False)
+            real.append(b)
+        except BlstError:
+            pass
+    cases.append(sig_agg_case(real))
+    inf = bytes([0xC0]) + bytes(95)
+    cases.append(sig_agg_case([sigs[0], inf, sigs[1]]))          # infinity contributes nothing
+    cases.append(sig_agg_case([inf]))
+    pt = g2_uncompress(sigs[5])
+    cases.append(sig_agg_case([sigs[5], g2_compress(E2.neg(pt))]))  # P + (-P) = identity
+    cases.append(sig_agg_case([sigs[2], sigs[2]]))                # doubling inside the tree
+    cases.append(sig_agg_case([sigs[3], bd.corrupt_not_in_group(bd.single_set(3), seed=3)[2]]))  # no subgroup check
+    cases.append(sig_agg_case([sigs[4], bd.corrupt_flip_x_bit(bd.single_set(4), bit=4)[2], sigs[6]]))
+    cases.append(sig_agg_case([sigs[7], bytes([0xE0]) + bytes(95)]))  # bad encoding
+    cases.append(sig_agg_case([g2_serialize(g2_uncompress(s)) for s in sigs[:5]]))  # 192-byte inputs
+    rng.shuffle(cases)
+    return cases
 
 
 if __name__ == "__main__":

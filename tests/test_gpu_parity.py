@@ -490,3 +490,51 @@ def test_pubkey_validate_matches_oracle(ctx):
             assert err == exp, (ln, pk.hex(), err, exp)
             if exp == 0:
                 assert out == g1_serialize(pt)
+
+
+def test_aggregate_signatures_matches_golden(ctx):
+    """Op-pool Signature.aggregate: every golden case of one encoding in one
+    batched call, plus an empty group, against the oracle's fixture."""
+    from lodestar_amd._native import LSG_ERR_EMPTY_AGGREGATE
+    gold = json.load(open(os.path.join(GOLDEN, "aggregate_signatures.json")))
+    by_len = {}
+    for c in gold["cases"]:
+        by_len.setdefault(len(c["sigs"][0]) // 2, []).append(c)
+    for ln, cases in by_len.items():
+        groups = [[bytes.fromhex(x) for x in c["sigs"]] for c in cases] + [[]]
+        out = ctx.aggregate_signatures(groups)
+        for c, (o, err) in zip(cases, out):
+            assert err == c["err"], c
+            if err == 0:
+                assert o.hex() == c["out"]
+        assert out[-1][1] == LSG_ERR_EMPTY_AGGREGATE
+    (o, err), = ctx.aggregate_signatures([[bytes(32)]])
+    assert err == 10  # BLST_INVALID_SIZE
+
+
+def test_aggregate_signatures_linearity_at_scale(ctx):
+    """4096 signatures (sync-committee / attestation-committee sizes mixed) in 40 groups over
+    one message per group: each aggregate must equal the signature of the group's summed key
+    (size-independent property; the signatures and the expected values come from lsg_sign)."""
+    from oracle.fields import R
+    import random
+    rng = random.Random(5)
+    sizes = [512] * 4 + [128] * 10 + [64] * 8 + [1, 2, 3, 7] * 4
+    sizes.append(4096 - sum(sizes))
+    assert sizes[-1] > 0
+    sks = [rng.randrange(1, R) for _ in range(4096)]
+    msgs, sums, pos = [], [], 0
+    for g, n in enumerate(sizes):
+        m = bd.msg("oppool-scale", g)
+        msgs += [m] * n
+        sums.append(sum(sks[pos:pos + n]) % R)
+        pos += n
+    sigs = ctx.sign(sks, msgs)
+    groups, pos = [], 0
+    for n in sizes:
+        groups.append(sigs[pos:pos + n])
+        pos += n
+    out = ctx.aggregate_signatures(groups)
+    expect = ctx.sign(sums, [bd.msg("oppool-scale", g) for g in range(len(sizes))])
+    for g, ((o, err), e) in enumerate(zip(out, expect)):
+        assert err == 0 and o == e, g

@@ -99,3 +99,28 @@ def test_mainnet_block_signatures_are_g2_points():
         Pt = g2_uncompress(bytes.fromhex(hx))
         assert in_g2_psi(Pt)
         assert g2_compress(Pt).hex() == hx
+
+
+def test_aggregate_signatures_oracle_and_golden():
+    """Op-pool aggregation: the golden fixture is the oracle's output, and
+    the oracle is pinned by a property independent of it: the aggregate of sk_i-signatures
+    over one message is the signature of sum(sk_i) (BLS linearity), as the sync-committee
+    contribution pool relies on (syncContributionAndProofPool.ts:169-186)."""
+    from oracle.curves import g2_compress
+    from oracle.verifier import aggregate_signatures
+    from tests import blsdata as bd
+    m = bd.msg("oppool", 0)
+    keys = [interop_secret_key(i) for i in range(5)]
+    sigs = [g2_compress(sign(k, m)) for k in keys]
+    assert aggregate_signatures(sigs) == g2_compress(sign(sum(keys) % R, m))
+    with pytest.raises(ValueError, match="EMPTY_AGGREGATE_ARRAY"):
+        aggregate_signatures([])
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aggregate_signatures.json")))
+    for c in gold["cases"]:
+        sg = [bytes.fromhex(x) for x in c["sigs"]]
+        if c["err"]:
+            with pytest.raises(BlstError) as e:
+                aggregate_signatures(sg)
+            assert e.value.code == c["err"]
+        else:
+            assert aggregate_signatures(sg).hex() == c["out"]
