@@ -39,7 +39,12 @@ def build(force=False, verbose=True):
         subprocess.check_call([sys.executable, gen, const])
     if not force and not needs_rebuild():
         return OUT
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", CSRC,
+    # Tower functions (Fp2/Fp6/Fp12, LSG_BIGFN) inlined into the device kernels: as calls they
+    # passed Fp12 operands through stack frames (k_miller_accum<2>: 3408 B/lane of scratch,
+    # ~477 KB of memory-side traffic per set); inlined, the accumulation has no scratch at all
+    # (profiles/r01_pmc_traffic*.json, profiles/r01_inline_ab.txt).  Host builds keep the calls.
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-DLSG_BIGFN=__host__ __device__ __forceinline__", "-I", CSRC,
            "-I", os.path.join(ROOT, "include")] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
     if verbose:
         print("[lodestar_amd.build]", " ".join(cmd), flush=True)

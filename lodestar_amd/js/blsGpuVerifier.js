@@ -177,6 +177,15 @@ class BlsGpuVerifier {
     return this.addon.pubkeyTableSet(this.ctx, firstIndex, pubkeys.map(pubkeyBytes));
   }
 
+  /** Op-pool aggregation (SURVEY 8f(4)): bls.Signature.aggregate(sigs.map(signatureFromBytesNoCheck))
+   * .toBytes() of opPools/attestationPool.ts:195, syncCommitteeMessagePool.ts:139,
+   * aggregatedAttestationPool.ts:322 and syncContributionAndProofPool.ts:185, for many groups in
+   * one device pass.  Returns [{signature: Uint8Array(96) | null, err}] per group; err is the
+   * BLST code of the group's first undecodable signature (101 = EMPTY_AGGREGATE_ARRAY). */
+  aggregateSignatures(groups) {
+    return this.addon.aggregateSignatures(this.ctx, groups);
+  }
+
   canAcceptWork() {
     return this.workersBusy < this.poolSize && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
   }

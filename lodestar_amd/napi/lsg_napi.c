@@ -519,6 +519,87 @@ static napi_value js_hash_to_g2(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* aggregateSignatures(ctx, groups: Uint8Array[][]) -> [{signature: Uint8Array(96) | null, err}]
+ * -- the op pools' bls.Signature.aggregate(sigs.map(signatureFromBytesNoCheck)).toBytes()
+ * for every group in one device pass (8f(4), lsg_aggregate_signatures). */
+static napi_value js_aggregate_signatures(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t ng = array_len(env, argv[1]);
+  if (ng == UINT32_MAX) {
+    napi_throw_type_error(env, NULL, "lsg_napi: aggregateSignatures(ctx, groups: Uint8Array[][])");
+    return NULL;
+  }
+  uint32_t* offs = (uint32_t*)calloc((size_t)ng + 1, sizeof(uint32_t));
+  size_t total = 0, len = 0;
+  for (uint32_t g = 0; g < ng; g++) {
+    napi_value grp;
+    napi_get_element(env, argv[1], g, &grp);
+    uint32_t n = array_len(env, grp);
+    if (n == UINT32_MAX) {
+      free(offs);
+      napi_throw_type_error(env, NULL, "lsg_napi: each group must be an array of signatures");
+      return NULL;
+    }
+    total += n;
+    offs[g + 1] = (uint32_t)total;
+  }
+  uint8_t* buf = (uint8_t*)malloc(total ? total * 192 : 1);
+  size_t k = 0;
+  for (uint32_t g = 0; g < ng; g++) {
+    napi_value grp;
+    napi_get_element(env, argv[1], g, &grp);
+    for (uint32_t i = 0; i < offs[g + 1] - offs[g]; i++, k++) {
+      napi_value sv;
+      const uint8_t* d;
+      size_t l;
+      napi_get_element(env, grp, i, &sv);
+      if (get_bytes(env, sv, &d, &l) || (k > 0 && l != len) || l > 192) {
+        free(buf);
+        free(offs);
+        napi_throw_type_error(env, NULL, "lsg_napi: signatures must be Uint8Arrays of one encoding");
+        return NULL;
+      }
+      len = l;
+      memcpy(buf + k * len, d, len);
+    }
+  }
+  uint8_t* out = (uint8_t*)calloc(ng ? (size_t)ng * 96 : 1, 1);
+  int32_t* err = (int32_t*)calloc(ng ? ng : 1, sizeof(int32_t));
+  int rc = ng ? lsg_aggregate_signatures(ctx, buf, (uint32_t)(total ? len : 96), offs, ng, out, err) : LSG_OK;
+  free(buf);
+  free(offs);
+  if (rc) {
+    free(out);
+    free(err);
+    return throw_lsg(env, ctx, "lsg_aggregate_signatures", rc);
+  }
+  napi_value res;
+  NAPI_CALL(env, napi_create_array_with_length(env, ng, &res));
+  for (uint32_t g = 0; g < ng; g++) {
+    napi_value o, sig;
+    napi_create_object(env, &o);
+    if (err[g] == 0) {
+      void* p;
+      napi_value ab;
+      napi_create_arraybuffer(env, 96, &p, &ab);
+      memcpy(p, out + 96 * (size_t)g, 96);
+      napi_create_typedarray(env, napi_uint8_array, 96, ab, 0, &sig);
+    } else {
+      napi_get_null(env, &sig);
+    }
+    napi_set_named_property(env, o, "signature", sig);
+    set_int(env, o, "err", err[g]);
+    napi_set_element(env, res, g, o);
+  }
+  free(out);
+  free(err);
+  return res;
+}
+
 /* ------------------------------------------------------------------ module */
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
@@ -532,6 +613,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, napi_enumerable, NULL},
       {"hashToG2", NULL, js_hash_to_g2, NULL, NULL, NULL, napi_enumerable, NULL},
       {"pubkeyTableSet", NULL, js_pubkey_table_set, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"aggregateSignatures", NULL, js_aggregate_signatures, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   NAPI_CALL(env, napi_define_properties(env, exports, sizeof props / sizeof props[0], props));
   return exports;

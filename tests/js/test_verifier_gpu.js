@@ -60,6 +60,15 @@ const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
                    signature: hex(cases.aggregate.sig)};
   assert.strictEqual(await pool.verifySignatureSets([byIndex, sets[0]], {batchable: true}), true);
   assert.strictEqual(await pool.verifySignatureSets([Object.assign({}, byIndex, {pubkeyIndices: ix.slice(1)})]), false);
+  // op-pool signature aggregation (SURVEY 8f(4)) against the oracle's golden fixture
+  const gold = JSON.parse(fs.readFileSync(path.join(__dirname, "..", "golden", "aggregate_signatures.json")));
+  const g96 = gold.cases.filter((c) => c.sigs[0].length === 192);
+  const aggs = pool.aggregateSignatures(g96.map((c) => c.sigs.map(hex)).concat([[]]));
+  g96.forEach((c, k) => {
+    assert.strictEqual(aggs[k].err, c.err);
+    if (c.err === 0) assert.strictEqual(Buffer.from(aggs[k].signature).toString("hex"), c.out);
+  });
+  assert.strictEqual(aggs[g96.length].err, 101);
   await pool.close();
   console.log("node host on GPU: all checks passed");
 })().catch((e) => {
