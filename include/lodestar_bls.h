@@ -15,6 +15,7 @@
  *   lsg_hash_to_g2         <- blst Hash_to_G2 inside Pairing.mul_n_aggregate
  *   lsg_sig_decode         <- maybeBatch.ts:23,36 Signature.fromBytes(bytes, affine, true)
  *   lsg_aggregate_signatures <- opPools Signature.aggregate
+ *   lsg_*signing_roots     <- util/signingRoot.ts:7-13 computeSigningRoot
  *   lsg_submit_jobs /      <- the asynchronous lsg_submit / lsg_wait pair of SURVEY.md 8b:
  *   lsg_wait_jobs             one BlsWorkReq[] package in flight per pipeline slot
  *   lsg_batch_* /          <- the per-GPU half of verifyMultipleSignatures for the
@@ -224,6 +225,19 @@ int lsg_pubkey_validate(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_
  * LSG_ERR_EMPTY_AGGREGATE for an empty group ("EMPTY_AGGREGATE_ARRAY"). */
 int lsg_aggregate_signatures(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, const uint32_t* offsets,
                              size_t n_groups, uint8_t* out96, int32_t* err);
+
+/* Signing roots on the GPU: computeSigningRoot(type, obj, domain) of
+ * state-transition/src/util/signingRoot.ts:7-13 = hash_tree_root(SigningData{objectRoot, domain}).
+ *   lsg_signing_roots              objectRoot given: roots32 = n x 32 bytes;
+ *   lsg_attestation_signing_roots  getAttestationDataSigningRoot (signatureSets/indexedAttestation.ts:11-19):
+ *                                  data128 = n SSZ-serialized phase0.AttestationData (128 bytes each:
+ *                                  slot, index, beaconBlockRoot, source{epoch, root}, target{epoch, root}).
+ * domain_stride 0: one 32-byte domain for every object; 32: one per object.  out32 = n x 32 bytes,
+ * the 32-byte messages lsg_set.msg carries. */
+int lsg_signing_roots(lsg_ctx* ctx, const uint8_t* roots32, size_t n, const uint8_t* domain32, uint32_t domain_stride,
+                      uint8_t* out32);
+int lsg_attestation_signing_roots(lsg_ctx* ctx, const uint8_t* data128, size_t n, const uint8_t* domain32,
+                                  uint32_t domain_stride, uint8_t* out32);
 
 /* Test/bench input generation (not on the verify path): sig_i = sk_i * H(m_i) compressed,
  * pk_i = sk_i * G1 uncompressed; sks are 32-byte big-endian secret keys. */

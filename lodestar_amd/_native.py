@@ -95,6 +95,7 @@ EXPORTS = [
     "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups", "lsg_probe_mad_peak",
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
+    "lsg_signing_roots", "lsg_attestation_signing_roots",
 ]
 
 
@@ -140,6 +141,8 @@ def load_library(path=LIB_PATH):
         lib.lsg_final_submit_groups.argtypes = [vp, ctypes.c_char_p, sz, sz, pu64]
         lib.lsg_final_wait_groups.argtypes = [vp, u64, pi32]
         lib.lsg_pubkey_validate.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
+        lib.lsg_signing_roots.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, u32, ctypes.c_char_p]
+        lib.lsg_attestation_signing_roots.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, u32, ctypes.c_char_p]
         lib.lsg_aggregate_signatures.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(u32), sz,
                                                  ctypes.c_char_p, pi32]
         lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
@@ -333,6 +336,29 @@ class Context:
         self._check(self.lib.lsg_aggregate_signatures(self.h, b"".join(flat), sl, offs, ng, out, err),
                     "lsg_aggregate_signatures")
         return [(out.raw[96 * g:96 * g + 96], err[g]) for g in range(ng)]
+
+    def _signing_roots(self, fn, objs, size, domains):
+        n = len(objs)
+        if n == 0:
+            return []
+        assert all(len(o) == size for o in objs)
+        if isinstance(domains, (bytes, bytearray)):
+            dom, stride = bytes(domains), 0
+        else:
+            assert len(domains) == n
+            dom, stride = b"".join(domains), 32
+        assert len(dom) == (32 if stride == 0 else 32 * n)
+        out = ctypes.create_string_buffer(32 * n)
+        self._check(getattr(self.lib, fn)(self.h, b"".join(objs), n, dom, stride, out), fn)
+        return [out.raw[32 * i:32 * i + 32] for i in range(n)]
+
+    def signing_roots(self, object_roots, domains):
+        """computeSigningRoot from object roots; `domains` is one 32-byte domain or a list."""
+        return self._signing_roots("lsg_signing_roots", object_roots, 32, domains)
+
+    def attestation_signing_roots(self, data128s, domains):
+        """getAttestationDataSigningRoot from SSZ-serialized phase0.AttestationData (128 B each)."""
+        return self._signing_roots("lsg_attestation_signing_roots", data128s, 128, domains)
 
     def hash_to_g2(self, msgs, dst=b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"):
         if not msgs:

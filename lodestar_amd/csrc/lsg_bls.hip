@@ -513,6 +513,82 @@ __global__ void LSG_KERNEL_ATTR k_g2p_compress(int n, const uint32_t* __restrict
   g2_compress(out96 + 96 * item, a, inf);
 }
 
+// ---- SSZ signing roots, one thread per object.  Chunks are 8 big-endian
+// SHA-256 words; every node is SHA-256 of exactly 64 bytes, so its second block is the
+// constant padding block of a 512-bit message.
+LSG_INL void ssz_hash2(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  uint32_t blk[16];
+  for (int k = 0; k < 8; k++) {
+    blk[k] = a[k];
+    blk[8 + k] = b[k];
+  }
+  sha256_compress(st, blk);
+  for (int k = 0; k < 16; k++) blk[k] = 0;
+  blk[0] = 0x80000000u;
+  blk[15] = 512;
+  sha256_compress(st, blk);
+  for (int k = 0; k < 8; k++) out[k] = st[k];
+}
+
+// `len` (<= 32) bytes at p as a zero-padded SSZ chunk
+LSG_INL void ssz_chunk(uint32_t* w, const uint8_t* p, int len) {
+  for (int k = 0; k < 8; k++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4; j++) v = (v << 8) | (4 * k + j < len ? p[4 * k + j] : 0u);
+    w[k] = v;
+  }
+}
+
+LSG_INL void ssz_store(uint8_t* out, const uint32_t* w) { be_words_to_bytes(out, w, 8); }
+
+// hash_tree_root(SigningData{objectRoot, domain}) (util/signingRoot.ts:7-13)
+__global__ void __launch_bounds__(64) k_signing_root(int n, const uint8_t* __restrict__ roots,
+                                                     const uint8_t* __restrict__ domains, uint32_t dstride,
+                                                     uint8_t* __restrict__ out32) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  uint32_t r[8], d[8], o[8];
+  ssz_chunk(r, roots + 32 * i, 32);
+  ssz_chunk(d, domains + dstride * i, 32);
+  ssz_hash2(r, d, o);
+  ssz_store(out32 + 32 * i, o);
+}
+
+// getAttestationDataSigningRoot (signatureSets/indexedAttestation.ts:11-19) from the SSZ
+// serialization of phase0.AttestationData (128 bytes: slot u64, index u64, beaconBlockRoot,
+// source {epoch u64, root}, target {epoch u64, root}): 5 fields -> 8 leaves, 3 levels, then
+// SigningData -- 10 node hashes per object
+__global__ void __launch_bounds__(64) k_attestation_signing_root(int n, const uint8_t* __restrict__ data,
+                                                                 const uint8_t* __restrict__ domains,
+                                                                 uint32_t dstride, uint8_t* __restrict__ out32) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  const uint8_t* a = data + 128 * i;
+  uint32_t l0[8], l1[8], l2[8], l3[8], l4[8], t[8], z[8], z1[8], h01[8], h23[8], h45[8];
+  for (int k = 0; k < 8; k++) z[k] = 0;
+  ssz_chunk(l0, a, 8);       // slot
+  ssz_chunk(l1, a + 8, 8);   // index
+  ssz_chunk(l2, a + 16, 32); // beaconBlockRoot
+  ssz_chunk(t, a + 48, 8);   // source = Checkpoint{epoch, root}
+  ssz_chunk(l3, a + 56, 32);
+  ssz_hash2(t, l3, l3);
+  ssz_chunk(t, a + 88, 8);   // target
+  ssz_chunk(l4, a + 96, 32);
+  ssz_hash2(t, l4, l4);
+  ssz_hash2(z, z, z1);       // leaves 5..7 are zero chunks
+  ssz_hash2(l0, l1, h01);
+  ssz_hash2(l2, l3, h23);
+  ssz_hash2(l4, z, h45);
+  ssz_hash2(h01, h23, h01);
+  ssz_hash2(h45, z1, h45);
+  ssz_hash2(h01, h45, t);    // AttestationData.hashTreeRoot
+  ssz_chunk(z, domains + dstride * i, 32);
+  ssz_hash2(t, z, t);
+  ssz_store(out32 + 32 * i, t);
+}
+
 // pk_i = [sk_i] G1, uncompressed 96 bytes (bench/test input generation)
 __global__ void LSG_KERNEL_ATTR k_sk_to_pk(int n, const uint8_t* __restrict__ sks,
                                                        uint8_t* __restrict__ out96) {
@@ -2298,6 +2374,46 @@ int lsg_aggregate_signatures(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, 
     if (!err[g]) memcpy(out96 + 96 * g, blob.data() + 96 * k, 96);
   }
   return LSG_OK;
+}
+
+// SSZ signing roots; kind 0: object roots given, 1: AttestationData bytes
+static int signing_roots(lsg_ctx* c, int kind, const uint8_t* objs, size_t n, const uint8_t* domain,
+                         uint32_t dstride, uint8_t* out32) {
+  const size_t ob = kind ? 128 : 32;
+  if (!c || !domain || (dstride != 0 && dstride != 32) || (n && (!objs || !out32)) || n > 0x7fffffffull)
+    return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  const size_t nd = dstride ? n : 1;
+  int rc;
+  if ((rc = ensure(s, s->d_aux, ob * n + 32 * nd)) || (rc = ensure(s, s->d_blob, 32 * n))) return rc;
+  uint8_t* d_obj = P_<uint8_t>(s->d_aux);
+  uint8_t* d_dom = d_obj + ob * n;
+  LSG_HIP(s, hipMemcpyAsync(d_obj, objs, ob * n, hipMemcpyHostToDevice, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(d_dom, domain, 32 * nd, hipMemcpyHostToDevice, s->st[0]));
+  const int nn = (int)n;
+  const unsigned blocks = (unsigned)((n + 63) / 64);
+  if (kind)
+    LAUNCH_T(s, "k_attestation_signing_root", k_attestation_signing_root, blocks, 64, nn, d_obj, d_dom, dstride,
+             P_<uint8_t>(s->d_blob));
+  else
+    LAUNCH_T(s, "k_signing_root", k_signing_root, blocks, 64, nn, d_obj, d_dom, dstride, P_<uint8_t>(s->d_blob));
+  LSG_HIP(s, hipMemcpyAsync(out32, s->d_blob.p, 32 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->last = s;
+  return LSG_OK;
+}
+
+int lsg_signing_roots(lsg_ctx* c, const uint8_t* roots32, size_t n, const uint8_t* domain32, uint32_t domain_stride,
+                      uint8_t* out32) {
+  return signing_roots(c, 0, roots32, n, domain32, domain_stride, out32);
+}
+
+int lsg_attestation_signing_roots(lsg_ctx* c, const uint8_t* data128, size_t n, const uint8_t* domain32,
+                                  uint32_t domain_stride, uint8_t* out32) {
+  return signing_roots(c, 1, data128, n, domain32, domain_stride, out32);
 }
 
 int lsg_sign(lsg_ctx* c, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96) {

@@ -81,3 +81,23 @@ def genesis_deposit_signing_root(pubkey_bytes):
     wc[0] = 0  # BLS_WITHDRAWAL_PREFIX
     domain = compute_domain(DOMAIN_DEPOSIT, GENESIS_FORK_VERSION_MINIMAL, bytes(32))
     return bytes(wc), compute_signing_root(deposit_message_root(pubkey_bytes, bytes(wc), MAX_EFFECTIVE_BALANCE), domain)
+
+
+def attestation_data_root(data128):
+    """ssz.phase0.AttestationData.hashTreeRoot over its 128-byte SSZ serialization (slot u64,
+    index u64, beaconBlockRoot, source Checkpoint{epoch u64, root}, target Checkpoint) -- the
+    objectRoot of getAttestationDataSigningRoot (state-transition/src/signatureSets/
+    indexedAttestation.ts:11-19).  SURVEY.md 8f(3)."""
+    assert len(data128) == 128
+    d = bytes(data128)
+
+    def u64(b):
+        return b + bytes(24)
+
+    def checkpoint(b):
+        return _merkleize([u64(b[:8]), b[8:40]])
+    return _merkleize([u64(d[0:8]), u64(d[8:16]), d[16:48], checkpoint(d[48:88]), checkpoint(d[88:128])])
+
+
+def attestation_signing_root(data128, domain):
+    return compute_signing_root(attestation_data_root(data128), domain)

@@ -538,3 +538,44 @@ def test_aggregate_signatures_linearity_at_scale(ctx):
     expect = ctx.sign(sums, [bd.msg("oppool-scale", g) for g in range(len(sizes))])
     for g, ((o, err), e) in enumerate(zip(out, expect)):
         assert err == 0 and o == e, g
+
+
+def test_signing_roots_pinned_by_genesis_kat(ctx):
+    """computeSigningRoot on the GPU reproduces the deposit signing root the
+    reference's genesis KAT signs (test/e2e/interop/genesisState.test.ts:49-56), and the
+    AttestationData form matches the oracle for per-object and shared domains."""
+    import random
+    from oracle import interop as oi
+    pk = bytes.fromhex(GENESIS_KAT["pubkey"])
+    wc, root = genesis_deposit_signing_root(pk)
+    domain = oi.compute_domain(oi.DOMAIN_DEPOSIT, oi.GENESIS_FORK_VERSION_MINIMAL, bytes(32))
+    obj = oi.deposit_message_root(pk, wc, oi.MAX_EFFECTIVE_BALANCE)
+    assert ctx.signing_roots([obj], domain) == [root]
+    rng = random.Random(11)
+    datas = [bytes(rng.getrandbits(8) for _ in range(128)) for _ in range(300)]
+    doms = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(300)]
+    assert ctx.attestation_signing_roots(datas, doms) == [oi.attestation_signing_root(d, m) for d, m in zip(datas, doms)]
+    assert ctx.attestation_signing_roots(datas[:5], doms[0]) == [oi.attestation_signing_root(d, doms[0])
+                                                                  for d in datas[:5]]
+    objs = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(65)]
+    assert ctx.signing_roots(objs, doms[:65]) == [oi.compute_signing_root(o, m) for o, m in zip(objs, doms)]
+
+
+def test_attestation_signing_roots_feed_verification(ctx):
+    """The GPU's attestation signing roots are the messages the verifier checks: sets signed
+    over them verify, and a set whose AttestationData changes by one bit does not."""
+    import random
+    from oracle.fields import R
+    rng = random.Random(12)
+    n = 64
+    datas = [bytes(rng.getrandbits(8) for _ in range(128)) for _ in range(n)]
+    domain = bytes(rng.getrandbits(8) for _ in range(32))
+    roots = ctx.attestation_signing_roots(datas, domain)
+    sks = [bd.sk(i) for i in range(n)]
+    sigs = ctx.sign(sks, roots)
+    sets = [([bd.pk_bytes(i)], roots[i], sigs[i]) for i in range(n)]
+    assert ctx.verify_sets(sets, seed=3)[0] == 1
+    bad = bytearray(datas[7])
+    bad[0] ^= 1
+    sets[7] = (sets[7][0], ctx.attestation_signing_roots([bytes(bad)], domain)[0], sets[7][2])
+    assert ctx.verify_sets(sets, seed=3)[0] == 0

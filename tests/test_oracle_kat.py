@@ -124,3 +124,19 @@ def test_aggregate_signatures_oracle_and_golden():
             assert e.value.code == c["err"]
         else:
             assert aggregate_signatures(sg).hex() == c["out"]
+
+
+def test_attestation_signing_root_oracle():
+    """AttestationData.hashTreeRoot restated against the tree written out
+    node by node; SigningData is the helper the genesis KAT pins."""
+    import hashlib
+    from oracle import interop as oi
+    h = lambda a, b: hashlib.sha256(a + b).digest()  # noqa: E731
+    d = bytes(range(128))
+    dom = bytes(range(100, 132))
+    u = lambda b: b + bytes(24)  # noqa: E731
+    z = bytes(32)
+    src, tgt = h(u(d[48:56]), d[56:88]), h(u(d[88:96]), d[96:128])
+    root = h(h(h(u(d[0:8]), u(d[8:16])), h(d[16:48], src)), h(h(tgt, z), h(z, z)))
+    assert oi.attestation_data_root(d) == root
+    assert oi.attestation_signing_root(d, dom) == h(root, dom)
