@@ -140,21 +140,26 @@ def pmc_traffic(kernel, sets_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=384)
+    ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--workload", choices=["firehose", "block"], default="firehose",
                     help="firehose: config D shard (default, the headline line); block: config C")
     ap.add_argument("--sets-per-gpu", type=int, default=None, help="sets per step (4096 firehose, 128 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=4, help="submissions in flight (<= library pipeline slots)")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="submissions in flight (<= library pipeline slots; 3 firehose, 4 block)")
     ap.add_argument("--groups", type=int, default=None,
-                    help="batches (steps) per submission, verified as separate RLC groups (6 firehose, 32 block)")
+                    help="batches (steps) per submission, verified as separate RLC groups (12 firehose, 32 block)")
     args = ap.parse_args()
     block = args.workload == "block"
     if args.sets_per_gpu is None:
         args.sets_per_gpu = 128 if block else 4096
+    # firehose default 12 x 3 (profiles/r01_bench_sweeps_inline.txt): 2.28M sets/s at p50 78 ms,
+    # against 2.03-2.19M at p50 52 ms for 6 x 4 and 2.33M at p50 97 ms for 12 x 4
     if args.groups is None:
-        args.groups = 32 if block else 6
+        args.groups = 32 if block else 12
+    if args.depth is None:
+        args.depth = 4 if block else 3
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
