@@ -263,7 +263,7 @@ def main():
         for name, ms in ticket_times:
             agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
     stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_miller_accum": "miller_accum2_per_set",
-                "k_miller_lines": "miller_lines", "k_h2c_map": "hash_map", "k_sig_scale": "sig_scale",
+                "k_miller_lines": "miller_lines", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
     per_set = {k: v for k, v in agg.items() if k in stage_of}
     dom = max(per_set, key=per_set.get)

@@ -73,6 +73,9 @@ namespace {
 #ifndef LSG_H2C_WAVES
 #define LSG_H2C_WAVES LSG_WAVES_PER_EU
 #endif
+#ifndef LSG_H2C_SPLIT
+#define LSG_H2C_SPLIT 1
+#endif
 #ifndef LSG_SUBGROUP_WAVES
 #define LSG_SUBGROUP_WAVES LSG_WAVES_PER_EU
 #endif
@@ -269,7 +272,22 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_map(int n, const uint32_t
   h2c_u_t u = lane_load<h2c_u_t>(U, item);
   g2p_t q0 = iso_map3(map_to_curve_sswu_ni(u.u0, lane_load<fp_t>(ninv, 2 * item)));
   g2p_t q1 = iso_map3(map_to_curve_sswu_ni(u.u1, lane_load<fp_t>(ninv, 2 * item + 1)));
+#if LSG_H2C_SPLIT
+  lane_store(Hp, item, g2_add(q0, q1));  // k_h2c_clear finishes the point
+#else
   g2p_t q = clear_cofactor_g2(g2_add(q0, q1));
+  bool is_inf = proj_is_inf(q);
+  lane_store(Hp, item, q);
+  lane_store(zN, item, is_inf ? fp_zero() : fp2_norm(q.Z));
+  if (lead) hinf[item] = is_inf ? 1 : 0;
+#endif
+}
+// stage 2b (LSG_H2C_SPLIT): clear_cofactor in place.  Split from the map so that neither
+// kernel holds the other's live state: the fused kernel spilled 757 registers.
+__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, uint32_t* __restrict__ Hp,
+                                                            uint32_t* __restrict__ zN, uint8_t* __restrict__ hinf) {
+  LANE_ITEM(n);
+  g2p_t q = clear_cofactor_g2(lane_load<g2p_t>(Hp, item));
   bool is_inf = proj_is_inf(q);
   lane_store(Hp, item, q);
   lane_store(zN, item, is_inf ? fp_zero() : fp2_norm(q.Z));
@@ -1184,6 +1202,9 @@ int launch_hash(Slot* s, int n) {
   if ((rc = batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)))) return rc;
   LAUNCH(s, k_h2c_map, n, n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp),
          P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf));
+#if LSG_H2C_SPLIT
+  LAUNCH(s, k_h2c_clear, n, n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf));
+#endif
   if ((rc = batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)))) return rc;
   LAUNCH(s, k_h2c_affine, n, n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi), P_<uint8_t>(s->d_hinf),
          P_<uint32_t>(s->d_H));

@@ -600,6 +600,33 @@ static napi_value js_aggregate_signatures(napi_env env, napi_callback_info info)
   return res;
 }
 
+/* attestationSigningRoots(ctx, data: Uint8Array (n x 128 B SSZ AttestationData), domain: Uint8Array
+ * (32 B shared, or n x 32 B)) -> Uint8Array(n x 32): getAttestationDataSigningRoot for n objects
+ * (8f(3), lsg_attestation_signing_roots) */
+static napi_value js_attestation_signing_roots(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  const uint8_t *d, *dom;
+  size_t dl, doml;
+  if (get_bytes(env, argv[1], &d, &dl) || get_bytes(env, argv[2], &dom, &doml) || dl % 128 ||
+      (doml != 32 && doml != 32 * (dl / 128))) {
+    napi_throw_type_error(env, NULL, "lsg_napi: attestationSigningRoots(ctx, data: n x 128 B, domain: 32 B | n x 32 B)");
+    return NULL;
+  }
+  const size_t n = dl / 128;
+  void* outp;
+  napi_value ab, out;
+  NAPI_CALL(env, napi_create_arraybuffer(env, 32 * n, &outp, &ab));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, 32 * n, ab, 0, &out));
+  uint32_t stride = doml == 32 ? 0 : 32;
+  int rc = n ? lsg_attestation_signing_roots(ctx, d, n, dom, stride, (uint8_t*)outp) : LSG_OK;
+  if (rc) return throw_lsg(env, ctx, "lsg_attestation_signing_roots", rc);
+  return out;
+}
+
 /* ------------------------------------------------------------------ module */
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
@@ -614,6 +641,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"hashToG2", NULL, js_hash_to_g2, NULL, NULL, NULL, napi_enumerable, NULL},
       {"pubkeyTableSet", NULL, js_pubkey_table_set, NULL, NULL, NULL, napi_enumerable, NULL},
       {"aggregateSignatures", NULL, js_aggregate_signatures, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"attestationSigningRoots", NULL, js_attestation_signing_roots, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   NAPI_CALL(env, napi_define_properties(env, exports, sizeof props / sizeof props[0], props));
   return exports;

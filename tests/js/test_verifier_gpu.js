@@ -69,6 +69,10 @@ const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
     if (c.err === 0) assert.strictEqual(Buffer.from(aggs[k].signature).toString("hex"), c.out);
   });
   assert.strictEqual(aggs[g96.length].err, 101);
+  // signing roots (SURVEY 8f(3)) against the oracle's values in the cases file
+  const sr = cases.signing_roots;
+  const roots = pool.addon.attestationSigningRoots(pool.ctx, hex(sr.data), hex(sr.domain));
+  assert.strictEqual(Buffer.from(roots).toString("hex"), sr.roots);
   await pool.close();
   console.log("node host on GPU: all checks passed");
 })().catch((e) => {

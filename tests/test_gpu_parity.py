@@ -279,6 +279,9 @@ def test_node_host_on_gpu(ctx, tmp_path):
     pts = [ov.public_key_from_bytes(p) for p in agg[0]]
     h2c_msg = bd.msg("node-h2c", 0)
     dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    from oracle import interop as oi
+    sr_data = bytes((7 * k + 3) & 255 for k in range(3 * 128))
+    sr_dom = bytes(range(32, 64))
     cases = {
         "valid": [{"pks": [p.hex() for p in s[0]], "msg": s[1].hex(), "sig": s[2].hex()} for s in valid],
         "wrong_message": {"pks": [p.hex() for p in wrong[0]], "msg": wrong[1].hex(), "sig": wrong[2].hex()},
@@ -286,6 +289,9 @@ def test_node_host_on_gpu(ctx, tmp_path):
         "aggregate_pk": g1_serialize(ov.aggregate_pubkeys(pts)).hex(),
         "same_message": {"msg": sm_msg.hex(), "sets": sm_sets, "expected": sm_exp},
         "h2c": {"msg": h2c_msg.hex(), "dst": dst.decode(), "out": g2_serialize(h2c.hash_to_g2(h2c_msg, dst)).hex()},
+        "signing_roots": {"data": sr_data.hex(), "domain": sr_dom.hex(),
+                          "roots": b"".join(oi.attestation_signing_root(sr_data[128 * k:128 * k + 128], sr_dom)
+                                            for k in range(3)).hex()},
     }
     f = tmp_path / "cases.json"
     f.write_text(json.dumps(cases))
