@@ -262,7 +262,11 @@ def main():
     for ticket_times in ktimes:
         for name, ms in ticket_times:
             agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
-    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_miller_accum": "miller_accum2_per_set",
+    # pairs per Miller item: the library's LSG_MILLER_K (default 4) sets k_miller_accum's work per set
+    mk = os.environ.get("LSG_MILLER_K", "4")
+    accum_key = f"miller_accum{mk}_per_set" if f"miller_accum{mk}_per_set" in opc["stage_fp_muls"] \
+        else "miller_accum2_per_set"
+    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_miller_accum": accum_key,
                 "k_miller_lines": "miller_lines", "k_sig_scale": "sig_scale",
                 "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
     per_set = {k: v for k, v in agg.items() if k in stage_of}
@@ -283,6 +287,8 @@ def main():
         per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / n
     else:
         per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / n
+    # the whole-path counts price the Miller stage at K = 2; credit only the work K actually does
+    per_set_muls += opc["stage_fp_muls"][accum_key] - opc["stage_fp_muls"]["miller_accum2_per_set"]
     pks_per_set = sum(len(p) for p, _, _ in sets) / len(sets)
     per_set_muls += (pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]

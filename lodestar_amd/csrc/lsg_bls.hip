@@ -1321,8 +1321,10 @@ constexpr int LSG_MILLER_KMAX = 4;  // pairs per multi-Miller item: 1, 2 or 4 (e
 int miller_k() {
   static int k = [] {
     const char* e = getenv("LSG_MILLER_K");
-    int v = e ? atoi(e) : 2;  // K=2 measured best on MI355X (profiles/r01_bench_sweeps.txt)
-    return (v == 1 || v == 2 || v == 4) ? v : 2;
+    // K=4 since the tower is inlined: 2.45M vs 2.35M sets/s at 12x3 (profiles/r01_inline_ab.txt);
+    // before, with Fp12 stack frames, K=2 was best (profiles/r01_bench_sweeps.txt)
+    int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4) ? v : 4;
   }();
   return k;
 }

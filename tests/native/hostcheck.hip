@@ -240,6 +240,11 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
     lsg_mul_count = 0;
     (void)miller_accum_multi<2>(P2, use2, [&](int, int st) { return lines[st]; });
     counts[13] = lsg_mul_count / 2;
+    g1a_t P4[4] = {P, P, P, P};
+    bool use4[4] = {true, true, true, true};
+    lsg_mul_count = 0;
+    (void)miller_accum_multi<4>(P4, use4, [&](int, int st) { return lines[st]; });
+    counts[14] = lsg_mul_count / 4;  // K = 4 pairs per item (the default, LSG_MILLER_K)
   }
   lsg_mul_count = 0;
   (void)g2_add(rs, rs);

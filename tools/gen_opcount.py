@@ -13,7 +13,7 @@ from tests import blsdata as bd  # noqa: E402
 
 NAMES = ["sig_decode", "sig_subgroup", "pk_decode", "pk_scale", "hash_map", "sig_scale", "miller",
          "g2_add", "fp12_mul", "final_exp", "g1_add", "miller_multi2_per_set", "miller_lines",
-         "miller_accum2_per_set"]
+         "miller_accum2_per_set", "miller_accum4_per_set"]
 
 
 def main():
