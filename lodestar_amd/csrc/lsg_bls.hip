@@ -751,11 +751,16 @@ TreePlan plan_tree(const std::vector<std::vector<int32_t>>& groups) {
         }
       }
     }
+    // a level that leaves group g's single value in slot g is the last one: it writes out[]
+    // directly and the gather launch is skipped (one launch less per tree on the chain)
+    bool placed = !done;
+    for (size_t g = 0; placed && g < ng; g++)
+      if (nxt[g].size() != 1 || nxt[g][0] != (int32_t)g) placed = false;
     P.levels.push_back({P.idx.size(), cnt});
     P.idx.insert(P.idx.end(), ia.begin(), ia.end());
     P.idx.insert(P.idx.end(), ib.begin(), ib.end());
     P.max_level = std::max(P.max_level, cnt);
-    if (done) break;
+    if (done || placed) break;
     cur.swap(nxt);
   }
   return P;
