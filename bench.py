@@ -1,22 +1,36 @@
 #!/usr/bin/env python3
-"""Benchmark: BLS signature sets verified/sec on MI355X (BASELINE.json metric).
+"""Benchmark: BLS signature sets verified/sec on MI355X (BASELINE.json metric), through the
+drop-in jobs path (lsg_submit_jobs / lsg_wait_jobs: the C ABI BlsGpuVerifier calls).
 
-Workload ("epoch firehose"): every GPU verifies a shard of 4096
-single-pubkey gossip-attestation sets per step (weak scaling: at 8 GPUs the node covers the
-~32k-set mainnet slot).  Keys are the interop keys sk_{v mod 1024}
-(packages/state-transition/src/util/interop.ts:19-22), messages sha256(b"lodestar-mi355x" ||
-b"firehose" || i), signatures sk*H(m) -- synthetic, generated on the GPU before timing.
+One step = one work package per GPU (BlsWorkReq[]: the jobs one worker would get,
+packages/beacon-node/src/chain/bls/multithread/worker.ts:30-106), run the way the Node host
+runs it: the C side copies every input byte from host memory into pinned staging, draws
+fresh RLC randomizers from the OS CSPRNG (getrandom), plans the bucket MSM, launches every
+stage, and the wait applies the reference's verdict rules; the bench then checks every job's
+verdict.  Nothing is pre-staged on the device and no per-package work happens outside the
+timed region except building the host-side job arrays (PreparedJobs, once per distinct
+package) -- what the Node host does when it serialises sets.
 
-One step = the sharded hot path of SURVEY.md 8(e) on inputs already resident in HBM:
-  per GPU  lsg_batch_submit/wait: decode + subgroup-check signatures, decode pubkeys,
-           hash_to_G2, 64-bit RLC scalars, per-set Miller loops, signature-sum Miller loop,
-           Fp12 product
-  node     all_gather of the 576-byte Fp12 partials (RCCL over xGMI when N > 1)
-  rank 0.. lsg_final_submit/wait: product of partials + one final exponentiation -> verdict
-Steps are pipelined as a firehose verifier runs them: two batches in flight (the library's two
-pipeline slots) and the final exponentiation of batch k on its own stream while batch k+1
-computes.  Every batch is verified (verdict checked) inside the timed region.
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+Workloads:
+  jobs         config D shape (default, the headline): 32,768 single-pubkey gossip sets per
+               package = one mainnet slot of unaggregated attestations per GPU (weak scaling:
+               at 8 GPUs the node takes 8 slots' worth per step); one batchable job per set
+  block        config C: 32 blocks per package, each one non-batchable job of 128 aggregate
+               sets of 440-460 signers named by index into the device pubkey table
+  sync         config B: 64 sync-committee contributions per package, each one batchable
+               job of one 512-signer aggregate set
+  gossip       config A: one job of 128 single sets per package (latency-bound)
+  adversarial  config E: the jobs workload with 1% of the sets corrupted over the five kinds
+               (wrong message, flipped x bit, truncated, non-subgroup point, infinity); every
+               verdict is checked against its expected value
+Keys: interop keys sk_{v mod 1024} (state-transition/src/util/interop.ts:19-22); messages
+sha256(b"lodestar-mi355x" || workload || i); signatures made on the GPU before timing.
+
+N > 1 (torch.distributed.run, one process per GPU): every rank resolves its package with the
+node check of SURVEY.md 8e -- its partial (lsg_jobs_partial) is all-gathered over RCCL, the
+product of the N partials gets one final exponentiation (lsg_final_*), and the ticket is
+resolved with that verdict (lsg_wait_jobs_node).
+Launch: python bench.py [--gpus N --steps K --warmup W --workload jobs]
 """
 import argparse
 import collections
@@ -28,52 +42,141 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# 2 pipeline slots x 2 streams + the final-exponentiation stream (+ RCCL's): give each its
-# own hardware queue instead of HIP's default 4 shared ones
+# pipeline slots x 2 streams + the final-exponentiation streams: give each its own hardware
+# queue instead of HIP's default 4 shared ones
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 METRIC = "BLS signature sets verified/sec (whole node) at 1/2/4/8 MI355X; p50 batch latency"
+N_KEYS = 1024
 
 
 def interop_sk(i):
     return int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER
 
 
-def make_shard(ctx, rank, n):
-    keys = 1024
-    sks = [interop_sk(i) for i in range(keys)]
-    pks = ctx.sk_to_pk(sks)
-    base = rank * n
-    msgs = [hashlib.sha256(b"lodestar-mi355x" + b"firehose" + (base + i).to_bytes(8, "little")).digest()
-            for i in range(n)]
-    sigs = ctx.sign([sks[(base + i) % keys] for i in range(n)], msgs)
-    return [([pks[(base + i) % keys]], msgs[i], sigs[i]) for i in range(n)]
+def msg(tag, i):
+    return hashlib.sha256(b"lodestar-mi355x" + tag + i.to_bytes(8, "little")).digest()
 
 
-def make_block(ctx, rank, n):
-    """SURVEY 8(d) config C, "full mainnet block body": n aggregate-attestation sets of 440-460
-    signers each (~450), distinct messages.  Keys live in the device pubkey table (8f(1),
-    lsg_pubkey_table_set over the 1024 interop keys) and sets name their signers by index,
-    as the node's index2pubkey cache does; signatures are (sum sk) * H(m)."""
-    from lodestar_amd._native import PkIndices
-    keys = 1024
-    sks = [interop_sk(i) for i in range(keys)]
-    errs = ctx.pubkey_table_set(0, ctx.sk_to_pk(sks))
-    if any(errs):
-        raise SystemExit("pubkey table load failed")
-    idx, agg_sk, msgs = [], [], []
-    for i in range(n):
-        g = rank * n + i
-        size = 440 + (g * 7) % 21
-        start = (g * 53) % keys
-        ix = [(start + j) % keys for j in range(size)]
-        idx.append(PkIndices(ix))
-        agg_sk.append(sum(sks[k] for k in ix) % R_ORDER)
-        msgs.append(hashlib.sha256(b"lodestar-mi355x" + b"block" + g.to_bytes(8, "little")).digest())
-    sigs = ctx.sign(agg_sk, msgs)
-    return [(idx[i], msgs[i], sigs[i]) for i in range(n)]
+class Workload:
+    """Builds the distinct packages of one workload: .packages = list of (jobs, expected)
+    with expected = per-job (status, code) or None (all valid)."""
+
+    def __init__(self, ctx, name, rank, sets_per_step, n_packages):
+        from lodestar_amd._native import PkIndices
+        self.name = name
+        sks = [interop_sk(i) for i in range(N_KEYS)]
+        pks = ctx.sk_to_pk(sks)
+        self.packages = []
+        tag = name.encode()
+        if name in ("jobs", "adversarial", "gossip"):
+            n = 128 if name == "gossip" else sets_per_step
+            for p in range(n_packages):
+                base = (rank * n_packages + p) * n
+                msgs = [msg(tag, base + i) for i in range(n)]
+                sigs = ctx.sign([sks[(base + i) % N_KEYS] for i in range(n)], msgs)
+                sets = [([pks[(base + i) % N_KEYS]], msgs[i], sigs[i]) for i in range(n)]
+                if name == "gossip":
+                    self.packages.append(([(sets, 1)], None))
+                elif name == "jobs":
+                    self.packages.append(([([s], 1) for s in sets], None))
+                else:
+                    self.packages.append(self._corrupt(ctx, sets, seed=base))
+            self.sets_per_package = n
+            self.pks_per_set = 1.0
+        elif name == "block":
+            errs = ctx.pubkey_table_set(0, pks)
+            if any(errs):
+                raise SystemExit("pubkey table load failed")
+            blocks, per_block = 32, 128
+            for p in range(n_packages):
+                jobs, npk = [], 0
+                for b in range(blocks):
+                    idx, agg, msgs = [], [], []
+                    for i in range(per_block):
+                        g = ((rank * n_packages + p) * blocks + b) * per_block + i
+                        size = 440 + (g * 7) % 21
+                        start = (g * 53) % N_KEYS
+                        ix = [(start + j) % N_KEYS for j in range(size)]
+                        idx.append(PkIndices(ix))
+                        agg.append(sum(sks[k] for k in ix) % R_ORDER)
+                        msgs.append(msg(tag, g))
+                        npk += size
+                    sigs = ctx.sign(agg, msgs)
+                    jobs.append(([(idx[i], msgs[i], sigs[i]) for i in range(per_block)], 0))  # non-batchable
+                self.packages.append((jobs, None))
+            self.sets_per_package = blocks * per_block
+            self.pks_per_set = npk / (blocks * per_block)
+        elif name == "sync":
+            errs = ctx.pubkey_table_set(0, pks)
+            if any(errs):
+                raise SystemExit("pubkey table load failed")
+            contributions, size = 64, 512
+            for p in range(n_packages):
+                jobs = []
+                for c in range(contributions):
+                    g = (rank * n_packages + p) * contributions + c
+                    start = (g * 131) % N_KEYS
+                    ix = [(start + j) % N_KEYS for j in range(size)]
+                    m = msg(tag, g)
+                    sig = ctx.sign([sum(sks[k] for k in ix) % R_ORDER], [m])[0]
+                    jobs.append(([(PkIndices(ix), m, sig)], 1))
+                self.packages.append((jobs, None))
+            self.sets_per_package = contributions
+            self.pks_per_set = float(size)
+        else:
+            raise SystemExit(f"unknown workload {name}")
+
+    @staticmethod
+    def _non_subgroup_sig():
+        """A 96-byte compressed point on E2 outside G2, from the committed decode fixtures
+        (tests/golden/sig_decode.json: data, not the oracle)."""
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sig_decode.json")))
+        for c in gold["cases"]:
+            if c["err"] == 3 and len(c["sig"]) == 192:
+                return bytes.fromhex(c["sig"])
+        raise SystemExit("no non-subgroup fixture")
+
+    def _corrupt(self, ctx, sets, seed):
+        """1% corrupted, split evenly over the five kinds of SURVEY.md 8d config E with their
+        expected outcomes: wrong message -> false; truncated -> BLST_INVALID_SIZE; non-subgroup
+        point -> BLST_POINT_NOT_IN_GROUP; infinity -> false; flipped x bit -> the decode error
+        Signature.fromBytes gives (lsg_sig_decode; GPU decode parity is pinned by the golden
+        decode vectors in tests/test_gpu_parity.py).  Parity of these outcomes with the oracle is
+        tested in tests/test_gpu_configs.py (config E)."""
+        import random
+        rng = random.Random(seed)
+        n = len(sets)
+        idx = sorted(rng.sample(range(n), max(5, n // 100)))
+        out = list(sets)
+        exp = [(1, 0)] * n
+        nsg = self._non_subgroup_sig()
+        flips = []
+        for k, i in enumerate(idx):
+            pks, m, sig = out[i]
+            kind = k % 5
+            if kind == 0:
+                out[i], exp[i] = (pks, hashlib.sha256(m).digest(), sig), (0, 0)
+            elif kind == 1:
+                b = bytearray(sig)
+                b[40] ^= 1 << (k % 8)
+                out[i] = (pks, m, bytes(b))
+                flips.append(i)
+            elif kind == 2:
+                out[i], exp[i] = (pks, m, sig[:32]), (2, 10)
+            elif kind == 3:
+                out[i], exp[i] = (pks, m, nsg), (2, 3)
+            else:
+                out[i], exp[i] = (pks, m, bytes([0xC0]) + bytes(95)), (0, 0)
+        if flips:
+            dec = ctx.sig_decode([out[i][2] for i in flips])
+            for i, (_pt, e) in zip(flips, dec):
+                exp[i] = (2, e) if e else None
+            if any(exp[i] is None for i in flips):  # a flip that still decodes to a G2 point
+                raise SystemExit("flipped signature decoded to a subgroup point; change the seed")
+        return [([s], 1) for s in out], exp
 
 
 def host_cores():
@@ -89,7 +192,9 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
     """Reference-semantics CPU path: oracle/c (the C restatement of the oracle, checked against
     it and the golden vectors by tests/test_oracle_c.py) verifying the same workload the way
     the reference's worker pool does -- RLC batches of 16 sets (worker.ts:17,54), one thread
-    per host core (poolSize.ts:7) -- on a bounded sample of ~budget_s seconds."""
+    per host core (poolSize.ts:7) -- on a bounded sample of ~budget_s seconds.  A stand-in for
+    the @chainsafe/blst pool, which cannot run here; it runs at ~1.6 ms per set
+    and thread against the ~0.9 ms blst note of metrics/metrics/lodestar.ts:427."""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "c", "libbls_cpu.so"))
     lib.cpu_verify_chunks.restype = ctypes.c_int
@@ -101,12 +206,12 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
     def run(k):  # the first k sets of the workload (wrapping), 16-set batches on `cores` threads
         sub = [sets[i % len(sets)] for i in range(k)]
         pk = b"".join(p[0] for p, _, _ in sub)
-        msg = b"".join(m for _, m, _ in sub)
+        m = b"".join(x for _, x, _ in sub)
         sig = b"".join(s for _, _, s in sub)
         nch = -(-k // chunk)
         verdicts = (ctypes.c_int * nch)()
         t0 = time.perf_counter()
-        ok = lib.cpu_verify_chunks(pk, msg, sig, k, chunk, cores, 0x5EED, verdicts)
+        ok = lib.cpu_verify_chunks(pk, m, sig, k, chunk, cores, 0x5EED, verdicts)
         dt = time.perf_counter() - t0
         if ok != nch:
             raise SystemExit(f"cpu baseline: {nch - ok} of {nch} batches failed on valid sets")
@@ -117,22 +222,22 @@ def cpu_baseline_oracle(sets, budget_s=12.0):
     k = max(k, int(k * budget_s / max(dt, 1e-3)) // (chunk * cores) * chunk * cores)
     dt = run(k)
     return {"value": k / dt, "unit": "sets/s", "cores": cores, "kind": "port",
-            "sample": f"{k} sets of this workload in 16-set RLC batches on {cores} threads "
-                      f"(oracle/c, C restatement of the oracle, gcc -O3) in {dt:.1f}s"}
+            "sample": f"{k} single sets of this workload in 16-set RLC batches on {cores} threads "
+                      f"(oracle/c, C restatement of the oracle, gcc -O3) in {dt:.1f}s; "
+                      f"{1e3 * dt * cores / k:.2f} ms per set and thread"}
 
 
 def pmc_traffic(kernel, sets_per_launch):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (tools/gpu_traffic.sh ->
-    tools/pmc_traffic.py -> profiles/rNN_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE), when
-    they were measured at this launch size; None otherwise (PMC counters cannot be read from
-    inside the timed run)."""
+    """HBM bytes per launch of `kernel` from the committed PMC passes (tools/pmc_traffic.py ->
+    profiles/rNN_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE), when they were measured at
+    this launch size; None otherwise (PMC counters cannot be read inside the timed run)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None
     d = json.load(open(files[-1]))
     k = d["kernels"].get(kernel)
-    if k is None or d["sets_per_launch"] != sets_per_launch:
+    if k is None or d.get("sets_per_launch") != sets_per_launch:
         return None
     return k["hbm_bytes_per_dispatch"]
 
@@ -140,26 +245,18 @@ def pmc_traffic(kernel, sets_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=384)
-    ap.add_argument("--warmup", type=int, default=48)
-    ap.add_argument("--workload", choices=["firehose", "block"], default="firehose",
-                    help="firehose: config D shard (default, the headline line); block: config C")
-    ap.add_argument("--sets-per-gpu", type=int, default=None, help="sets per step (4096 firehose, 128 block)")
+    ap.add_argument("--steps", type=int, default=30, help="timed packages per GPU")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed packages per GPU (at least --depth are run)")
+    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial"], default="jobs")
+    ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
+    ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
+    ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=None,
-                    help="submissions in flight (<= library pipeline slots; 3 firehose, 4 block)")
-    ap.add_argument("--groups", type=int, default=None,
-                    help="batches (steps) per submission, verified as separate RLC groups (12 firehose, 32 block)")
     args = ap.parse_args()
-    block = args.workload == "block"
-    if args.sets_per_gpu is None:
-        args.sets_per_gpu = 128 if block else 4096
-    # firehose default 12 x 3 (profiles/r01_bench_sweeps_inline.txt): 2.28M sets/s at p50 78 ms,
-    # against 2.03-2.19M at p50 52 ms for 6 x 4 and 2.33M at p50 97 ms for 12 x 4
-    if args.groups is None:
-        args.groups = 32 if block else 12
     if args.depth is None:
-        args.depth = 4 if block else 3
+        args.depth = {"jobs": 3, "adversarial": 3, "block": 4, "sync": 6, "gossip": 8}[args.workload]
+    if args.packages is None:
+        args.packages = args.depth + 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -171,151 +268,173 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from lodestar_amd._native import Context
+    from lodestar_amd._native import Context, PreparedJobs
     ctx = Context(local)
-    n = args.sets_per_gpu
-    M = max(1, args.groups)
-    sets = make_block(ctx, rank, n * M) if block else make_shard(ctx, rank, n * M)
-    # M steps' shards staged as one package; each ticket verifies them as M separate RLC
-    # batches (groups of n sets, one Miller partial and one final exponentiation each)
-    staged = ctx.stage(sets, seed=0x5EED + rank)
+    wl = Workload(ctx, args.workload, rank, args.sets_per_step, args.packages)
+    prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
+    n_sets = wl.sets_per_package
+    max_pks = int(n_sets * wl.pks_per_set) + 1
+    ctx.reserve(n_sets, max_pks, 32 * n_sets, n_slots=args.depth + 1)
 
-    def gather(parts):
-        """all-gather the M partials of one ticket; -> per group, the partials of every rank"""
-        if dist is None:
-            return [[p] for p in parts]
+    import numpy as np
+
+    def verdict_ok(k, res, n_jobs):
+        st = np.frombuffer(res, dtype=np.int32, count=2 * n_jobs).reshape(-1, 2)
+        exp = wl.packages[k][1]
+        if exp is None:
+            return bool((st[:, 0] == 1).all())
+        e = np.array([[s, c if s == 2 else 0] for s, c in exp], dtype=np.int32)
+        got = st.copy()
+        got[got[:, 0] != 2, 1] = 0
+        return bool((got == e).all())
+
+    def gather_node(part):
+        """all-gather the 576-byte partials of one package over RCCL; -> node verdict ticket"""
         import torch
-        t = torch.frombuffer(bytearray(b"".join(parts)), dtype=torch.uint8).cuda(local)
-        out = torch.empty(world * 576 * M, dtype=torch.uint8, device=t.device)
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda(local)
+        out = torch.empty(world * 576, dtype=torch.uint8, device=t.device)
         dist.all_gather_into_tensor(out, t)
         b = out.cpu().numpy().tobytes()
-        return [[b[576 * (k * M + g):576 * (k * M + g) + 576] for k in range(world)] for g in range(M)]
+        ft = ctx.final_submit([b[576 * r:576 * r + 576] for r in range(world)])
+        if ft is None:
+            raise SystemExit("final-exponentiation entries exhausted")
+        return ft
+
+    stats_acc = collections.Counter()
+
+    def run(n_pkgs, depth, capture=False, seq0=0):
+        """n_pkgs packages, `depth` in flight; returns per-package submit->verdict latencies and
+        (capture) per-package HIP-event kernel times"""
+        lat, times = [], []
+        pend = collections.deque()
+        done = 0
+        seq = seq0
+
+        def submit():
+            nonlocal seq
+            k = seq % len(prepared)
+            t = ctx.submit_jobs(prepared[k])
+            if t is None:
+                raise SystemExit("pipeline slots exhausted: lower --depth")
+            pend.append((t, k, time.perf_counter()))
+            seq += 1
+
+        while len(pend) < min(depth, n_pkgs):
+            submit()
+        while pend:
+            t, k, t_sub = pend.popleft()
+            if dist is not None:  # node check of SURVEY.md 8e
+                part, _has = ctx.jobs_partial(t)
+                node_ok = ctx.final_wait(gather_node(part))
+                res, st = ctx.wait_jobs_node(t, 1 if node_ok else 0, raw=True)
+            else:
+                res, st = ctx.wait_jobs(t, raw=True)
+            lat.append(time.perf_counter() - t_sub)
+            if not verdict_ok(k, res, t[1]):
+                raise SystemExit(f"rank {rank}: package {k} verdicts differ from the expected ones")
+            stats_acc.update({"batch_retries": st["batch_retries"], "n_final_exps": st["n_final_exps"]})
+            if capture:
+                times.append(ctx.last_kernel_times())
+            done += 1
+            if done + len(pend) < n_pkgs:
+                submit()
+        return lat, times
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    def check(anyerr, ok):
-        if anyerr or not ok:
-            raise SystemExit(f"rank {rank}: verification failed (anyerr={anyerr}, verdict={ok})")
-
-    def submit():
-        t = ctx.batch_submit(staged, group_size=n if M > 1 else 0)
-        if t is None:
-            raise SystemExit("pipeline slots exhausted: lower --depth")
-        return t
-
-    def run(k_tickets, depth=2, capture=False):
-        """k_tickets submissions of M batches each, `depth` in flight; returns per-ticket
-        submit->last-verdict latencies and (if capture) the per-kernel HIP-event times of the
-        last ticket and its final exponentiations."""
-        lat, times = [], []
-        pend_b, pend_f = collections.deque(), collections.deque()
-        submitted = 0
-        while submitted < k_tickets and len(pend_b) < depth:
-            pend_b.append((submit(), time.perf_counter()))
-            submitted += 1
-        while pend_b:
-            tb, t_sub = pend_b.popleft()
-            parts, _errs, anyerr = ctx.batch_wait(tb)
-            check(anyerr, True)
-            if M == 1:
-                parts = [parts]
-            if capture:  # HIP-event kernel times of this ticket (recorded on the kernels' own streams)
-                times.append(ctx.last_kernel_times())
-            ft = ctx.final_submit_groups(gather(parts))  # the M batches' final checks in one ticket
-            if ft is None:
-                raise SystemExit("final-exponentiation entries exhausted")
-            pend_f.append((ft, t_sub, anyerr))
-            if submitted < k_tickets:
-                pend_b.append((submit(), time.perf_counter()))
-                submitted += 1
-            while pend_f and (len(pend_f) > 1 or not pend_b):
-                ft0, t0, ae = pend_f.popleft()
-                check(ae, all(ctx.final_wait_groups(ft0)))
-                lat.append(time.perf_counter() - t0)
-        return lat, times
-
-    tickets = -(-args.steps // M)
-    steps = tickets * M
-    run(max(1, -(-args.warmup // M)), depth=args.depth)
+    run(max(args.warmup, args.depth), args.depth)
+    allocs0 = ctx.allocation_count()
+    stats_acc.clear()
     barrier()
     t0 = time.perf_counter()
-    lat, ktimes = run(tickets, depth=args.depth, capture=True)
+    lat, ktimes = run(args.steps, args.depth, capture=True)
     barrier()
     elapsed = time.perf_counter() - t0
+    allocs = ctx.allocation_count() - allocs0
     if dist is not None:
         import torch
         te = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
-    # unloaded latency: one batch at a time
-    lat1, _ = run(3, depth=1)
+    # unloaded latency: one package at a time, each alone on the GPU
+    lat1, _ = run(3, 1)
 
     # kernel-level roofline for the dominant kernel, from HIP events recorded on the streams
-    # the kernels ran on during the last timed batch
+    # the kernels ran on, averaged over the timed packages
     opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
-    probe_fp, probe_mad = ctx.probe_fp_mul_rate()
+    probe_fp, _probe_mad = ctx.probe_fp_mul_rate()
     peak_mad = ctx.probe_mad_peak()  # measured v_mad_u64_u32 issue rate of this GPU (k_probe_mad)
-    # per-ticket sum per kernel name (tree levels add up), averaged over the timed tickets
-    agg = {}
-    for ticket_times in ktimes:
-        for name, ms in ticket_times:
+    agg, calls = {}, {}
+    for pkg_times in ktimes:
+        for name, ms in pkg_times:
             agg[name] = agg.get(name, 0.0) + ms / len(ktimes)
-    # pairs per Miller item: the library's LSG_MILLER_K (default 4) sets k_miller_accum's work per set
+            calls[name] = calls.get(name, 0) + 1 / len(ktimes)
     mk = os.environ.get("LSG_MILLER_K", "4")
     accum_key = f"miller_accum{mk}_per_set" if f"miller_accum{mk}_per_set" in opc["stage_fp_muls"] \
         else "miller_accum2_per_set"
-    stage_of = {"k_miller_multi": "miller_multi2_per_set", "k_miller_accum": accum_key,
-                "k_miller_lines": "miller_lines", "k_sig_scale": "sig_scale",
-                "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
-    per_set = {k: v for k, v in agg.items() if k in stage_of}
+    stage_of = {"k_miller_accum": accum_key, "k_miller_lines": "miller_lines", "k_sig_subgroup": "sig_subgroup",
+                "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale", "k_h2c_map": "hash_map"}
+    per_set = {k: v for k, v in agg.items() if k in stage_of and k != "k_h2c_map"}
     dom = max(per_set, key=per_set.get)
-    muls = opc["stage_fp_muls"][stage_of[dom]] * n * M  # one launch covers the M groups' sets
-    achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] * 1e-3) / 1e12
+    muls = opc["stage_fp_muls"][stage_of[dom]] * n_sets  # one launch covers the package's sets
+    achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] / max(calls[dom], 1) * 1e-3) / 1e12
     peak = peak_mad / 1e12
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
             "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
-            "traffic": pmc_traffic(dom, n * M),
-            "kernel_ms": round(agg[dom], 3), "work_per_launch_fp_muls": muls}
-    total_sets = n * world * steps
+            "traffic": pmc_traffic(dom, n_sets),
+            "kernel_ms": round(agg[dom] / max(calls[dom], 1), 3), "work_per_launch_fp_muls": muls}
+    total_sets = n_sets * world * args.steps
     value = total_sets / elapsed
-    # whole-path work per set: the per-set stages with the bucket-MSM signature sums (groups of
-    # n >= 256 sets take the MSM path, smaller ones per-set [r_i] sig_i) plus each group's share
-    # of its per-group stages, plus one G1 addition per extra signer of an aggregate set
-    if n >= 256:
-        per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / n
+    # whole-path work per set: the per-set stages with the bucket-MSM signature sum (groups of
+    # >= 256 sets) plus the package group's share of its per-group stages, plus one G1
+    # addition per extra signer of an aggregate set
+    group = n_sets if args.workload in ("jobs", "adversarial") else (128 if args.workload in ("block", "gossip") else 1)
+    if group >= 256:
+        per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / group
     else:
-        per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / n
-    # the whole-path counts price the Miller stage at K = 2; credit only the work K actually does
+        per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / group
     per_set_muls += opc["stage_fp_muls"][accum_key] - opc["stage_fp_muls"]["miller_accum2_per_set"]
-    pks_per_set = sum(len(p) for p, _, _ in sets) / len(sets)
-    per_set_muls += (pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
+    per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            if block:  # the CPU path gets the aggregated keys for free (favours the CPU)
-                cpu = cpu_baseline_oracle([([ctx.aggregate_pubkeys(p)[0]], m, sg) for p, m, sg in sets[:256]])
-                cpu["sample"] += "; pubkey aggregation (main thread in the reference) excluded"
-            else:
+            if args.workload in ("jobs", "adversarial", "gossip"):
+                sets = [s for job, _ in wl.packages[0][0] for s in job]
+                if args.workload == "adversarial":
+                    sets = [s for (job, _), e in zip(wl.packages[0][0], wl.packages[0][1]) if e == (1, 0) for s in job]
                 cpu = cpu_baseline_oracle(sets)
+            else:  # aggregate workloads: the CPU path gets the aggregated keys for free (favours the CPU)
+                from lodestar_amd._native import PkIndices  # noqa: F401
+                sub = [s for job, _ in wl.packages[0][0] for s in job][:256]
+                cpu = cpu_baseline_oracle([([ctx.aggregate_pubkeys(p)[0]], m, sg) for p, m, sg in sub])
+                cpu["sample"] += "; pubkey aggregation (main thread in the reference) excluded"
+        desc = {
+            "jobs": "firehose (SURVEY 8d config D): one mainnet slot of unaggregated attestations per GPU -- "
+                    "single-pubkey gossip sets, one batchable job each, through lsg_submit_jobs/lsg_wait_jobs",
+            "adversarial": "adversarial (SURVEY 8d config E): the firehose package with 1% corrupted sets, "
+                           "batch failure + chunk/per-job retry, every verdict checked",
+            "block": "block-body (SURVEY 8d config C): 32 blocks per package, each a non-batchable job of 128 "
+                     "aggregate sets of 440-460 signers named by index into the device pubkey table",
+            "sync": "sync-committee contributions (SURVEY 8d config B): 64 batchable jobs per package, each one "
+                    "512-signer aggregate set (keys by index)",
+            "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
+        }[args.workload]
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": steps,
-            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": ({"workload": "block-body (SURVEY 8d config C): aggregate-attestation sets of 440-460 "
-                                    "signers named by index into the device pubkey table, distinct messages, one "
-                                    "RLC multi-pairing per block",
-                        "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
-                        "pubkeys_per_set": round(pks_per_set, 1), "parallelism": f"shard{world}"} if block else
-                       {"workload": "firehose-32k shard (SURVEY 8d config D): single-pubkey gossip sets, RLC batch "
-                                    "per GPU, RCCL all-gather of Fp12 partials, one final exponentiation",
-                        "sets_per_gpu": n, "global_batch": n * world, "keys": 1024,
-                        "parallelism": f"shard{world}"}),
+            "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+            "warmup": max(args.warmup, args.depth), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (interop keys, GPU-signed; fresh OS-CSPRNG randomizers per package)",
+            "config": {"workload": desc, "sets_per_step_per_gpu": n_sets, "global_batch": n_sets * world,
+                       "jobs_per_package": len(wl.packages[0][0]), "pubkeys_per_set": round(wl.pks_per_set, 1),
+                       "keys": N_KEYS, "parallelism": f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
-            "pipeline_depth": args.depth, "batches_per_submission": M,
+            "pipeline_depth": args.depth, "distinct_packages": len(prepared),
+            "allocations_in_timed_region": allocs,
+            "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},
@@ -323,7 +442,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    staged.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

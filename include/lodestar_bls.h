@@ -18,9 +18,12 @@
  *   lsg_*signing_roots     <- util/signingRoot.ts:7-13 computeSigningRoot
  *   lsg_submit_jobs /      <- the asynchronous lsg_submit / lsg_wait pair of SURVEY.md 8b:
  *   lsg_wait_jobs             one BlsWorkReq[] package in flight per pipeline slot
- *   lsg_batch_* /          <- the per-GPU half of verifyMultipleSignatures for the
- *   lsg_final_*               node-sharded path: Miller-loop product
- *                             per shard, all-gathered by the caller, one final exponentiation
+ *   lsg_init_devices       <- the node-wide pool (chain.ts:195-198, multithread/poolSize.ts:7):
+ *                             one context over every GPU of the node
+ *   lsg_jobs_partial /     <- the per-GPU half of a package for one-process-per-GPU hosts
+ *   lsg_wait_jobs_node        (SURVEY.md 8e): Miller-loop product of the package group,
+ *   lsg_batch_partial /       all-gathered by the caller, one final exponentiation
+ *   lsg_final_*               (lsg_final_*), then the verdicts resolved with it
  *
  * Plain pointers and sizes only; every call returns an int status (LSG_OK = 0) and never
  * throws.  Verdicts and error codes follow blst's numbering (BLST_* below).  All compute
@@ -45,6 +48,7 @@ extern "C" {
 #define LSG_ERR_NOMEM 4
 #define LSG_ERR_CLOSED 5
 #define LSG_ERR_BUSY 6 /* every pipeline slot holds an outstanding ticket (canAcceptWork false) */
+#define LSG_ERR_ENTROPY 7 /* the OS CSPRNG (getrandom) failed: no RLC randomizers, nothing verified */
 
 /* ---- blst error codes (blst.h BLST_ERROR) + @chainsafe/blst's size error */
 #define LSG_BLST_SUCCESS 0
@@ -75,8 +79,7 @@ extern "C" {
 #define LSG_JOB_PRIORITY 2u
 
 typedef struct lsg_ctx lsg_ctx;
-typedef struct lsg_staged lsg_staged; /* device-resident package of sets */
-typedef uint64_t lsg_ticket;          /* handle of an in-flight submission */
+typedef uint64_t lsg_ticket; /* handle of an in-flight submission */
 
 /* One signature set (ISignatureSet, state-transition/src/util/signatureSets.ts:10-22).
  * Pubkeys are the set's n_pks keys back to back, each pk_len bytes (48 compressed or
@@ -112,27 +115,59 @@ typedef struct {
   uint32_t batch_sigs_success;
   uint64_t start_ns;
   uint64_t end_ns;
-  uint32_t n_final_exps; /* final exponentiations launched (batches + retries) */
+  uint32_t n_final_exps; /* final exponentiations run (package, chunk and job groups; node check) */
   uint32_t reserved;
 } lsg_stats;
 
-/* Context owning one device's streams and buffers.  device_ordinal < 0 -> device 0.
- * A context has two pipeline slots (each: a main and a side HIP stream plus its own
- * device state) and a final-exponentiation stream, so up to two packages are in flight
- * while earlier final exponentiations finish.  Calls are serialised by an internal mutex. */
+/* A context over one or more devices.  Per device it owns 16 pipeline slots (each: a main
+ * and a side HIP stream plus its own device buffers; lsg_pipeline_slots), and device 0 owns
+ * 64 final-exponentiation entries on 8 streams (lsg_final_*).  Calls are serialised by an
+ * internal mutex; waits block without holding it.
+ *   lsg_init(d)              one device (d < 0: device 0)
+ *   lsg_init_devices(ids, n) the node's GPUs (chain.ts:195-198 builds ONE verifier per node;
+ *                            its pool spans every core, multithread/poolSize.ts:7).  A package
+ *                            is split into whole jobs by cumulative set count; each device
+ *                            reduces its share to one Fp12 partial, the partials are
+ *                            all-gathered over RCCL (communicators owned by the context) and
+ *                            one final exponentiation on device 0 checks the node; on failure
+ *                            every device localises with its own check.
+ *                            Duplicate ids (tests) exchange by device copies instead. */
 int lsg_init(int device_ordinal, lsg_ctx** out);
+int lsg_init_devices(const int* device_ids, int n_devices, lsg_ctx** out);
 int lsg_destroy(lsg_ctx* ctx);
+int lsg_device_count(lsg_ctx* ctx, int32_t* n);
 const char* lsg_last_error(lsg_ctx* ctx);
 int lsg_device_name(lsg_ctx* ctx, char* buf, size_t len);
+/* Preallocate every device and pinned buffer of the first n_slots pipeline slots (0 = all) of
+ * every device for packages of up to max_sets sets, max_pks keys and max_msg_bytes message
+ * bytes, so that submissions within those bounds allocate nothing. */
+int lsg_reserve(lsg_ctx* ctx, size_t max_sets, size_t max_pks, size_t max_msg_bytes, int32_t n_slots);
+/* Device + pinned allocations made by this process so far (steady-state checks). */
+int lsg_allocation_count(lsg_ctx* ctx, uint64_t* n);
 
 /* worker.ts:30-106 for one work package (BlsWorkReq[] -> BlsWorkResult), asynchronous:
- * submit copies the jobs into pinned staging memory, launches every stage and returns a
- * ticket (LSG_ERR_BUSY when both slots are outstanding: back-pressure as in
- * canAcceptWork, multithread/index.ts:143-149); wait blocks on that ticket, applies the
- * batch/retry verdict rules and runs the per-job retries.  seed != 0 makes the RLC
- * randomizers deterministic (tests); seed == 0 draws them from the OS CSPRNG. */
+ * submit copies the jobs into pinned staging memory, draws the RLC randomizers, launches every
+ * stage and returns a ticket (LSG_ERR_BUSY when all slots are outstanding: back-pressure as in
+ * canAcceptWork, multithread/index.ts:143-149).  All batchable sets of the package form ONE
+ * RLC group (one final exponentiation); only if it fails are the reference's 16-job chunks
+ * and then the jobs of failing chunks checked (on the resident per-set values), so verdicts
+ * and the batch_retries / batch_sigs_success counters are those of worker.ts.  wait blocks on
+ * the ticket and applies those rules.  seed != 0 makes the randomizers deterministic (tests);
+ * seed == 0 draws them from getrandom (LSG_ERR_ENTROPY if that fails). */
 int lsg_submit_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket);
 int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n_jobs] */, lsg_stats* stats);
+/* One process per GPU (SURVEY.md 8e over torch.distributed / any host collective), on a
+ * single-device context: lsg_jobs_partial blocks until the package group's Miller product is
+ * ready and writes it (576 bytes, canonical; the identity when the package has no batchable
+ * set; *has_batch says which).  The caller all-gathers the partials, checks their product with
+ * lsg_final_*, and resolves the ticket with that node verdict (1 passed, 0 failed: this GPU's
+ * own package check then localises).  lsg_wait_jobs == lsg_wait_jobs_node(..., -1, ...). */
+int lsg_jobs_partial(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* has_batch);
+int lsg_wait_jobs_node(lsg_ctx* ctx, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results,
+                       lsg_stats* stats);
+/* Whole-job assignment of lsg_init_devices (host only, no device needed): owner[j] = device of
+ * job j = floor(sets before j * n_devices / total sets). */
+int lsg_assign_jobs(const uint32_t* job_sets, size_t n_jobs, int32_t n_devices, int32_t* owner);
 /* Number of pipeline slots (packages that may be outstanding at once): the back-pressure
  * bound of canAcceptWork (multithread/index.ts:143-149 workersBusy < poolSize). */
 int lsg_pipeline_slots(lsg_ctx* ctx, int32_t* n);
@@ -159,26 +194,13 @@ int lsg_hash_to_g2(lsg_ctx* ctx, const uint8_t* msgs, uint32_t msg_len, size_t n
  * out192[i] = uncompressed affine point, err[i] = BLST_* (0 = ok). */
 int lsg_sig_decode(lsg_ctx* ctx, const uint8_t* sigs, uint32_t sig_len, size_t n, uint8_t* out192, int32_t* err);
 
-/* Sharded batch: one shard's sets -> its un-exponentiated Miller product
- * (576 bytes: 12 canonical big-endian Fp in tower order) over the sets that decode, and
- * per-set error codes.  *any_error != 0 means the shard cannot be batched (the caller
- * falls back to per-job verification). */
+/* One shard's sets -> its un-exponentiated Miller product (576 bytes: 12 canonical big-endian
+ * Fp in tower order) over the sets that decode, and per-set error codes (synchronous;
+ * single-device contexts).  *any_error != 0 means the shard cannot be batched as a whole. */
 int lsg_batch_partial(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
                       int32_t* set_err, int32_t* any_error);
-/* The same split for pipelining: stage copies a package (and its randomizers) into device
- * memory once; submit runs the kernels on the resident package (which must outlive the
- * ticket) and wait returns the partial.  The benchmark times submit..wait only. */
-int lsg_stage(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_staged** out);
-int lsg_staged_free(lsg_ctx* ctx, lsg_staged* staged);
-int lsg_batch_submit(lsg_ctx* ctx, const lsg_staged* staged, lsg_ticket* ticket);
-int lsg_batch_wait(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* set_err, int32_t* any_error);
-/* Several RLC batches in one submission: groups of group_size consecutive sets (the last may
- * be shorter; 0 = one group) each get their own Miller partial, so the matching
- * lsg_batch_wait writes ceil(n_sets / group_size) x 576 bytes.  One launch then carries the
- * per-set work of every group, which keeps more waves in flight than one group per ticket. */
-int lsg_batch_submit_groups(lsg_ctx* ctx, const lsg_staged* staged, size_t group_size, lsg_ticket* ticket);
 /* prod(partials) -> final exponentiation on the GPU -> *valid = (result == 1).  The
- * submit/wait pair runs on the context's final stream, overlapping later batches. */
+ * submit/wait pair runs on device 0's final-exponentiation entries, overlapping packages. */
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
 int lsg_final_submit(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket);
 int lsg_final_wait(lsg_ctx* ctx, lsg_ticket ticket, int32_t* valid);

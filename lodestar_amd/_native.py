@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("LSG_LIB", os.path.join(HERE, "liblodestar_bls.so"))  
 LSG_OK = 0
 LSG_ERR_NO_DEVICE = 2
 LSG_ERR_BUSY = 6
+LSG_ERR_ENTROPY = 7
 
 LSG_INVALID = 0
 LSG_VALID = 1
@@ -88,11 +89,12 @@ _lib = None
 _lib_lock = threading.Lock()
 
 EXPORTS = [
-    "lsg_init", "lsg_destroy", "lsg_last_error", "lsg_device_name", "lsg_verify_jobs", "lsg_verify_sets",
+    "lsg_init", "lsg_init_devices", "lsg_destroy", "lsg_device_count", "lsg_last_error", "lsg_device_name",
+    "lsg_reserve", "lsg_allocation_count", "lsg_verify_jobs", "lsg_verify_sets",
     "lsg_aggregate_pubkeys", "lsg_hash_to_g2", "lsg_sig_decode", "lsg_batch_partial", "lsg_final_verify",
     "lsg_probe_fp_mul_rate", "lsg_last_kernel_times", "lsg_sign", "lsg_sk_to_pk",
-    "lsg_submit_jobs", "lsg_wait_jobs", "lsg_poll", "lsg_stage", "lsg_staged_free", "lsg_batch_submit",
-    "lsg_batch_wait", "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_batch_submit_groups", "lsg_probe_mad_peak",
+    "lsg_submit_jobs", "lsg_wait_jobs", "lsg_wait_jobs_node", "lsg_jobs_partial", "lsg_assign_jobs", "lsg_poll",
+    "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_probe_mad_peak",
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
     "lsg_signing_roots", "lsg_attestation_signing_roots",
@@ -111,6 +113,13 @@ def load_library(path=LIB_PATH):
         vp, u32, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_size_t
         pi32 = ctypes.POINTER(ctypes.c_int32)
         lib.lsg_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        lib.lsg_init_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]
+        lib.lsg_device_count.argtypes = [vp, pi32]
+        lib.lsg_reserve.argtypes = [vp, sz, sz, sz, i32]
+        lib.lsg_allocation_count.argtypes = [vp, ctypes.POINTER(u64)]
+        lib.lsg_wait_jobs_node.argtypes = [vp, u64, i32, ctypes.POINTER(LsgJobResult), ctypes.POINTER(LsgStats)]
+        lib.lsg_jobs_partial.argtypes = [vp, u64, ctypes.c_char_p, pi32]
+        lib.lsg_assign_jobs.argtypes = [ctypes.POINTER(u32), sz, i32, pi32]
         lib.lsg_destroy.argtypes = [vp]
         lib.lsg_last_error.argtypes = [vp]
         lib.lsg_last_error.restype = ctypes.c_char_p
@@ -132,10 +141,6 @@ def load_library(path=LIB_PATH):
         lib.lsg_submit_jobs.argtypes = [vp, ctypes.POINTER(LsgJob), sz, u64, pu64]
         lib.lsg_wait_jobs.argtypes = [vp, u64, ctypes.POINTER(LsgJobResult), ctypes.POINTER(LsgStats)]
         lib.lsg_poll.argtypes = [vp, u64, pi32]
-        lib.lsg_stage.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.POINTER(vp)]
-        lib.lsg_staged_free.argtypes = [vp, vp]
-        lib.lsg_batch_submit.argtypes = [vp, vp, pu64]
-        lib.lsg_batch_submit_groups.argtypes = [vp, vp, sz, pu64]
         lib.lsg_pubkey_table_set.argtypes = [vp, sz, ctypes.c_char_p, u32, sz, pi32]
         lib.lsg_pubkey_table_size.argtypes = [vp, ctypes.POINTER(sz)]
         lib.lsg_final_submit_groups.argtypes = [vp, ctypes.c_char_p, sz, sz, pu64]
@@ -145,7 +150,6 @@ def load_library(path=LIB_PATH):
         lib.lsg_attestation_signing_roots.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, u32, ctypes.c_char_p]
         lib.lsg_aggregate_signatures.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(u32), sz,
                                                  ctypes.c_char_p, pi32]
-        lib.lsg_batch_wait.argtypes = [vp, u64, ctypes.c_char_p, pi32, pi32]
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
         lib.lsg_pipeline_slots.argtypes = [vp, pi32]
@@ -187,17 +191,118 @@ class SetBuffer:
         self.n = len(sets)
 
 
-class Context:
-    """One device context (lsg_ctx).  Raises NativeUnavailable without a gfx950 GPU."""
+def assign_jobs(job_sizes, n_devices):
+    """lsg_assign_jobs (host only): the device of every job for lsg_init_devices."""
+    lib = load_library()
+    n = len(job_sizes)
+    sizes = (ctypes.c_uint32 * max(n, 1))(*job_sizes)
+    owner = (ctypes.c_int32 * max(n, 1))()
+    rc = lib.lsg_assign_jobs(sizes, n, int(n_devices), owner)
+    if rc != LSG_OK:
+        raise ValueError(f"lsg_assign_jobs failed ({rc})")
+    return list(owner[:n])
 
-    def __init__(self, device=0):
+
+class PreparedJobs:
+    """A package of jobs laid out once as lsg_job / lsg_set arrays (numpy-filled), so that it
+    can be submitted repeatedly without per-set Python work: every lsg_submit_jobs still copies
+    all its bytes from host memory and draws fresh randomizers.  jobs: list of (sets, flags),
+    sets = list of (pks, msg, sig) as for Context.verify_jobs."""
+
+    def __init__(self, jobs):
+        import numpy as np
+        flat = [st for sets, _ in jobs for st in sets]
+        n = len(flat)
+        pk_parts, pk_len, n_pks = [], np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint32)
+        for i, (pks, _m, _s) in enumerate(flat):
+            if isinstance(pks, PkIndices):
+                pk_len[i], b = LSG_PK_INDEX, pks.tobytes()
+            else:
+                pk_len[i] = len(pks[0]) if pks else 96
+                if any(len(p) != pk_len[i] for p in pks):
+                    raise ValueError("all pubkeys of one set must share one encoding length")
+                b = b"".join(pks)
+            n_pks[i] = len(pks)
+            pk_parts.append(b)
+
+        def pack(parts):
+            lens = np.array([len(p) for p in parts] or [0], np.uint64)
+            offs = np.zeros_like(lens)
+            if len(parts) > 1:
+                offs[1:] = np.cumsum(lens)[:-1]
+            buf = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8).copy()
+            return buf, offs, lens
+
+        self._pk, pk_off, _ = pack(pk_parts)
+        self._msg, msg_off, msg_len = pack([m for _, m, _ in flat])
+        self._sig, sig_off, sig_len = pack([s for _, _, s in flat])
+        self.sets = (LsgSet * max(n, 1))()
+        dt = np.dtype({"names": ["pks", "pk_len", "n_pks", "msg", "msg_len", "sig", "sig_len"],
+                       "formats": [np.uint64, np.uint32, np.uint32, np.uint64, np.uint32, np.uint64, np.uint32],
+                       "offsets": [LsgSet.pks.offset, LsgSet.pk_len.offset, LsgSet.n_pks.offset, LsgSet.msg.offset,
+                                   LsgSet.msg_len.offset, LsgSet.sig.offset, LsgSet.sig_len.offset],
+                       "itemsize": ctypes.sizeof(LsgSet)})
+        v = np.frombuffer(self.sets, dtype=dt)
+        if n:
+            v["pks"][:n] = np.where(n_pks[:n] > 0, self._pk.ctypes.data + pk_off[:n], 0)
+            v["pk_len"][:n] = pk_len[:n]
+            v["n_pks"][:n] = n_pks[:n]
+            v["msg"][:n] = np.where(msg_len[:n] > 0, self._msg.ctypes.data + msg_off[:n], 0)
+            v["msg_len"][:n] = msg_len[:n]
+            v["sig"][:n] = np.where(sig_len[:n] > 0, self._sig.ctypes.data + sig_off[:n], 0)
+            v["sig_len"][:n] = sig_len[:n]
+        self.n_jobs = len(jobs)
+        self.n_sets = n
+        self.jobs = (LsgJob * max(len(jobs), 1))()
+        jd = np.dtype({"names": ["sets", "n_sets", "flags"], "formats": [np.uint64, np.uint32, np.uint32],
+                       "offsets": [LsgJob.sets.offset, LsgJob.n_sets.offset, LsgJob.flags.offset],
+                       "itemsize": ctypes.sizeof(LsgJob)})
+        jv = np.frombuffer(self.jobs, dtype=jd)
+        counts = np.array([len(sets) for sets, _ in jobs] or [0], np.uint64)
+        firsts = np.zeros_like(counts)
+        if len(jobs) > 1:
+            firsts[1:] = np.cumsum(counts)[:-1]
+        if jobs:
+            jv["sets"][:len(jobs)] = ctypes.addressof(self.sets) + firsts * ctypes.sizeof(LsgSet)
+            jv["n_sets"][:len(jobs)] = counts
+            jv["flags"][:len(jobs)] = [f for _, f in jobs]
+
+
+class Context:
+    """A device context (lsg_ctx) over `device`, or over the list `devices` (lsg_init_devices).
+    Raises NativeUnavailable without a gfx950 GPU."""
+
+    def __init__(self, device=0, devices=None):
         self.lib = load_library()
         h = ctypes.c_void_p()
-        rc = self.lib.lsg_init(int(device), ctypes.byref(h))
+        if devices is None:
+            rc = self.lib.lsg_init(int(device), ctypes.byref(h))
+        else:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            rc = self.lib.lsg_init_devices(ids, len(devices), ctypes.byref(h))
         if rc != LSG_OK:
-            raise NativeUnavailable(f"lsg_init({device}) failed with status {rc} (no gfx950 device?)")
+            raise NativeUnavailable(f"lsg_init({devices if devices is not None else device}) failed with status {rc} "
+                                    f"(no gfx950 device?)")
         self.h = h
-        self.device = device
+        self.device = device if devices is None else devices[0]
+        self.devices = [self.device] if devices is None else list(devices)
+
+    def reserve(self, max_sets, max_pks=None, max_msg_bytes=None, n_slots=0):
+        """lsg_reserve: preallocate the first n_slots pipeline slots (0 = all) for packages of up
+        to max_sets sets (so that steady-state submissions allocate nothing)."""
+        max_pks = max_sets if max_pks is None else max_pks
+        max_msg_bytes = 32 * max_sets if max_msg_bytes is None else max_msg_bytes
+        self._check(self.lib.lsg_reserve(self.h, max_sets, max_pks, max_msg_bytes, n_slots), "lsg_reserve")
+
+    def allocation_count(self):
+        v = ctypes.c_uint64()
+        self._check(self.lib.lsg_allocation_count(self.h, ctypes.byref(v)), "lsg_allocation_count")
+        return v.value
+
+    def device_count(self):
+        v = ctypes.c_int32()
+        self._check(self.lib.lsg_device_count(self.h, ctypes.byref(v)), "lsg_device_count")
+        return v.value
 
     def close(self):
         if getattr(self, "h", None):
@@ -219,46 +324,53 @@ class Context:
         self._check(self.lib.lsg_device_name(self.h, b, 256), "lsg_device_name")
         return b.value.decode()
 
-    @staticmethod
-    def _job_array(jobs):
-        bufs = [SetBuffer(sets) for sets, _ in jobs]
-        arr = (LsgJob * max(len(jobs), 1))()
-        for i, ((sets, flags), b) in enumerate(zip(jobs, bufs)):
-            arr[i].sets = b.arr
-            arr[i].n_sets = b.n
-            arr[i].flags = flags
-        return arr, bufs
-
     def verify_jobs(self, jobs, seed=0):
-        """jobs: list of (sets, flags) with sets = list of (pks, msg, sig).
+        """jobs: list of (sets, flags) with sets = list of (pks, msg, sig), or PreparedJobs.
         Returns (results list of (status, err_code), stats dict)."""
-        arr, _bufs = self._job_array(jobs)
-        res = (LsgJobResult * max(len(jobs), 1))()
-        st = LsgStats()
-        self._check(self.lib.lsg_verify_jobs(self.h, arr, len(jobs), seed, res, ctypes.byref(st)), "lsg_verify_jobs")
-        out = [(res[i].status, res[i].err_code) for i in range(len(jobs))]
-        stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
-        return out, stats
+        t = self.submit_jobs(jobs, seed=seed)
+        if t is None:
+            raise RuntimeError("lsg_submit_jobs: every pipeline slot is busy")
+        return self.wait_jobs(t)
 
     def submit_jobs(self, jobs, seed=0):
-        """Asynchronous verify_jobs: returns a ticket for wait_jobs, or None when both
-        pipeline slots are busy (LSG_ERR_BUSY).  The inputs are copied before returning."""
-        arr, _bufs = self._job_array(jobs)
+        """Asynchronous verify_jobs: returns a ticket for wait_jobs, or None when every
+        pipeline slot is busy (LSG_ERR_BUSY).  The inputs are copied before returning."""
+        p = jobs if isinstance(jobs, PreparedJobs) else PreparedJobs(jobs)
         t = ctypes.c_uint64()
-        rc = self.lib.lsg_submit_jobs(self.h, arr, len(jobs), seed, ctypes.byref(t))
+        rc = self.lib.lsg_submit_jobs(self.h, p.jobs, p.n_jobs, seed, ctypes.byref(t))
         if rc == LSG_ERR_BUSY:
             return None
         self._check(rc, "lsg_submit_jobs")
-        return (t.value, len(jobs))
+        return (t.value, p.n_jobs)
 
-    def wait_jobs(self, ticket):
-        t, n = ticket
-        res = (LsgJobResult * max(n, 1))()
-        st = LsgStats()
-        self._check(self.lib.lsg_wait_jobs(self.h, t, res, ctypes.byref(st)), "lsg_wait_jobs")
+    @staticmethod
+    def _results(res, st, n):
         out = [(res[i].status, res[i].err_code) for i in range(n)]
         stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
         return out, stats
+
+    def wait_jobs(self, ticket, raw=False):
+        """-> (per-job (status, err_code), stats); raw=True returns the ctypes result array."""
+        return self.wait_jobs_node(ticket, -1, raw=raw)
+
+    def wait_jobs_node(self, ticket, node_valid, raw=False):
+        """lsg_wait_jobs_node: resolve a ticket with the node verdict of the all-gathered
+        partials (1 passed, 0 failed; -1 = this GPU's own check, i.e. wait_jobs)."""
+        t, n = ticket
+        res = (LsgJobResult * max(n, 1))()
+        st = LsgStats()
+        self._check(self.lib.lsg_wait_jobs_node(self.h, t, int(node_valid), res, ctypes.byref(st)),
+                    "lsg_wait_jobs_node")
+        if raw:
+            return res, {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
+        return self._results(res, st, n)
+
+    def jobs_partial(self, ticket):
+        """lsg_jobs_partial: (576-byte Miller product of the package group, has_batch)."""
+        out = ctypes.create_string_buffer(576)
+        hb = ctypes.c_int32()
+        self._check(self.lib.lsg_jobs_partial(self.h, ticket[0], out, ctypes.byref(hb)), "lsg_jobs_partial")
+        return out.raw, bool(hb.value)
 
     def probe_mad_peak(self):
         v = ctypes.c_double()
@@ -388,36 +500,6 @@ class Context:
                     "lsg_batch_partial")
         return out.raw, [errs[i] for i in range(b.n)], bool(anyerr.value)
 
-    def stage(self, sets, seed=0):
-        """Copy a package into device memory once (lsg_stage); returns a Staged handle."""
-        b = SetBuffer(sets)
-        h = ctypes.c_void_p()
-        self._check(self.lib.lsg_stage(self.h, b.arr, b.n, seed, ctypes.byref(h)), "lsg_stage")
-        return Staged(self, h, b.n)
-
-    def batch_submit(self, staged, group_size=0):
-        """Submit a staged package; group_size > 0 splits it into RLC groups of that many
-        consecutive sets, each with its own partial.  None when every slot is busy."""
-        t = ctypes.c_uint64()
-        rc = self.lib.lsg_batch_submit_groups(self.h, staged.h, int(group_size), ctypes.byref(t))
-        if rc == LSG_ERR_BUSY:
-            return None
-        self._check(rc, "lsg_batch_submit_groups")
-        ng = 1 if group_size <= 0 or group_size >= staged.n else -(-staged.n // group_size)
-        return (t.value, staged.n, ng)
-
-    def batch_wait(self, ticket):
-        """-> (partial 576 bytes, per-set error codes, any_error); for a grouped submission the
-        first element is the list of the groups' partials"""
-        t, n, ng = ticket
-        out = ctypes.create_string_buffer(576 * ng)
-        errs = (ctypes.c_int32 * max(n, 1))()
-        anyerr = ctypes.c_int32()
-        self._check(self.lib.lsg_batch_wait(self.h, t, out, errs, ctypes.byref(anyerr)), "lsg_batch_wait")
-        raw = out.raw
-        parts = raw if ng == 1 else [raw[576 * g:576 * g + 576] for g in range(ng)]
-        return parts, [errs[i] for i in range(n)], bool(anyerr.value)
-
     def final_verify(self, partials):
         v = ctypes.c_int32()
         self._check(self.lib.lsg_final_verify(self.h, b"".join(partials), len(partials), ctypes.byref(v)),
@@ -486,15 +568,3 @@ class Context:
         ms = (ctypes.c_double * max_entries)()
         n = self.lib.lsg_last_kernel_times(self.h, names, ms, max_entries)
         return [(names[i].decode(), ms[i]) for i in range(n)]
-
-
-class Staged:
-    """A device-resident package (lsg_staged); must outlive the tickets that use it."""
-
-    def __init__(self, ctx, h, n):
-        self.ctx, self.h, self.n = ctx, h, n
-
-    def free(self):
-        if self.h:
-            self.ctx._check(self.ctx.lib.lsg_staged_free(self.ctx.h, self.h), "lsg_staged_free")
-            self.h = None

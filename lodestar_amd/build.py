@@ -12,9 +12,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
-SOURCES = ["lsg_bls.hip", "lsg_serial.hip"]
+# kernel translation units compile in parallel; lsg_host.hip is the orchestration + C ABI
+SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip", "lsg_k_reduce.hip", "lsg_serial.hip",
+           "lsg_host.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
-           "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_quad.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp", "lsg_serial.h"]
+           "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp",
+           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h"]
+OBJ = os.path.join(HERE, "_obj")
 
 
 def hipcc():
@@ -24,33 +28,66 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def _deps():
+    return [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(ROOT, "include", "lodestar_bls.h"),
+                                                       os.path.abspath(__file__)]
+
+
 def needs_rebuild():
     if not os.path.exists(OUT):
         return True
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "lodestar_bls.h"),
-                                                                  os.path.abspath(__file__)]
+    deps = [os.path.join(CSRC, f) for f in SOURCES] + _deps()
     return max(os.path.getmtime(d) for d in deps if os.path.exists(d)) > os.path.getmtime(OUT)
 
 
-def build(force=False, verbose=True):
+# Tower functions (Fp2/Fp6/Fp12, LSG_BIGFN) inlined into the device kernels: as calls they
+# passed Fp12 operands through stack frames (k_miller_accum<2>: 3408 B/lane of scratch,
+# ~477 KB of memory-side traffic per set); inlined, the accumulation has no scratch at all
+# (profiles/r01_pmc_traffic*.json, profiles/r01_inline_ab.txt).  Host builds keep the calls.
+CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DLSG_BIGFN=__host__ __device__ __forceinline__"]
+
+
+def _compile(src, verbose, extra):
+    obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    srcp = os.path.join(CSRC, src)
+    dep_t = max(os.path.getmtime(d) for d in [srcp] + _deps() if os.path.exists(d))
+    if os.path.exists(obj) and os.path.getmtime(obj) >= dep_t and not extra:
+        return obj
+    cmd = [hipcc()] + CFLAGS + extra + ["-I", CSRC, "-I", os.path.join(ROOT, "include"), "-c", srcp, "-o", obj + ".tmp"]
+    if verbose:
+        print("[lodestar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force=False, verbose=True, extra=None, out=None):
+    """Compile the kernel translation units in parallel (hipcc --offload-arch=gfx950) and link
+    liblodestar_bls.so (with RCCL for the multi-device partial exchange).  extra: additional
+    compiler flags (A/B builds, written to `out` instead of the default library)."""
+    from concurrent.futures import ThreadPoolExecutor
     gen = os.path.join(ROOT, "tools", "gen_constants.py")
     const = os.path.join(CSRC, "lsg_constants.hpp")
     if not os.path.exists(const) or os.path.getmtime(gen) > os.path.getmtime(const):
         subprocess.check_call([sys.executable, gen, const])
-    if not force and not needs_rebuild():
+    extra = list(extra or [])
+    out = out or OUT
+    if not force and not extra and out == OUT and not needs_rebuild():
         return OUT
-    # Tower functions (Fp2/Fp6/Fp12, LSG_BIGFN) inlined into the device kernels: as calls they
-    # passed Fp12 operands through stack frames (k_miller_accum<2>: 3408 B/lane of scratch,
-    # ~477 KB of memory-side traffic per set); inlined, the accumulation has no scratch at all
-    # (profiles/r01_pmc_traffic*.json, profiles/r01_inline_ab.txt).  Host builds keep the calls.
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-DLSG_BIGFN=__host__ __device__ __forceinline__", "-I", CSRC,
-           "-I", os.path.join(ROOT, "include")] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
+    os.makedirs(OBJ, exist_ok=True)
+    if force:
+        for f in os.listdir(OBJ):
+            os.remove(os.path.join(OBJ, f))
+    jobs = int(os.environ.get("LSG_BUILD_JOBS", str(min(8, os.cpu_count() or 4))))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose, extra), SOURCES))
+    cmd = [hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared"] + objs + ["-L/opt/rocm/lib", "-lrccl",
+                                                                           "-Wl,-rpath,/opt/rocm/lib", "-o", out + ".tmp"]
     if verbose:
         print("[lodestar_amd.build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 NAPI_SRC = os.path.join(HERE, "napi", "lsg_napi.c")

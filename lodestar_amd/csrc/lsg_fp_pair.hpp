@@ -27,7 +27,7 @@
 #endif
 #define LSG_GROUP LSG_PAIR_G
 #define LSG_PAIR_MODE 1
-#define LSG_QUAD_MODE 1  // register-lean (narrow-issue) tower formulas, see lsg_tower.hpp
+#define LSG_LEAN_TOWER 1  // register-lean (narrow-issue) tower formulas, see lsg_tower.hpp
 constexpr int LSG_PL = 14 / LSG_GROUP;  // limbs per lane
 constexpr uint32_t LSG_M29 = (1u << 29) - 1;
 

@@ -1,0 +1,2307 @@
+// lsg_host.hip -- host orchestration and the C ABI (include/lodestar_bls.h) of the MI355X
+// BLS12-381 signature-set verifier.  No kernels live here (they are in lsg_k_*.hip and
+// lsg_serial.hip, reached through lsg_launch.h / lsg_serial.h).
+//
+// Reference path replaced (file:line under /root/reference):
+//   packages/beacon-node/src/chain/bls/multithread/worker.ts:30-114  verifyManySignatureSets,
+//       deserializeSet: batch-of-jobs verification with the per-job retry fallback
+//   packages/beacon-node/src/chain/bls/maybeBatch.ts:16-39         RLC batch vs single verify
+//   packages/beacon-node/src/chain/bls/utils.ts:5-26               pubkey aggregation
+//   + the un-vendored @chainsafe/blst@0.2.8 arithmetic underneath.
+//
+// One package (BlsWorkReq[]: the jobs one worker would get) runs as ONE ticket:
+//   phase A (submit, no host synchronisation): every batchable set of the package is one RLC
+//     group (bucket MSM for its signature sum), every non-batchable job its own group; each
+//     group gets its Miller product and one final exponentiation, launched speculatively.
+//   resolve (wait): the reference's verdict rules (worker.ts:51-96).  A passing package
+//     group answers every batchable job at once; only when it fails are the 16-job chunks of
+//     worker.ts (phase B) and then the jobs of failing chunks (phase C) checked, on the
+//     per-set values still resident, so per-job verdicts and the batch_retries /
+//     batch_sigs_success counters are the reference's.
+// Per device a context owns LSG_SLOTS pipeline slots (two streams each, all buffers
+// preallocated by lsg_reserve); several devices share one ticket (whole jobs per device, one
+// all-gather of the 576-byte partials, one node final exponentiation: SURVEY.md 8e).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <errno.h>
+#include <string.h>
+#include <sys/random.h>
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lodestar_bls.h"
+#include "lsg_launch.h"
+#include "lsg_layout.h"
+#include "lsg_serial.h"
+
+using namespace lsgl;
+
+namespace {
+
+const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+const uint32_t DST_POP_LEN = 43;
+constexpr int LSG_SLOTS = 16;      // packages in flight per device
+constexpr int LSG_FINALS = 64;     // final-exponentiation entries in flight (lsg_final_*)
+constexpr int LSG_FE_STREAMS = 8;  // streams the final-exponentiation entries share
+constexpr int LSG_MAX_DEVICES = 16;
+constexpr int LSG_MILLER_KMAX = 4;
+
+uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// OS CSPRNG bytes (getrandom(2)); false if the kernel cannot provide them.  There is no
+// deterministic fallback: predictable RLC multipliers would let forged sets cancel.
+bool os_random(void* buf, size_t len) {
+  uint8_t* p = (uint8_t*)buf;
+  while (len) {
+    ssize_t r = getrandom(p, len, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += r;
+    len -= (size_t)r;
+  }
+  return true;
+}
+
+std::atomic<uint64_t> g_allocs{0};  // device + pinned allocations made (lsg_allocation_count)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+struct HostBuf {  // pinned host memory (async copies)
+  void* p = nullptr;
+  size_t cap = 0;
+};
+struct Timer {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+// chunkifyMaximizeChunkSize (multithread/utils.ts:4-19)
+std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t chunk_count = len / min_per_chunk;
+  if (chunk_count <= 1) {
+    out.push_back({0, len});
+    return out;
+  }
+  size_t per = (len + chunk_count - 1) / chunk_count;
+  for (size_t i = 0; i < len; i += per) out.push_back({i, std::min(len, i + per)});
+  return out;
+}
+
+// ---- segmented-reduction plans (lsgk::seg_reduce): int32 words appended to a slot's plan
+// arena, uploaded once per phase
+struct SegPass {
+  int ips_log2 = 0, n_chunks = 0;
+  size_t chunk_off = 0;  // words into the arena
+  int src = 0;           // 0: the reduction's input, 1/2: tmp buffer A/B
+  int tmp_out = 1;       // tmp buffer (1/2) that negative outputs go to
+};
+struct SegPlan {
+  int op = 0;
+  bool has_idx = false;
+  size_t idx_off = 0;
+  std::vector<SegPass> passes;
+  size_t tmp_items = 0;  // per tmp buffer
+};
+constexpr int SEG_FOLD = 8;  // serial folds per lane pair within one pass
+
+int ips_for(double avg) {
+  int l = 0;
+  while (l < 5 && (double)(2 << l) * 4.0 <= avg) l++;
+  return l;
+}
+
+// Segments s = 0..ns-1: elements [seg_off[s], seg_off[s] + seg_len[s]) of the idx list (at
+// idx_off in the arena; has_idx) or of the input itself; result s goes to dst[dst_base + s].
+SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& seg_off,
+                 const std::vector<int32_t>& seg_len, bool has_idx, size_t idx_off, int32_t dst_base) {
+  SegPlan P;
+  P.op = op;
+  P.has_idx = has_idx;
+  P.idx_off = idx_off;
+  const size_t ns = seg_len.size();
+  if (ns == 0) return P;
+  size_t total = 0;
+  for (int32_t l : seg_len) total += (size_t)l;
+  // pending: (segment, element offset, length, source) still to reduce
+  struct Pend {
+    int32_t seg, off, len;
+  };
+  std::vector<Pend> cur(ns);
+  for (size_t s = 0; s < ns; s++) cur[s] = {(int32_t)s, seg_off[s], seg_len[s]};
+  double avg = (double)total / (double)ns;
+  int src = 0, tmp_out = 1;
+  while (!cur.empty()) {
+    SegPass pass;
+    pass.ips_log2 = ips_for(avg);
+    pass.src = src;
+    pass.tmp_out = tmp_out;
+    const int32_t cap = (int32_t)((1 << pass.ips_log2) * SEG_FOLD);
+    pass.chunk_off = A.size();
+    std::vector<Pend> nxt;
+    int32_t t = 0;
+    size_t nxt_total = 0;
+    for (const Pend& p : cur) {
+      if (p.len <= cap) {
+        A.push_back(p.off);
+        A.push_back(p.len);
+        A.push_back(dst_base + p.seg);
+        pass.n_chunks++;
+      } else {
+        const int32_t first = t;
+        for (int32_t o = 0; o < p.len; o += cap) {
+          A.push_back(p.off + o);
+          A.push_back(std::min(cap, p.len - o));
+          A.push_back(-(t + 1));
+          t++;
+          pass.n_chunks++;
+        }
+        nxt.push_back({p.seg, first, t - first});
+        nxt_total += (size_t)(t - first);
+      }
+    }
+    P.tmp_items = std::max(P.tmp_items, (size_t)t);
+    P.passes.push_back(pass);
+    avg = nxt.empty() ? 1.0 : (double)nxt_total / (double)nxt.size();
+    cur.swap(nxt);
+    src = tmp_out;  // the next pass reads this pass's partial results, contiguously
+    tmp_out = tmp_out == 1 ? 2 : 1;
+  }
+  return P;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- state
+namespace {
+
+enum SlotKind { SLOT_FREE = 0, SLOT_JOBS = 1, SLOT_FINAL = 3 };
+
+struct Dev;
+
+// One RLC group: sets [first, first + len) (a contiguous range: the package group, one
+// non-batchable job, one 16-job chunk or one job).
+struct Grp {
+  size_t first = 0, len = 0;
+  bool msm = false;
+};
+
+// ---- group stages of one phase (no host synchronisation).  Groups with msm sum their
+// signatures by the bucket MSM over the unscaled points in d_rs (MSM groups must come first);
+// the rest sum the scaled points in rs.  Then per group ML(-G1, S_g) on a row, the product
+// with the group's Miller items (fall: items [0, n_items) followed by one slot per group),
+// the canonical product F_g (d_Fb, D2H into h_blob when export), and FE(F_g) into d_verdict.
+struct PhasePlan {
+  std::vector<Grp> groups;
+  size_t n_msm = 0;
+  SegPlan buckets, bits, sums, prod;
+  size_t n_items = 0;   // Miller items of the phase's groups (fall slots 0 .. n_items-1)
+  size_t item_off = 0;  // item_first / item_cnt in the plan arena
+};
+
+struct JobRec {
+  size_t first = 0, count = 0;  // staged set range
+  uint32_t flags = 0;
+};
+
+struct Slot {
+  Dev* d = nullptr;
+  int index = 0;
+  hipStream_t st[2] = {nullptr, nullptr};  // [0] main, [1] side
+  bool own_streams = true;
+  int cur = 0;
+  hipEvent_t ev_in = nullptr, ev_sig = nullptr, ev_grp = nullptr, ev_part = nullptr, ev_done = nullptr,
+             ev_node = nullptr;
+  // inputs (device copies of the pinned staging arena)
+  DevBuf d_sig, d_siglen, d_msg, d_msgoff, d_msglen, d_pk, d_pklen, d_rnd, d_mode, d_dst;
+  HostBuf h_arena;
+  size_t n_sets = 0, n_pks = 0;
+  std::vector<uint32_t> pk_cnt, pk_first;
+  std::vector<uint64_t> rnd;
+  bool single_keys = false;  // every set has exactly one key (key i is set i's)
+  // per-set state
+  DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_rs2, d_fall,
+      d_fall2;
+  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi;
+  DevBuf binv_lv[2], binv_iv[2];
+  DevBuf d_lines;
+  bool rs2_ready = false;
+  // groups
+  DevBuf d_S, d_F, d_verdict, d_Sb, d_fgb, d_Fb, d_bkt, d_bits, d_aux, d_gath, d_nodeF, d_nodeV;
+  DevBuf seg_tmp[3][2];  // reduction scratch per use: [0] pubkeys, [1] signature sums, [2] Fp12 products
+  // plan arena
+  std::vector<int32_t> plan;
+  HostBuf h_plan;
+  DevBuf d_plan;
+  PhasePlan phA;   // phase A: the package group + non-batchable jobs
+  SegPlan pkagg;   // pubkey aggregation of multi-key sets
+  SegPlan phA_node;  // device 0 of a multi-device ticket: product of the gathered partials
+  HostBuf h_mode;  // per-set sig_prep modes of a phase
+  // pinned result mirrors
+  HostBuf h_err, h_pinf, h_pkerr, h_verdict, h_blob, h_nodeV;
+  std::vector<Timer> timers;
+  size_t ntimers = 0;
+  // ticket state
+  int kind = SLOT_FREE;
+  uint64_t serial = 0;
+  std::vector<JobRec> jobs;         // this device's share of the package, caller order
+  std::vector<size_t> job_ids;      // caller job index of jobs[k]
+  std::vector<size_t> batch_order;  // indices into jobs: batchable jobs in staging order
+  size_t nb_sets = 0;               // sets of the batchable jobs (staged first)
+  std::vector<Grp> groups;          // phase-A groups (MSM groups first)
+  int big_g = -1;                   // the package group's index in groups
+  bool chunk_mode = false;          // phase A ran one group per 16-job chunk (LSG_PACKAGE_GROUP=0)
+  std::vector<int> chunk_group;     // chunk mode: per chunk of batch_order, its phase-A group
+  std::vector<int> job_group;       // per job: its phase-A group (non-batchable), else -1
+  std::vector<lsg_job_result> results;
+  lsg_stats stats;
+  bool has_node = false;  // this slot computed the node check (device 0 of a multi-device ticket)
+};
+
+struct Dev {
+  lsg_ctx* c = nullptr;
+  int device = 0;
+  int ord = 0;  // position in the context's device list
+  hipStream_t s_util = nullptr;
+  hipStream_t s_fe[LSG_FE_STREAMS] = {};
+  Slot slots[LSG_SLOTS];
+  Slot finals[LSG_FINALS];
+  Slot util;
+  // validator pubkey table (lsg_pubkey_table_set): projective lane-form keys + validity bytes
+  DevBuf d_pktab, d_pktab_ok;
+  size_t pktab_n = 0, pktab_cap = 0;
+  const Slot* last = nullptr;  // slot whose timers lsg_last_kernel_times reports
+};
+
+}  // namespace
+
+struct lsg_ctx {
+  std::mutex mu;
+  std::string err;
+  int n_dev = 0;
+  Dev* dev[LSG_MAX_DEVICES] = {};
+  bool rccl = false;  // several distinct devices: the partials are all-gathered over RCCL
+  ncclComm_t comm[LSG_MAX_DEVICES] = {};
+  uint64_t next_serial = 1;
+};
+
+namespace {
+
+int fail_c(lsg_ctx* c, const char* what, hipError_t e) {
+  c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return LSG_ERR_DEVICE;
+}
+int fail(Slot* s, const char* what, hipError_t e) { return fail_c(s->d->c, what, e); }
+
+#define LSG_HIP(s, call)                               \
+  do {                                                 \
+    hipError_t _e = (call);                            \
+    if (_e != hipSuccess) return fail((s), #call, _e); \
+  } while (0)
+#define LSG_HIPC(c, call)                                \
+  do {                                                   \
+    hipError_t _e = (call);                              \
+    if (_e != hipSuccess) return fail_c((c), #call, _e); \
+  } while (0)
+#define LSG_RC(call)         \
+  do {                       \
+    int _rc = (call);        \
+    if (_rc) return _rc;     \
+  } while (0)
+
+int ensure(Slot* s, DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 64;
+  if (b.cap >= bytes) return LSG_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)4096);
+  hipError_t e = hipMalloc(&b.p, cap);
+  if (e != hipSuccess) return fail(s, "hipMalloc", e);
+  g_allocs++;
+  b.cap = cap;
+  return LSG_OK;
+}
+
+int ensure_host(Slot* s, HostBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 64;
+  if (b.cap >= bytes) return LSG_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)4096);
+  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(s, "hipHostMalloc", e);
+  g_allocs++;
+  b.cap = cap;
+  return LSG_OK;
+}
+
+void free_dev(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+void free_host(HostBuf& b) {
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+template <class T>
+T* P_(const DevBuf& b) {
+  return (T*)b.p;
+}
+template <class T>
+T* H_(const HostBuf& b) {
+  return (T*)b.p;
+}
+
+inline hipStream_t S_(Slot* s) { return s->st[s->cur]; }
+
+void timer_reset(Slot* s) {
+  s->ntimers = 0;
+  s->cur = 0;
+}
+void timer_begin(Slot* s, const char* name) {
+  if (s->ntimers >= s->timers.size()) {
+    Timer t;
+    (void)hipEventCreate(&t.a);
+    (void)hipEventCreate(&t.b);
+    s->timers.push_back(t);
+  }
+  Timer& t = s->timers[s->ntimers];
+  t.name = name;
+  (void)hipEventRecord(t.a, S_(s));
+}
+void timer_end(Slot* s) {
+  (void)hipEventRecord(s->timers[s->ntimers].b, S_(s));
+  s->ntimers++;
+}
+
+// a launch through lsg_launch.h on the slot's current stream, timed with HIP events
+#define KL(s, name, call)                                 \
+  do {                                                    \
+    timer_begin((s), name);                               \
+    hipError_t _le = (call);                              \
+    timer_end((s));                                       \
+    if (_le != hipSuccess) return fail((s), name, _le);   \
+  } while (0)
+
+// device pointer of arena word `off`
+inline const int32_t* PL(Slot* s, size_t off) { return P_<int32_t>(s->d_plan) + off; }
+
+int slot_create(Dev* d, Slot* s, int index, hipStream_t shared) {
+  s->d = d;
+  s->index = index;
+  if (shared) {
+    s->st[0] = s->st[1] = shared;
+    s->own_streams = false;
+  } else {
+    for (int k = 0; k < 2; k++) LSG_HIP(s, hipStreamCreateWithFlags(&s->st[k], hipStreamNonBlocking));
+  }
+  hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_part, &s->ev_done, &s->ev_node};
+  for (hipEvent_t* e : evs) LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  LSG_RC(ensure(s, s->d_dst, 256));
+  LSG_HIP(s, hipMemcpy(s->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice));
+  return LSG_OK;
+}
+
+void slot_destroy(Slot* s) {
+  if (!s->d) return;
+  for (int k = 0; k < 2; k++)
+    if (s->st[k]) (void)hipStreamSynchronize(s->st[k]);
+  DevBuf* bufs[] = {&s->d_sig,  &s->d_siglen, &s->d_msg,  &s->d_msgoff, &s->d_msglen, &s->d_pk,    &s->d_pklen,
+                    &s->d_rnd,  &s->d_mode,   &s->d_dst,  &s->d_ub,     &s->d_sigaff, &s->d_siginf, &s->d_seterr,
+                    &s->d_pkp,  &s->d_pkerr,  &s->d_agg,  &s->d_P,      &s->d_pinf,   &s->d_H,     &s->d_hinf,
+                    &s->d_rs,   &s->d_rs2,    &s->d_fall, &s->d_fall2,  &s->d_Pp,     &s->d_zP,    &s->d_zPi,
+                    &s->d_U,    &s->d_nrm,    &s->d_nrmi, &s->d_Hp,     &s->d_zN,     &s->d_zNi,   &s->binv_lv[0],
+                    &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
+                    &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
+                    &s->d_nodeF, &s->d_nodeV, &s->d_plan};
+  for (DevBuf* b : bufs) free_dev(*b);
+  for (auto& u : s->seg_tmp)
+    for (DevBuf& b : u) free_dev(b);
+  HostBuf* hb[] = {&s->h_arena, &s->h_err, &s->h_pinf, &s->h_pkerr, &s->h_verdict, &s->h_blob, &s->h_plan, &s->h_nodeV};
+  for (HostBuf* b : hb) free_host(*b);
+  for (Timer& t : s->timers) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  s->timers.clear();
+  hipEvent_t evs[] = {s->ev_in, s->ev_sig, s->ev_grp, s->ev_part, s->ev_done, s->ev_node};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  if (s->own_streams)
+    for (int k = 0; k < 2; k++)
+      if (s->st[k]) (void)hipStreamDestroy(s->st[k]);
+  s->d = nullptr;
+}
+
+// ---- sizes
+int miller_k() {
+  static int k = [] {
+    const char* e = getenv("LSG_MILLER_K");
+    // K=4 since the tower is inlined: 2.45M vs 2.35M sets/s at 12x3 (profiles/r01_inline_ab.txt)
+    int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4) ? v : 4;
+  }();
+  return k;
+}
+
+// Minimum RLC group size for the bucket MSM (env LSG_MSM_MIN_GROUP): below ~150 sets the
+// fixed cost of 2040 buckets and 64 bit sums per group exceeds the per-set scalar
+// multiplications it replaces.
+size_t msm_min_group() {
+  const char* e = getenv("LSG_MSM_MIN_GROUP");
+  const long x = e ? atol(e) : 256;
+  return x < 1 ? (size_t)1 : (size_t)x;
+}
+
+// Phase A as the reference batches it: one RLC group per 16-job chunk instead of one package
+// group (env LSG_PACKAGE_GROUP=0; A/B and the equivalence test of the two modes)
+bool package_group_mode() {
+  const char* e = getenv("LSG_PACKAGE_GROUP");
+  return !(e && atoi(e) == 0);
+}
+
+// inputs for up to n sets / np keys / mb message bytes
+int size_inputs(Slot* s, size_t n, size_t np, size_t mb) {
+  const size_t nn = std::max(n, (size_t)1), pp = std::max(np, (size_t)1);
+  auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
+  const size_t arena = al(192 * nn) + al(4 * nn) * 3 + al(4 * pp) + al(8 * nn) + al(96 * pp) + al(std::max(mb, (size_t)1)) + nn;
+  LSG_RC(ensure_host(s, s->h_arena, arena));
+  LSG_RC(ensure(s, s->d_sig, 192 * nn));
+  LSG_RC(ensure(s, s->d_siglen, 4 * nn));
+  LSG_RC(ensure(s, s->d_msg, std::max(mb, (size_t)1)));
+  LSG_RC(ensure(s, s->d_msgoff, 4 * nn));
+  LSG_RC(ensure(s, s->d_msglen, 4 * nn));
+  LSG_RC(ensure(s, s->d_pk, 96 * pp));
+  LSG_RC(ensure(s, s->d_pklen, 4 * pp));
+  LSG_RC(ensure(s, s->d_rnd, 8 * nn));
+  LSG_RC(ensure(s, s->d_mode, nn));
+  return LSG_OK;
+}
+
+// per-set state and group buffers for n sets / np keys / ng groups (n_msm of them bucket-MSM
+// groups) in any phase
+int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, bool pkg = false) {
+  const size_t nn = std::max(n, (size_t)1), pp = std::max(np, (size_t)1), gg = std::max(ng, (size_t)1);
+  const size_t g_msm = std::max(n_msm, (size_t)1);
+  struct {
+    DevBuf* b;
+    size_t bytes;
+  } dev[] = {{&s->d_ub, 256 * nn},
+             {&s->d_sigaff, 4 * W_G2A * nn},
+             {&s->d_siginf, nn},
+             {&s->d_seterr, 4 * nn},
+             {&s->d_pkp, 4 * W_G1P * pp},
+             {&s->d_pkerr, 4 * pp},
+             {&s->d_agg, 4 * W_G1P * nn},
+             {&s->d_P, 4 * W_G1A * nn},
+             {&s->d_pinf, nn},
+             {&s->d_H, 4 * W_G2A * nn},
+             {&s->d_hinf, nn},
+             {&s->d_rs, 4 * W_G2P * nn},
+             {&s->d_Pp, 4 * W_G1P * nn},
+             {&s->d_zP, 4 * W_FP * nn},
+             {&s->d_zPi, 4 * W_FP * nn},
+             {&s->d_U, 4 * W_H2CU * nn},
+             {&s->d_nrm, 4 * W_FP * 2 * nn},
+             {&s->d_nrmi, 4 * W_FP * 2 * nn},
+             {&s->d_Hp, 4 * W_G2P * nn},
+             {&s->d_zN, 4 * W_FP * nn},
+             {&s->d_zNi, 4 * W_FP * nn},
+             {&s->binv_lv[0], 4 * W_FP * 2 * nn},
+             {&s->binv_iv[0], 4 * W_FP * 2 * nn},
+             {&s->binv_lv[1], 4 * W_FP * nn},
+             {&s->binv_iv[1], 4 * W_FP * nn},
+             {&s->d_S, 4 * W_G2P * gg},
+             {&s->d_F, 4 * W_F12 * gg},
+             {&s->d_verdict, 4 * gg},
+             {&s->d_Sb, (size_t)288 * (MSM_BITS * g_msm + gg)},
+             {&s->d_fgb, 576 * gg},
+             {&s->d_Fb, 576 * gg},
+             {&s->d_bkt, 4 * W_G2P * (size_t)MSM_WINDOWS * MSM_DIGITS * g_msm},
+             {&s->d_bits, 4 * W_G2P * (size_t)MSM_BITS * g_msm},
+             {&s->d_gath, 576 * (LSG_MAX_DEVICES + 2)},  // partials, the identity, the node product
+             {&s->d_nodeF, 4 * W_F12 * (LSG_MAX_DEVICES + 1)},
+             {&s->d_nodeV, 64}};
+  for (auto& x : dev) LSG_RC(ensure(s, *x.b, x.bytes));
+  if (pkg) {  // package slots: Miller lines and items, fallback signature sums
+    LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
+    LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg)));
+    LSG_RC(ensure(s, s->d_fall2, 4 * W_F12 * (nn + gg)));
+    LSG_RC(ensure(s, s->d_rs2, 4 * W_G2P * nn));
+  }
+  LSG_RC(ensure_host(s, s->h_err, 4 * nn));
+  LSG_RC(ensure_host(s, s->h_pinf, nn));
+  LSG_RC(ensure_host(s, s->h_pkerr, 4 * pp));
+  LSG_RC(ensure_host(s, s->h_verdict, 4 * gg));
+  LSG_RC(ensure_host(s, s->h_blob, 576 * gg));
+  LSG_RC(ensure_host(s, s->h_nodeV, 64));
+  return LSG_OK;
+}
+
+// reduction scratch for a plan
+int size_seg(Slot* s, int use, const SegPlan& P) {
+  if (P.tmp_items == 0) return LSG_OK;
+  const size_t W = P.op == 0 ? W_G1P : (P.op == 1 ? W_G2P : W_F12);
+  LSG_RC(ensure(s, s->seg_tmp[use][0], 4 * W * P.tmp_items));
+  return ensure(s, s->seg_tmp[use][1], 4 * W * P.tmp_items);
+}
+
+// upload the plan arena (one copy on the main stream, before ev_in)
+int upload_plan(Slot* s) {
+  const size_t bytes = 4 * std::max(s->plan.size(), (size_t)1);
+  LSG_RC(ensure_host(s, s->h_plan, bytes));
+  LSG_RC(ensure(s, s->d_plan, bytes));
+  if (!s->plan.empty()) {
+    memcpy(s->h_plan.p, s->plan.data(), 4 * s->plan.size());
+    LSG_HIP(s, hipMemcpyAsync(s->d_plan.p, s->h_plan.p, 4 * s->plan.size(), hipMemcpyHostToDevice, s->st[0]));
+  }
+  return LSG_OK;
+}
+
+// run a planned reduction on the current stream; use selects the scratch pair
+int run_seg(Slot* s, int use, const char* name, const SegPlan& P, const uint32_t* src, uint32_t* dst) {
+  LSG_RC(size_seg(s, use, P));
+  uint32_t* tmp[3] = {nullptr, P_<uint32_t>(s->seg_tmp[use][0]), P_<uint32_t>(s->seg_tmp[use][1])};
+  const int32_t* idx = P.has_idx ? PL(s, P.idx_off) : nullptr;
+  for (size_t k = 0; k < P.passes.size(); k++) {
+    const SegPass& q = P.passes[k];
+    const uint32_t* in = q.src == 0 ? src : tmp[q.src];
+    KL(s, name, lsgk::seg_reduce(S_(s), P.op, q.n_chunks, q.ips_log2, PL(s, q.chunk_off), k == 0 ? idx : nullptr, in, dst,
+                                 tmp[q.tmp_out]));
+  }
+  return LSG_OK;
+}
+
+// out[i] = 1 / v[i] (0 for v[i] = 0) for n lane-form Fp values, on the current stream: a
+// product tree up, one inversion at the root, products back down (Montgomery's trick).
+int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, uint32_t* out) {
+  if (n == 0) return LSG_OK;
+  std::vector<size_t> sz{n}, off{0};
+  size_t total = 0;
+  do {
+    size_t m = (sz.back() + 1) / 2;
+    off.push_back(total);
+    sz.push_back(m);
+    total += m;
+  } while (sz.back() > 1);
+  LSG_RC(ensure(s, s->binv_lv[ws], 4 * W_FP * total));
+  LSG_RC(ensure(s, s->binv_iv[ws], 4 * W_FP * total));
+  uint32_t* lv = P_<uint32_t>(s->binv_lv[ws]);
+  uint32_t* iv = P_<uint32_t>(s->binv_iv[ws]);
+  const size_t L = sz.size() - 1;
+  auto lvl = [&](size_t k) { return k == 0 ? (uint32_t*)v : lv + W_FP * off[k]; };
+  for (size_t k = 1; k <= L; k++)
+    KL(s, name, lsgk::binv_up(S_(s), (int)sz[k], (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1), lvl(k)));
+  KL(s, name, lsgk::binv_root(S_(s), lvl(L), iv + W_FP * off[L]));
+  for (size_t k = L; k >= 1; k--)
+    KL(s, name, lsgk::binv_down(S_(s), (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1), iv + W_FP * off[k],
+                                k == 1 ? out : iv + W_FP * off[k - 1]));
+  return LSG_OK;
+}
+
+// hash_to_G2 of the slot's n expanded messages (d_ub) into d_H / d_hinf on the current stream
+int launch_hash(Slot* s, int n) {
+  KL(s, "k_h2c_prep", lsgk::h2c_prep(S_(s), n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrm)));
+  LSG_RC(batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)));
+  KL(s, "k_h2c_map", lsgk::h2c_map(S_(s), n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp)));
+  KL(s, "k_h2c_clear",
+     lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf)));
+  LSG_RC(batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)));
+  KL(s, "k_h2c_affine", lsgk::h2c_affine(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi),
+                                         P_<uint8_t>(s->d_hinf), P_<uint32_t>(s->d_H)));
+  return LSG_OK;
+}
+
+// ---- staging: the package's sets into the slot's pinned arena (order given by `order`),
+// randomizers drawn here (seed == 0: OS CSPRNG; else deterministic, for tests)
+int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
+  size_t npk = 0, msg_total = 0;
+  for (size_t i = 0; i < n; i++) {
+    npk += sets[i]->n_pks;
+    msg_total += sets[i]->msg_len;
+  }
+  s->n_sets = n;
+  s->n_pks = npk;
+  LSG_RC(size_inputs(s, n, npk, msg_total));
+  const size_t nn = std::max(n, (size_t)1), np = std::max(npk, (size_t)1);
+  auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
+  const size_t o_sig = 0, o_siglen = al(o_sig + 192 * nn), o_msgoff = al(o_siglen + 4 * nn),
+               o_msglen = al(o_msgoff + 4 * nn), o_pklen = al(o_msglen + 4 * nn), o_rnd = al(o_pklen + 4 * np),
+               o_pk = al(o_rnd + 8 * nn), o_msg = al(o_pk + 96 * np);
+  uint8_t* A = H_<uint8_t>(s->h_arena);
+  uint32_t* siglen = (uint32_t*)(A + o_siglen);
+  uint32_t* msgoff = (uint32_t*)(A + o_msgoff);
+  uint32_t* msglen = (uint32_t*)(A + o_msglen);
+  uint32_t* pklen = (uint32_t*)(A + o_pklen);
+  uint64_t* rnd = (uint64_t*)(A + o_rnd);
+  siglen[0] = msgoff[0] = msglen[0] = pklen[0] = 0;
+  rnd[0] = 0;
+  s->pk_cnt.resize(n);
+  s->pk_first.resize(n);
+  s->rnd.resize(n);
+  size_t mo = 0, po = 0;
+  bool single = npk == n;
+  for (size_t i = 0; i < n; i++) {
+    const lsg_set* q = sets[i];
+    siglen[i] = q->sig_len;
+    uint8_t* sg = A + o_sig + 192 * i;
+    if ((q->sig_len == 96 || q->sig_len == 192) && q->sig)
+      memcpy(sg, q->sig, q->sig_len);
+    else
+      memset(sg, 0, 96);
+    msgoff[i] = (uint32_t)mo;
+    msglen[i] = q->msg_len;
+    if (q->msg_len) memcpy(A + o_msg + mo, q->msg, q->msg_len);
+    mo += q->msg_len;
+    s->pk_cnt[i] = q->n_pks;
+    s->pk_first[i] = (uint32_t)po;
+    if (q->n_pks != 1) single = false;
+    for (uint32_t k = 0; k < q->n_pks; k++) {
+      pklen[po] = q->pk_len;
+      uint8_t* pd = A + o_pk + 96 * po;
+      if ((q->pk_len == 48 || q->pk_len == 96 || q->pk_len == LSG_PK_INDEX) && q->pks)
+        memcpy(pd, q->pks + (size_t)q->pk_len * k, q->pk_len);
+      else
+        memset(pd, 0, 4);
+      po++;
+    }
+  }
+  s->single_keys = single && n > 0;
+  if (scale && n) {
+    if (seed == 0) {
+      if (!os_random(rnd, 8 * n)) {
+        s->d->c->err = "no entropy for the RLC randomizers (getrandom failed)";
+        return LSG_ERR_ENTROPY;
+      }
+      for (size_t i = 0; i < n; i++)
+        while (rnd[i] == 0)
+          if (!os_random(&rnd[i], 8)) {
+            s->d->c->err = "no entropy for the RLC randomizers (getrandom failed)";
+            return LSG_ERR_ENTROPY;
+          }
+    } else {
+      uint64_t sd = seed;
+      for (size_t i = 0; i < n; i++) {
+        uint64_t r;
+        do r = splitmix64(sd);
+        while (r == 0);
+        rnd[i] = r;
+      }
+    }
+  } else if (n) {
+    memset(rnd, 0, 8 * n);
+  }
+  memcpy(s->rnd.data(), rnd, 8 * n);
+  hipStream_t S = s->st[0];
+  struct {
+    DevBuf* d;
+    size_t off, len;
+  } cp[] = {{&s->d_sig, o_sig, 192 * nn},      {&s->d_siglen, o_siglen, 4 * nn}, {&s->d_msg, o_msg, std::max(msg_total, (size_t)1)},
+            {&s->d_msgoff, o_msgoff, 4 * nn}, {&s->d_msglen, o_msglen, 4 * nn}, {&s->d_pk, o_pk, 96 * np},
+            {&s->d_pklen, o_pklen, 4 * np},   {&s->d_rnd, o_rnd, 8 * nn}};
+  for (auto& x : cp) LSG_HIP(s, hipMemcpyAsync(x.d->p, A + x.off, x.len, hipMemcpyHostToDevice, S));
+  return LSG_OK;
+}
+
+// ---- Miller items: <= K consecutive sets of one range (group); item_first / item_cnt go to
+// the arena.  Returns the number of items; set_item (optional) maps set -> item.
+size_t plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges, size_t* off,
+                  std::vector<int32_t>* set_item, std::vector<std::pair<int32_t, int32_t>>* range_items) {
+  const size_t K = (size_t)miller_k();
+  std::vector<int32_t> first, cnt;
+  for (auto& r : ranges) {
+    const int32_t i0 = (int32_t)first.size();
+    for (size_t i = r.first; i < r.second; i += K) {
+      size_t c = std::min(K, r.second - i);
+      if (set_item)
+        for (size_t k = 0; k < c; k++) (*set_item)[i + k] = (int32_t)first.size();
+      first.push_back((int32_t)i);
+      cnt.push_back((int32_t)c);
+    }
+    if (range_items) range_items->push_back({i0, (int32_t)first.size()});
+  }
+  *off = s->plan.size();
+  s->plan.insert(s->plan.end(), first.begin(), first.end());
+  s->plan.insert(s->plan.end(), cnt.begin(), cnt.end());
+  return first.size();
+}
+
+int plan_phase(Slot* s, PhasePlan& Ph) {
+  std::vector<int32_t>& A = s->plan;
+  const size_t ng = Ph.groups.size();
+  Ph.n_msm = 0;
+  while (Ph.n_msm < ng && Ph.groups[Ph.n_msm].msm) Ph.n_msm++;
+  // bucket MSM: per MSM group, bucket (w, d) = the sets whose w-th byte of r_i is d
+  if (Ph.n_msm) {
+    const size_t nb = (size_t)MSM_WINDOWS * MSM_DIGITS;
+    std::vector<int32_t> cnt(Ph.n_msm * nb, 0);
+    for (size_t g = 0; g < Ph.n_msm; g++)
+      for (size_t i = Ph.groups[g].first; i < Ph.groups[g].first + Ph.groups[g].len; i++) {
+        const uint64_t r = s->rnd[i];
+        for (int w = 0; w < MSM_WINDOWS; w++) {
+          const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
+          if (d) cnt[g * nb + (size_t)w * MSM_DIGITS + d - 1]++;
+        }
+      }
+    std::vector<int32_t> seg_off(Ph.n_msm * nb), seg_len(cnt);
+    int32_t tot = 0;
+    for (size_t b = 0; b < cnt.size(); b++) {
+      seg_off[b] = tot;
+      tot += cnt[b];
+    }
+    const size_t idx_off = A.size();
+    A.resize(idx_off + (size_t)tot);
+    int32_t* idx = A.data() + idx_off;
+    std::vector<int32_t> fill(seg_off);
+    for (size_t g = 0; g < Ph.n_msm; g++)
+      for (size_t i = Ph.groups[g].first; i < Ph.groups[g].first + Ph.groups[g].len; i++) {
+        const uint64_t r = s->rnd[i];
+        for (int w = 0; w < MSM_WINDOWS; w++) {
+          const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
+          if (d) idx[fill[g * nb + (size_t)w * MSM_DIGITS + d - 1]++] = (int32_t)i;
+        }
+      }
+    Ph.buckets = plan_seg(A, 1, seg_off, seg_len, true, idx_off, 0);
+    // bit (g, k = 8w + j): the buckets (g, w, d) whose digit d has bit j set
+    const size_t bidx = A.size();
+    std::vector<int32_t> boff, blen;
+    for (size_t g = 0; g < Ph.n_msm; g++)
+      for (int w = 0; w < MSM_WINDOWS; w++)
+        for (int j = 0; j < 8; j++) {
+          boff.push_back((int32_t)(A.size() - bidx));
+          for (uint32_t d = 1; d <= 255; d++)
+            if ((d >> j) & 1u) A.push_back((int32_t)(g * nb + (size_t)w * MSM_DIGITS + d - 1));
+          blen.push_back((int32_t)(A.size() - bidx) - boff.back());
+        }
+    Ph.bits = plan_seg(A, 1, boff, blen, true, bidx, 0);
+  }
+  // scaled groups: S_g = sum of the contiguous scaled points
+  if (Ph.n_msm < ng) {
+    std::vector<int32_t> off, len;
+    for (size_t g = Ph.n_msm; g < ng; g++) {
+      off.push_back((int32_t)Ph.groups[g].first);
+      len.push_back((int32_t)Ph.groups[g].len);
+    }
+    Ph.sums = plan_seg(A, 1, off, len, false, 0, (int32_t)Ph.n_msm);
+  }
+  // Miller items of this phase: <= K consecutive sets, never crossing a group
+  std::vector<std::pair<int32_t, int32_t>> gi;
+  {
+    std::vector<std::pair<size_t, size_t>> ranges;
+    for (auto& g : Ph.groups) ranges.push_back({g.first, g.first + g.len});
+    Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &gi);
+  }
+  // F_g = f_g * prod of the group's items; element ids index fall
+  const size_t pidx = A.size();
+  std::vector<int32_t> poff, plen;
+  for (size_t g = 0; g < ng; g++) {
+    poff.push_back((int32_t)(A.size() - pidx));
+    for (int32_t it = gi[g].first; it < gi[g].second; it++) A.push_back(it);
+    A.push_back((int32_t)(Ph.n_items + g));
+    plen.push_back((int32_t)(A.size() - pidx) - poff.back());
+  }
+  Ph.prod = plan_seg(A, 2, poff, plen, true, pidx, 0);
+  return LSG_OK;
+}
+
+// Miller accumulation of planned items (after ev_sig on the main stream)
+int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall) {
+  const int ni = (int)n_items;
+  const int32_t* items = PL(s, item_off);
+  KL(s, "k_miller_accum",
+     lsgk::miller_accum(S_(s), miller_k(), ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
+                        P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), (int)s->n_sets, P_<uint32_t>(s->d_lines),
+                        fall));
+  return LSG_OK;
+}
+
+// side stream: signature sums -> ML(-G1, S_g) -> fall slots; main stream: products, export, FE
+int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fall, bool export_blobs) {
+  const size_t ng = Ph.groups.size();
+  if (ng == 0) return LSG_OK;
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, ng, Ph.n_msm, true));
+  const size_t n = Ph.n_items;
+  s->cur = 1;
+  if (Ph.n_msm) {
+    LSG_RC(run_seg(s, 1, "msm_buckets", Ph.buckets, rs, P_<uint32_t>(s->d_bkt)));
+    LSG_RC(run_seg(s, 1, "msm_bits", Ph.bits, P_<uint32_t>(s->d_bkt), P_<uint32_t>(s->d_bits)));
+    KL(s, "k_g2p_to_canon", lsgk::g2p_to_canon(S_(s), (int)(MSM_BITS * Ph.n_msm), P_<uint32_t>(s->d_bits),
+                                               P_<uint8_t>(s->d_Sb)));
+    KL(s, "k_row_horner_miller",
+       lsg_row_horner_miller(S_(s), (int)Ph.n_msm, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
+  }
+  if (Ph.n_msm < ng) {
+    const int nsm = (int)(ng - Ph.n_msm);
+    LSG_RC(run_seg(s, 1, "sig_sums", Ph.sums, rs, P_<uint32_t>(s->d_S)));
+    uint8_t* sb = P_<uint8_t>(s->d_Sb) + (size_t)288 * MSM_BITS * Ph.n_msm;
+    KL(s, "k_g2p_to_canon", lsgk::g2p_to_canon(S_(s), nsm, P_<uint32_t>(s->d_S) + W_G2P * Ph.n_msm, sb));
+    KL(s, "k_row_miller_neg_g1",
+       lsg_row_miller_neg_g1(S_(s), nsm, sb, P_<uint8_t>(s->d_fgb) + 576 * Ph.n_msm));
+  }
+  KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S_(s), (int)ng, P_<uint8_t>(s->d_fgb), fall + W_F12 * n));
+  LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
+  s->cur = 0;
+  LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_grp, 0));
+  LSG_RC(run_seg(s, 2, "fp12_product", Ph.prod, fall, P_<uint32_t>(s->d_F)));
+  KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S_(s), (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_Fb)));
+  if (export_blobs) LSG_HIP(s, hipMemcpyAsync(s->h_blob.p, s->d_Fb.p, 576 * ng, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipEventRecord(s->ev_part, s->st[0]));
+  return LSG_OK;
+}
+
+// FE of the phase's groups + verdict readback (main stream)
+int launch_fe(Slot* s, size_t ng) {
+  if (ng == 0) return LSG_OK;
+  s->cur = 0;
+  KL(s, "k_row_final_exp", lsg_row_final_exp(S_(s), (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
+  LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, s->st[0]));
+  return LSG_OK;
+}
+
+// Per-set stages of the slot's package (no host synchronisation):
+//   side: pubkeys -> aggregation -> [r_i] scaling -> signature decode -> subgroup check (ev_sig)
+//   main: expand_message -> hash_to_G2 -> lines -> wait ev_sig -> Miller items f (fall)
+int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item_off, uint32_t* fall) {
+  const int n = (int)s->n_sets, np = (int)s->n_pks;
+  if (n == 0) return LSG_OK;
+  Dev* d = s->d;
+  LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
+  s->cur = 1;
+  LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
+  if (np > 0) {
+    // single-key sets decode straight into their aggregate slot
+    uint32_t* dst = s->single_keys ? P_<uint32_t>(s->d_agg) : P_<uint32_t>(s->d_pkp);
+    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen), dst,
+                                         P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok),
+                                         (uint32_t)d->pktab_n));
+  }
+  if (!s->single_keys) LSG_RC(run_seg(s, 0, "g1_aggregate", *pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
+  KL(s, "k_pk_scale", lsgk::pk_scale(S_(s), n, P_<uint32_t>(s->d_agg), P_<uint64_t>(s->d_rnd), P_<uint32_t>(s->d_Pp),
+                                     P_<uint32_t>(s->d_zP), P_<uint8_t>(s->d_pinf)));
+  LSG_RC(batch_inv(s, 1, "binv_pk", P_<uint32_t>(s->d_zP), (size_t)n, P_<uint32_t>(s->d_zPi)));
+  KL(s, "k_pk_affine", lsgk::pk_affine(S_(s), n, P_<uint32_t>(s->d_Pp), P_<uint32_t>(s->d_zPi), P_<uint32_t>(s->d_P)));
+  KL(s, "k_sig_decode", lsgk::sig_decode(S_(s), n, P_<uint8_t>(s->d_sig), P_<uint32_t>(s->d_siglen),
+                                         P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr)));
+  KL(s, "k_sig_subgroup", lsgk::sig_subgroup(S_(s), n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                             P_<int32_t>(s->d_seterr)));
+  LSG_HIP(s, hipEventRecord(s->ev_sig, s->st[1]));
+  s->cur = 0;
+  KL(s, "k_expand_msg", lsgk::expand_msg(S_(s), n, P_<uint8_t>(s->d_msg), P_<uint32_t>(s->d_msgoff),
+                                         P_<uint32_t>(s->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN,
+                                         P_<uint8_t>(s->d_ub)));
+  LSG_RC(launch_hash(s, n));
+  KL(s, "k_miller_lines", lsgk::miller_lines(S_(s), n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
+  LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
+  if (n_items) LSG_RC(launch_accum(s, n_items, item_off, fall));
+  return LSG_OK;
+}
+
+// pubkey aggregation plan (sets with several keys): segment i = keys pk_first[i] ..
+SegPlan plan_pk_agg(Slot* s) {
+  std::vector<int32_t> off(s->n_sets), len(s->n_sets);
+  for (size_t i = 0; i < s->n_sets; i++) {
+    off[i] = (int32_t)s->pk_first[i];
+    len[i] = (int32_t)s->pk_cnt[i];
+  }
+  return plan_seg(s->plan, 0, off, len, false, 0, 0);
+}
+
+// D2H of per-set status into the pinned mirrors, then ev_done on the main stream
+int launch_readback(Slot* s, bool status) {
+  hipStream_t S = s->st[0];
+  const size_t n = s->n_sets, np = s->n_pks;
+  if (s->own_streams) {  // join the side stream
+    LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
+    LSG_HIP(s, hipStreamWaitEvent(S, s->ev_grp, 0));
+  }
+  if (status) {
+    if (n) {
+      LSG_HIP(s, hipMemcpyAsync(s->h_err.p, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, S));
+      LSG_HIP(s, hipMemcpyAsync(s->h_pinf.p, s->d_pinf.p, n, hipMemcpyDeviceToHost, S));
+    }
+    if (np) LSG_HIP(s, hipMemcpyAsync(s->h_pkerr.p, s->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, S));
+  }
+  LSG_HIP(s, hipEventRecord(s->ev_done, S));
+  return LSG_OK;
+}
+
+struct SetStatus {
+  const int32_t* err;         // per set: BLST code (0 ok)
+  std::vector<uint8_t> pinf;  // per set: aggregated pk is infinity (2: no keys at all)
+  const int32_t* pkerr;       // per pubkey
+};
+
+SetStatus read_status(Slot* s) {
+  SetStatus ss;
+  const size_t n = s->n_sets;
+  ss.err = H_<int32_t>(s->h_err);
+  ss.pkerr = H_<int32_t>(s->h_pkerr);
+  ss.pinf.assign(H_<uint8_t>(s->h_pinf), H_<uint8_t>(s->h_pinf) + n);
+  for (size_t i = 0; i < n; i++)
+    if (s->pk_cnt[i] == 0) ss.pinf[i] = 2;  // PublicKey.aggregate([]) throws
+  return ss;
+}
+
+int32_t set_error(const SetStatus& ss, size_t i) {
+  if (ss.err[i]) return ss.err[i];
+  if (ss.pinf[i] == 2) return LSG_ERR_EMPTY_AGGREGATE;
+  return ss.pinf[i] ? LSG_BLST_PK_IS_INFINITY : 0;
+}
+
+// Error a job's maybeBatch call would throw, in the reference's order:
+// Signature.fromBytes over all sets first (maybeBatch.ts:17-26 map), then
+// mul_n_aggregate rejecting an infinite public key (BLST_PK_IS_INFINITY).
+int32_t job_error(const SetStatus& ss, size_t first, size_t count) {
+  if (count == 0) return LSG_ERR_EMPTY_SET;
+  for (size_t k = 0; k < count; k++)
+    if (ss.err[first + k]) return ss.err[first + k];
+  for (size_t k = 0; k < count; k++)
+    if (ss.pinf[first + k]) return set_error(ss, first + k);
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- packages
+namespace {
+
+const uint8_t* fp12_one_blob() {  // canonical Fp12 one: c0.c0.c0 = 1
+  static uint8_t b[576] = {0};
+  b[47] = 1;
+  return b;
+}
+
+// sig_prep into `out` for the slot's sets on the side stream.  mode: per-set bytes (1 =
+// scale) or null; rnd null = no scaling at all (every group sums by the bucket MSM).
+int launch_sig_prep(Slot* s, bool scale, const std::vector<uint8_t>* mode, uint32_t* out) {
+  const int n = (int)s->n_sets;
+  if (n == 0) return LSG_OK;
+  s->cur = 1;
+  const uint8_t* dm = nullptr;
+  if (scale && mode) {
+    LSG_RC(ensure_host(s, s->h_mode, (size_t)n));
+    LSG_RC(ensure(s, s->d_mode, (size_t)n));
+    memcpy(s->h_mode.p, mode->data(), (size_t)n);
+    LSG_HIP(s, hipMemcpyAsync(s->d_mode.p, s->h_mode.p, (size_t)n, hipMemcpyHostToDevice, s->st[1]));
+    dm = P_<uint8_t>(s->d_mode);
+  }
+  KL(s, "k_sig_prep", lsgk::sig_prep(S_(s), n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                     P_<int32_t>(s->d_seterr), P_<uint8_t>(s->d_pinf),
+                                     scale ? P_<uint64_t>(s->d_rnd) : nullptr, dm, out));
+  return LSG_OK;
+}
+
+// Part 1 of phase A on one device: stage this device's jobs (ids into `jobs`; batchable jobs
+// first), plan and launch every per-set stage and group stage up to the canonical products
+// (ev_part).  n_node > 0: this slot also reduces the all-gathered partials of n_node devices
+// (its plan holds that product's chunk list).
+int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint64_t seed, int n_node) {
+  timer_reset(s);
+  s->plan.clear();
+  memset(&s->stats, 0, sizeof(s->stats));
+  s->stats.start_ns = now_ns();
+  const size_t nj = ids.size();
+  s->jobs.assign(nj, JobRec());
+  s->job_ids = ids;
+  s->results.assign(nj, lsg_job_result{LSG_INVALID, 0});
+  s->job_group.assign(nj, -1);
+  s->batch_order.clear();
+  s->big_g = -1;
+  s->rs2_ready = false;
+  s->has_node = n_node > 0;
+  std::vector<const lsg_set*> flat;
+  std::vector<size_t> nonb;
+  for (int pass = 0; pass < 2; pass++)
+    for (size_t k = 0; k < nj; k++) {
+      const lsg_job& J = jobs[ids[k]];
+      const bool b = (J.flags & LSG_JOB_BATCHABLE) != 0;
+      if (b != (pass == 0)) continue;
+      s->jobs[k].first = flat.size();
+      s->jobs[k].count = J.n_sets;
+      s->jobs[k].flags = J.flags;
+      for (uint32_t q = 0; q < J.n_sets; q++) flat.push_back(&J.sets[q]);
+      (b ? s->batch_order : nonb).push_back(k);
+    }
+  s->nb_sets = 0;
+  for (size_t k : s->batch_order) s->nb_sets += s->jobs[k].count;
+  LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true));
+  // phase-A groups, MSM groups first: the package group, then one per non-batchable job
+  PhasePlan& A = s->phA;
+  A = PhasePlan();
+  std::vector<Grp> gm, gs;
+  std::vector<int> om, os;  // owner: -2 the package group, else the job
+  auto add = [&](size_t first, size_t len, int owner) {
+    Grp g;
+    g.first = first;
+    g.len = len;
+    g.msm = len >= msm_min_group();
+    (g.msm ? gm : gs).push_back(g);
+    (g.msm ? om : os).push_back(owner);
+  };
+  s->chunk_mode = !package_group_mode();
+  s->chunk_group.clear();
+  std::vector<std::pair<size_t, size_t>> chunks;
+  if (s->chunk_mode) {
+    chunks = chunkify(s->batch_order.size(), 16);
+    for (size_t c = 0; c < chunks.size(); c++) {
+      size_t len = 0;
+      for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
+      if (len) add(s->jobs[s->batch_order[chunks[c].first]].first, len, -3 - (int)c);
+    }
+    s->chunk_group.assign(chunks.size(), -1);
+  } else if (s->nb_sets) {
+    add(0, s->nb_sets, -2);
+  }
+  for (size_t k : nonb) {
+    if (s->jobs[k].count == 0)
+      s->results[k] = {LSG_ERROR, LSG_ERR_EMPTY_SET};  // maybeBatch.ts:29-31
+    else
+      add(s->jobs[k].first, s->jobs[k].count, (int)k);
+  }
+  A.groups = gm;
+  A.groups.insert(A.groups.end(), gs.begin(), gs.end());
+  om.insert(om.end(), os.begin(), os.end());
+  for (size_t g = 0; g < om.size(); g++) {
+    if (om[g] == -2)
+      s->big_g = (int)g;
+    else if (om[g] <= -3)
+      s->chunk_group[(size_t)(-3 - om[g])] = (int)g;
+    else
+      s->job_group[(size_t)om[g]] = (int)g;
+  }
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, A.groups.size(), gm.size(), true));
+  if (!s->single_keys) s->pkagg = plan_pk_agg(s);
+  LSG_RC(plan_phase(s, A));
+  SegPlan node;
+  if (n_node > 0) {
+    std::vector<int32_t> off{0}, len{(int32_t)n_node};
+    node = plan_seg(s->plan, 2, off, len, false, 0, 0);
+  }
+  LSG_RC(upload_plan(s));
+  LSG_RC(launch_set_stages(s, &s->pkagg, A.n_items, A.item_off, P_<uint32_t>(s->d_fall)));
+  // signature points: unscaled for MSM groups, [r_i] sig_i for the rest
+  if (!A.groups.empty()) {
+    const bool any_small = A.n_msm < A.groups.size();
+    std::vector<uint8_t> mode;
+    if (any_small && A.n_msm) {
+      mode.assign(s->n_sets, 0);
+      for (size_t g = A.n_msm; g < A.groups.size(); g++)
+        memset(mode.data() + A.groups[g].first, 1, A.groups[g].len);
+    }
+    LSG_RC(launch_sig_prep(s, any_small, mode.empty() ? nullptr : &mode, P_<uint32_t>(s->d_rs)));
+  }
+  LSG_RC(launch_phase(s, A, P_<uint32_t>(s->d_rs), P_<uint32_t>(s->d_fall), true));
+  if (A.groups.empty() || s->big_g < 0) {  // no package group: the partial is the identity
+    s->cur = 0;
+    LSG_HIP(s, hipMemcpyAsync(P_<uint8_t>(s->d_gath) + 576 * LSG_MAX_DEVICES, fp12_one_blob(), 576,
+                              hipMemcpyHostToDevice, s->st[0]));
+    LSG_HIP(s, hipEventRecord(s->ev_part, s->st[0]));
+  }
+  s->phA_node = node;
+  return LSG_OK;
+}
+
+// device pointer of the package group's canonical partial (576 bytes)
+const uint8_t* pkg_partial_dev(Slot* s) {
+  if (s->phA.groups.empty() || s->big_g < 0) return P_<uint8_t>(s->d_gath) + 576 * LSG_MAX_DEVICES;
+  return P_<uint8_t>(s->d_Fb) + 576 * (size_t)s->big_g;
+}
+
+// node check on this slot (device 0 of the ticket): product of the n gathered partials in
+// d_gath, one final exponentiation -> h_nodeV (ev_node)
+int pkg_node_check(Slot* s, int n) {
+  s->cur = 0;
+  const uint32_t* nf = P_<uint32_t>(s->d_nodeF);
+  KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S_(s), n, P_<uint8_t>(s->d_gath), P_<uint32_t>(s->d_nodeF)));
+  LSG_RC(run_seg(s, 2, "fp12_product", s->phA_node, nf, P_<uint32_t>(s->d_nodeF) + W_F12 * (size_t)n));
+  uint8_t* blob = P_<uint8_t>(s->d_gath) + 576 * (size_t)(LSG_MAX_DEVICES + 1);
+  KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S_(s), 1, P_<uint32_t>(s->d_nodeF) + W_F12 * (size_t)n, blob));
+  KL(s, "k_row_final_exp", lsg_row_final_exp(S_(s), 1, blob, P_<int32_t>(s->d_nodeV)));
+  LSG_HIP(s, hipMemcpyAsync(s->h_nodeV.p, s->d_nodeV.p, 4, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipEventRecord(s->ev_node, s->st[0]));
+  return LSG_OK;
+}
+
+// Part 2 of phase A: every group's final exponentiation and the status readback (ev_done)
+int pkg_part2(Slot* s) {
+  LSG_RC(launch_fe(s, s->phA.groups.size()));
+  return launch_readback(s, true);
+}
+
+// One fallback phase (worker.ts:74-96) over `groups` (scaled signature sums, own Miller items
+// into fall2), synchronous; verdicts into v.
+int run_fallback_phase(Slot* s, const std::vector<Grp>& groups, std::vector<int32_t>& v) {
+  v.assign(groups.size(), 0);
+  if (groups.empty()) return LSG_OK;
+  timer_reset(s);
+  s->plan.clear();
+  PhasePlan Ph;
+  Ph.groups = groups;
+  for (auto& g : Ph.groups) g.msm = false;
+  LSG_RC(plan_phase(s, Ph));
+  LSG_RC(upload_plan(s));
+  std::vector<uint8_t> mode(s->n_sets, 0);
+  for (auto& g : groups) memset(mode.data() + g.first, 1, g.len);
+  // the side stream needs the plan: order it after the upload on the main stream
+  LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
+  LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
+  LSG_RC(launch_sig_prep(s, true, &mode, P_<uint32_t>(s->d_rs2)));
+  s->cur = 0;
+  LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, P_<uint32_t>(s->d_fall2)));
+  LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), P_<uint32_t>(s->d_fall2), false));
+  LSG_RC(launch_fe(s, groups.size()));
+  LSG_RC(launch_readback(s, false));
+  LSG_HIP(s, hipEventSynchronize(s->ev_done));
+  s->stats.n_final_exps += (uint32_t)groups.size();
+  memcpy(v.data(), s->h_verdict.p, 4 * groups.size());
+  return LSG_OK;
+}
+
+// The reference's verdict rules for this device's share of the package (worker.ts:30-106),
+// after ev_done.  node_valid: 1 = the node-wide check of all devices' partials passed, 0 = it
+// failed (this device's own package check localises), -1 = no node check (single device).
+int pkg_resolve(Slot* s, int node_valid) {
+  const SetStatus ss = read_status(s);
+  const PhasePlan& A = s->phA;
+  std::vector<int32_t> vA(H_<int32_t>(s->h_verdict), H_<int32_t>(s->h_verdict) + A.groups.size());
+  s->stats.n_final_exps += (uint32_t)A.groups.size();
+  const size_t nj = s->jobs.size();
+  // worker.ts:108-114: deserializeSet runs first; a bad pubkey throws out of
+  // verifyManySignatureSets and rejects every job of the package
+  int32_t pkfail = 0;
+  for (size_t k = 0; k < s->n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
+  if (pkfail) {
+    for (size_t j = 0; j < nj; j++) s->results[j] = {LSG_ERROR, pkfail};
+    return LSG_OK;
+  }
+  // non-batchable jobs: their own group (worker.ts:88-96)
+  for (size_t j = 0; j < nj; j++) {
+    const int g = s->job_group[j];
+    if (g < 0) continue;
+    const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
+    s->results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{vA[(size_t)g] ? LSG_VALID : LSG_INVALID, 0};
+  }
+  if (s->batch_order.empty()) return LSG_OK;
+  // batchable jobs: chunks of >= 16 jobs (worker.ts:51-86)
+  const bool big_ok = s->big_g < 0 || node_valid == 1 || (node_valid != 1 && vA[(size_t)s->big_g] != 0);
+  auto chunks = chunkify(s->batch_order.size(), 16);
+  std::vector<size_t> retry;  // jobs verified individually (phase C)
+  std::vector<Grp> chk;       // chunks checked on their own (phase B)
+  std::vector<std::pair<size_t, size_t>> chk_jobs;
+  bool any_err_chunk = false;
+  std::vector<uint8_t> chunk_err(chunks.size(), 0);
+  for (size_t c = 0; c < chunks.size(); c++) {
+    for (size_t q = chunks[c].first; q < chunks[c].second && !chunk_err[c]; q++) {
+      const JobRec& J = s->jobs[s->batch_order[q]];
+      for (size_t i = J.first; i < J.first + J.count; i++)
+        if (set_error(ss, i)) {
+          chunk_err[c] = 1;
+          break;
+        }
+    }
+    any_err_chunk = any_err_chunk || chunk_err[c];
+  }
+  for (size_t c = 0; c < chunks.size(); c++) {
+    const size_t first = s->jobs[s->batch_order[chunks[c].first]].first;
+    size_t len = 0;
+    for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
+    if (len == 0) {  // maybeBatch([]) throws: retried, and every job throws again
+      s->stats.batch_retries++;
+      for (size_t q = chunks[c].first; q < chunks[c].second; q++)
+        s->results[s->batch_order[q]] = {LSG_ERROR, LSG_ERR_EMPTY_SET};
+      continue;
+    }
+    if (!chunk_err[c] && s->chunk_mode) {  // the chunk's own phase-A group decides
+      if (vA[(size_t)s->chunk_group[c]]) {
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
+        s->stats.batch_sigs_success += (uint32_t)len;
+      } else {
+        s->stats.batch_retries++;
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
+      }
+    } else if (!chunk_err[c]) {
+      if (big_ok) {
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
+        s->stats.batch_sigs_success += (uint32_t)len;
+      } else if (chunks.size() == 1 && !any_err_chunk) {
+        // the package group is exactly this chunk: its verdict is the chunk's
+        s->stats.batch_retries++;
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
+      } else {
+        Grp g;
+        g.first = first;
+        g.len = len;
+        chk.push_back(g);
+        chk_jobs.push_back(chunks[c]);
+      }
+    } else {  // the chunk throws (worker.ts:79-85): every job is verified on its own
+      s->stats.batch_retries++;
+      for (size_t q = chunks[c].first; q < chunks[c].second; q++) {
+        const size_t j = s->batch_order[q];
+        const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
+        if (e)
+          s->results[j] = {LSG_ERROR, e};
+        else if (big_ok && !s->chunk_mode)  // its sets are in the passing package group
+          s->results[j] = {LSG_VALID, 0};
+        else
+          retry.push_back(j);
+      }
+    }
+  }
+  std::vector<int32_t> v;
+  if (!chk.empty()) {  // phase B
+    LSG_RC(run_fallback_phase(s, chk, v));
+    for (size_t c = 0; c < chk.size(); c++) {
+      if (v[c]) {
+        for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
+        s->stats.batch_sigs_success += (uint32_t)chk[c].len;
+      } else {
+        s->stats.batch_retries++;
+        for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) retry.push_back(s->batch_order[q]);
+      }
+    }
+  }
+  if (!retry.empty()) {  // phase C
+    std::vector<Grp> g3;
+    std::vector<size_t> g3job;
+    for (size_t j : retry) {
+      const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
+      if (e) {
+        s->results[j] = {LSG_ERROR, e};
+        continue;
+      }
+      Grp g;
+      g.first = s->jobs[j].first;
+      g.len = s->jobs[j].count;
+      g3.push_back(g);
+      g3job.push_back(j);
+    }
+    LSG_RC(run_fallback_phase(s, g3, v));
+    for (size_t g = 0; g < g3.size(); g++) s->results[g3job[g]] = {v[g] ? LSG_VALID : LSG_INVALID, 0};
+  }
+  return LSG_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- tickets
+namespace {
+
+// Whole jobs per device by cumulative set count (never splits a job): job j goes
+// to floor(sets_before_j * n_dev / total).
+void assign_jobs(const uint32_t* sizes, size_t n_jobs, int n_dev, int32_t* owner) {
+  uint64_t total = 0;
+  for (size_t j = 0; j < n_jobs; j++) total += sizes[j];
+  uint64_t before = 0;
+  for (size_t j = 0; j < n_jobs; j++) {
+    owner[j] = (total == 0 || n_dev <= 1) ? 0 : (int32_t)std::min<uint64_t>((uint64_t)n_dev - 1, before * (uint64_t)n_dev / total);
+    before += sizes[j];
+  }
+}
+
+uint64_t make_ticket(lsg_ctx* c, int kind, int index, uint64_t* serial) {
+  *serial = c->next_serial++;
+  return (*serial << 16) | ((uint64_t)kind << 8) | (uint64_t)index;
+}
+
+// package index of a jobs ticket (slot `index` on every device), or -1
+int ticket_pkg(lsg_ctx* c, uint64_t t) {
+  const int k = (int)((t >> 8) & 255), i = (int)(t & 255);
+  if (k != SLOT_JOBS || i >= LSG_SLOTS) return -1;
+  const Slot& s = c->dev[0]->slots[i];
+  if (s.kind != SLOT_JOBS || s.serial != (t >> 16)) return -1;
+  return i;
+}
+Slot* ticket_final(lsg_ctx* c, uint64_t t) {
+  const int k = (int)((t >> 8) & 255), i = (int)(t & 255);
+  if (k != SLOT_FINAL || i >= LSG_FINALS) return nullptr;
+  Slot* s = &c->dev[0]->finals[i];
+  if (s->kind != SLOT_FINAL || s->serial != (t >> 16)) return nullptr;
+  return s;
+}
+
+void sync_slot(Slot* s) {
+  for (int k = 0; k < 2; k++)
+    if (s->st[k]) (void)hipStreamSynchronize(s->st[k]);
+}
+
+bool force_exchange() {
+  const char* e = getenv("LSG_FORCE_EXCHANGE");
+  return e && atoi(e) != 0;
+}
+
+// all-gather of the devices' partials into device 0's d_gath, then the node check there
+int pkg_exchange(lsg_ctx* c, int p) {
+  const int n = c->n_dev;
+  Slot* s0 = &c->dev[0]->slots[p];
+  if (c->rccl) {
+    // one collective over xGMI: every device contributes 576 bytes
+    ncclResult_t r = ncclGroupStart();
+    for (int d = 0; d < n && r == ncclSuccess; d++) {
+      Slot* s = &c->dev[d]->slots[p];
+      (void)hipSetDevice(c->dev[d]->device);
+      r = ncclAllGather(pkg_partial_dev(s), s->d_gath.p, 576, ncclUint8, c->comm[d], s->st[0]);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    (void)hipSetDevice(c->dev[0]->device);
+    if (r != ncclSuccess) {
+      c->err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
+      return LSG_ERR_DEVICE;
+    }
+  } else {
+    // duplicate device list (tests): device-to-device copies on device 0's main stream
+    (void)hipSetDevice(c->dev[0]->device);
+    for (int d = 0; d < n; d++) {
+      Slot* s = &c->dev[d]->slots[p];
+      LSG_HIP(s0, hipStreamWaitEvent(s0->st[0], s->ev_part, 0));
+      uint8_t* dst = P_<uint8_t>(s0->d_gath) + 576 * (size_t)d;
+      if (c->dev[d]->device == c->dev[0]->device)
+        LSG_HIP(s0, hipMemcpyAsync(dst, pkg_partial_dev(s), 576, hipMemcpyDeviceToDevice, s0->st[0]));
+      else
+        LSG_HIP(s0, hipMemcpyPeerAsync(dst, c->dev[0]->device, pkg_partial_dev(s), c->dev[d]->device, 576, s0->st[0]));
+    }
+  }
+  return pkg_node_check(s0, n);
+}
+
+int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket) {
+  int p = -1;
+  for (int i = 0; i < LSG_SLOTS && p < 0; i++)
+    if (c->dev[0]->slots[i].kind == SLOT_FREE) p = i;
+  if (p < 0) {
+    c->err = "all pipeline slots are busy (wait on an outstanding ticket first)";
+    return LSG_ERR_BUSY;
+  }
+  const int n = c->n_dev;
+  const bool exch = n > 1 || force_exchange();
+  std::vector<std::vector<size_t>> ids(n);
+  {
+    std::vector<uint32_t> sizes(n_jobs);
+    std::vector<int32_t> owner(n_jobs);
+    for (size_t j = 0; j < n_jobs; j++) sizes[j] = jobs[j].n_sets;
+    assign_jobs(sizes.data(), n_jobs, n, owner.data());
+    for (size_t j = 0; j < n_jobs; j++) ids[(size_t)owner[j]].push_back(j);
+  }
+  int rc = LSG_OK;
+  for (int d = 0; d < n && !rc; d++) {
+    (void)hipSetDevice(c->dev[d]->device);
+    // distinct seeds per device for tests; 0 stays 0 (OS CSPRNG on every device)
+    const uint64_t sd = seed ? seed + 0x9e3779b97f4a7c15ull * (uint64_t)d : 0;
+    rc = pkg_part1(&c->dev[d]->slots[p], jobs, ids[d], sd, (d == 0 && exch) ? n : 0);
+  }
+  if (!rc && exch) rc = pkg_exchange(c, p);
+  for (int d = 0; d < n && !rc; d++) {
+    (void)hipSetDevice(c->dev[d]->device);
+    rc = pkg_part2(&c->dev[d]->slots[p]);
+  }
+  (void)hipSetDevice(c->dev[0]->device);
+  if (rc) {
+    for (int d = 0; d < n; d++) sync_slot(&c->dev[d]->slots[p]);
+    return rc;
+  }
+  uint64_t serial;
+  *ticket = make_ticket(c, SLOT_JOBS, p, &serial);
+  for (int d = 0; d < n; d++) {
+    Slot* s = &c->dev[d]->slots[p];
+    s->kind = SLOT_JOBS;
+    s->serial = serial;
+  }
+  c->dev[0]->slots[p].stats.reserved = (uint32_t)n_jobs;  // the ticket's job count
+  return LSG_OK;
+}
+
+// resolve a package: node_valid as pkg_resolve (-2: the ticket's own node check)
+int wait_pkg(lsg_ctx* c, int p, int node_valid, lsg_job_result* results, lsg_stats* stats) {
+  const int n = c->n_dev;
+  int rc = LSG_OK;
+  for (int d = 0; d < n && !rc; d++) {
+    Slot* s = &c->dev[d]->slots[p];
+    (void)hipSetDevice(c->dev[d]->device);
+    if (hipEventSynchronize(s->ev_done) != hipSuccess) rc = fail(s, "hipEventSynchronize", hipGetLastError());
+  }
+  Slot* s0 = &c->dev[0]->slots[p];
+  if (!rc && node_valid == -2) node_valid = s0->has_node ? (H_<int32_t>(s0->h_nodeV)[0] ? 1 : 0) : -1;
+  lsg_stats total;
+  memset(&total, 0, sizeof(total));
+  total.start_ns = s0->stats.start_ns;
+  for (int d = 0; d < n && !rc; d++) {
+    Slot* s = &c->dev[d]->slots[p];
+    (void)hipSetDevice(c->dev[d]->device);
+    rc = pkg_resolve(s, node_valid);
+    if (rc) break;
+    for (size_t k = 0; k < s->jobs.size(); k++) results[s->job_ids[k]] = s->results[k];
+    total.batch_retries += s->stats.batch_retries;
+    total.batch_sigs_success += s->stats.batch_sigs_success;
+    total.n_final_exps += s->stats.n_final_exps;
+  }
+  if (s0->has_node) total.n_final_exps += 1;
+  total.end_ns = now_ns();
+  if (stats) *stats = total;
+  for (int d = 0; d < n; d++) {
+    Slot* s = &c->dev[d]->slots[p];
+    if (rc) sync_slot(s);
+    s->kind = SLOT_FREE;
+    c->dev[d]->last = s;
+  }
+  (void)hipSetDevice(c->dev[0]->device);
+  return rc;
+}
+
+#define LSG_ENTER(c)                         \
+  std::lock_guard<std::mutex> _lk((c)->mu); \
+  LSG_HIPC((c), hipSetDevice((c)->dev[0]->device))
+
+// Block until a ticket's device work is done WITHOUT holding the context mutex, so a waiter
+// (e.g. an N-API worker thread) never stalls submissions from another thread.  The ticket's
+// slots cannot be recycled meanwhile: only the ticket's own wait call releases them.
+int presync_pkg(lsg_ctx* c, lsg_ticket t, bool partial_only) {
+  std::vector<std::pair<int, hipEvent_t>> evs;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int p = ticket_pkg(c, t);
+    if (p < 0) return LSG_ERR_INVALID_ARG;
+    for (int d = 0; d < c->n_dev; d++) {
+      Slot* s = &c->dev[d]->slots[p];
+      evs.push_back({c->dev[d]->device, partial_only ? s->ev_part : s->ev_done});
+    }
+  }
+  for (auto& e : evs) {
+    (void)hipSetDevice(e.first);
+    hipError_t r = hipEventSynchronize(e.second);
+    if (r != hipSuccess) return fail_c(c, "hipEventSynchronize", r);
+  }
+  return LSG_OK;
+}
+
+// ---- final-exponentiation entries (device 0): ng groups of pg partials
+int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg) {
+  timer_reset(s);
+  s->plan.clear();
+  const size_t n = ng * pg, np = std::max(n, (size_t)1), gq = std::max(ng, (size_t)1);
+  LSG_RC(ensure_host(s, s->h_blob, 576 * np));
+  LSG_RC(ensure(s, s->d_Fb, 576 * std::max(np, gq)));
+  LSG_RC(ensure(s, s->d_aux, 4 * W_F12 * np));
+  LSG_RC(ensure(s, s->d_F, 4 * W_F12 * gq));
+  LSG_RC(ensure(s, s->d_verdict, 4 * gq));
+  LSG_RC(ensure_host(s, s->h_verdict, 4 * gq));
+  s->n_sets = ng;  // verdict count
+  if (n) {
+    std::vector<int32_t> off, len;
+    for (size_t g = 0; g < ng; g++) {
+      off.push_back((int32_t)(g * pg));
+      len.push_back((int32_t)pg);
+    }
+    SegPlan P = plan_seg(s->plan, 2, off, len, false, 0, 0);
+    LSG_RC(upload_plan(s));
+    hipStream_t S = s->st[0];
+    memcpy(s->h_blob.p, partials576, 576 * n);
+    LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, s->h_blob.p, 576 * n, hipMemcpyHostToDevice, S));
+    KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S, (int)n, P_<uint8_t>(s->d_Fb), P_<uint32_t>(s->d_aux)));
+    LSG_RC(run_seg(s, 2, "fp12_product", P, P_<uint32_t>(s->d_aux), P_<uint32_t>(s->d_F)));
+    KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_Fb)));
+    KL(s, "k_row_final_exp", lsg_row_final_exp(S, (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
+    LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
+  } else {
+    s->n_sets = 0;
+  }
+  LSG_HIP(s, hipEventRecord(s->ev_done, s->st[0]));
+  return LSG_OK;
+}
+
+// stage + expand + hash on the utility slot (synchronous callers only)
+int util_hash(Slot* s, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst, uint32_t dst_len) {
+  std::vector<lsg_set> sets(n);
+  std::vector<const lsg_set*> sp(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&sets[i], 0, sizeof(lsg_set));
+    sets[i].msg = msgs + (size_t)msg_len * i;
+    sets[i].msg_len = msg_len;
+    sp[i] = &sets[i];
+  }
+  LSG_RC(stage_sets(s, sp.data(), n, 0, false));
+  LSG_RC(size_state(s, n, 0, 1, 0));
+  LSG_HIP(s, hipMemcpyAsync(s->d_dst.p, dst, dst_len, hipMemcpyHostToDevice, s->st[0]));
+  const int nn = (int)n;
+  KL(s, "k_expand_msg", lsgk::expand_msg(S_(s), nn, P_<uint8_t>(s->d_msg), P_<uint32_t>(s->d_msgoff),
+                                         P_<uint32_t>(s->d_msglen), P_<uint8_t>(s->d_dst), dst_len, P_<uint8_t>(s->d_ub)));
+  LSG_RC(launch_hash(s, nn));
+  // the utility slot's DST is restored for the next caller
+  LSG_HIP(s, hipMemcpyAsync(s->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice, s->st[0]));
+  return LSG_OK;
+}
+
+// keys (one "set" of n keys) into the utility slot's arena, decoded on its stream
+int util_stage_keys(Slot* s, const uint8_t* pks, uint32_t pk_len, size_t n) {
+  lsg_set q;
+  memset(&q, 0, sizeof(q));
+  q.pks = pks;
+  q.pk_len = pk_len;
+  q.n_pks = (uint32_t)n;
+  const lsg_set* qp = &q;
+  LSG_RC(stage_sets(s, &qp, 1, 0, false));
+  return size_state(s, 1, n, 1, 0);
+}
+
+int dev_create(lsg_ctx* c, int ord, int device, Dev** out) {
+  Dev* d = new Dev();
+  *out = d;
+  d->c = c;
+  d->device = device;
+  d->ord = ord;
+  LSG_HIPC(c, hipSetDevice(device));
+  LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_util, hipStreamNonBlocking));
+  for (int i = 0; i < LSG_SLOTS; i++) LSG_RC(slot_create(d, &d->slots[i], i, nullptr));
+  if (ord == 0) {
+    for (int i = 0; i < LSG_FE_STREAMS; i++) LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_fe[i], hipStreamNonBlocking));
+    for (int i = 0; i < LSG_FINALS; i++) LSG_RC(slot_create(d, &d->finals[i], i, d->s_fe[i % LSG_FE_STREAMS]));
+  }
+  return slot_create(d, &d->util, 0, d->s_util);
+}
+
+void dev_destroy(Dev* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  for (Slot& s : d->slots) slot_destroy(&s);
+  for (Slot& s : d->finals) slot_destroy(&s);
+  slot_destroy(&d->util);
+  free_dev(d->d_pktab);
+  free_dev(d->d_pktab_ok);
+  if (d->s_util) (void)hipStreamDestroy(d->s_util);
+  for (hipStream_t st : d->s_fe)
+    if (st) (void)hipStreamDestroy(st);
+  delete d;
+}
+
+// pubkey table rows first .. first+n-1 on one device
+int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, size_t n, std::vector<int32_t>& pkerr) {
+  lsg_ctx* c = d->c;
+  Slot* s = &d->util;
+  timer_reset(s);
+  LSG_HIPC(c, hipSetDevice(d->device));
+  const size_t need = first + n;
+  // tickets in flight read the table: drain the device before moving it or rewriting rows
+  // that may be read (an in-flight aggregate must never see a half-written row)
+  if (need > d->pktab_cap || first < d->pktab_n) LSG_HIPC(c, hipDeviceSynchronize());
+  if (need > d->pktab_cap) {
+    const size_t cap = std::max(std::max(need, 2 * d->pktab_cap), (size_t)1024);
+    DevBuf nt, nok;
+    LSG_HIPC(c, hipMalloc(&nt.p, 4 * W_G1P * cap));
+    g_allocs++;
+    nt.cap = 4 * W_G1P * cap;
+    hipError_t e = hipMalloc(&nok.p, cap);
+    if (e != hipSuccess) {
+      free_dev(nt);
+      return fail_c(c, "hipMalloc", e);
+    }
+    g_allocs++;
+    nok.cap = cap;
+    LSG_HIPC(c, hipMemset(nok.p, 0, cap));
+    if (d->pktab_n) {
+      LSG_HIPC(c, hipMemcpy(nt.p, d->d_pktab.p, 4 * W_G1P * d->pktab_n, hipMemcpyDeviceToDevice));
+      LSG_HIPC(c, hipMemcpy(nok.p, d->d_pktab_ok.p, d->pktab_n, hipMemcpyDeviceToDevice));
+    }
+    free_dev(d->d_pktab);
+    free_dev(d->d_pktab_ok);
+    d->d_pktab = nt;
+    d->d_pktab_ok = nok;
+    d->pktab_cap = cap;
+  }
+  LSG_RC(util_stage_keys(s, pks, pk_len, n));
+  // decode straight into the table rows first .. first + n - 1
+  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)n, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen),
+                                       P_<uint32_t>(d->d_pktab) + W_G1P * first, P_<int32_t>(s->d_pkerr), nullptr,
+                                       nullptr, 0u));
+  pkerr.assign(n, 0);
+  LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  std::vector<uint8_t> ok(n);
+  for (size_t k = 0; k < n; k++) ok[k] = pkerr[k] == 0 ? 1 : 0;
+  LSG_HIP(s, hipMemcpy(P_<uint8_t>(d->d_pktab_ok) + first, ok.data(), n, hipMemcpyHostToDevice));
+  d->pktab_n = std::max(d->pktab_n, need);
+  d->last = s;
+  return LSG_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- C ABI
+extern "C" {
+
+int lsg_init_devices(const int* device_ids, int n_devices, lsg_ctx** out) {
+  if (!out || !device_ids || n_devices < 1 || n_devices > LSG_MAX_DEVICES) return LSG_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return LSG_ERR_NO_DEVICE;
+  bool distinct = true;
+  for (int i = 0; i < n_devices; i++) {
+    const int dev = device_ids[i];
+    if (dev < 0 || dev >= count) return LSG_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return LSG_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LSG_ERR_NO_DEVICE;
+    for (int j = 0; j < i; j++)
+      if (device_ids[j] == dev) distinct = false;
+  }
+  lsg_ctx* c = new lsg_ctx();
+  c->n_dev = n_devices;
+  int rc = LSG_OK;
+  for (int i = 0; i < n_devices && !rc; i++) rc = dev_create(c, i, device_ids[i], &c->dev[i]);
+  if (!rc && distinct && (n_devices > 1 || force_exchange())) {
+    // the partial exchange of SURVEY.md 8e: one RCCL communicator per device, owned here
+    ncclResult_t r = ncclCommInitAll(c->comm, n_devices, device_ids);
+    if (r != ncclSuccess) {
+      c->err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+      rc = LSG_ERR_DEVICE;
+    } else {
+      c->rccl = true;
+    }
+  }
+  (void)hipSetDevice(device_ids[0]);
+  if (rc) {
+    lsg_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return LSG_OK;
+}
+
+int lsg_init(int device_ordinal, lsg_ctx** out) {
+  const int dev = device_ordinal < 0 ? 0 : device_ordinal;
+  return lsg_init_devices(&dev, 1, out);
+}
+
+int lsg_destroy(lsg_ctx* c) {
+  if (!c) return LSG_ERR_INVALID_ARG;
+  for (int d = 0; d < c->n_dev; d++) dev_destroy(c->dev[d]);
+  if (c->rccl)
+    for (int d = 0; d < c->n_dev; d++)
+      if (c->comm[d]) (void)ncclCommDestroy(c->comm[d]);
+  delete c;
+  return LSG_OK;
+}
+
+int lsg_device_count(lsg_ctx* c, int32_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  *n = c->n_dev;
+  return LSG_OK;
+}
+
+const char* lsg_last_error(lsg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int lsg_device_name(lsg_ctx* c, char* buf, size_t len) {
+  if (!c || !buf || !len) return LSG_ERR_INVALID_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->dev[0]->device) != hipSuccess) return LSG_ERR_DEVICE;
+  snprintf(buf, len, "%s (%s, %d CUs)%s", prop.name, prop.gcnArchName, prop.multiProcessorCount,
+           c->n_dev > 1 ? " x several" : "");
+  return LSG_OK;
+}
+
+int lsg_reserve(lsg_ctx* c, size_t max_sets, size_t max_pks, size_t max_msg_bytes, int32_t n_slots) {
+  if (!c || n_slots < 0) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  const int ns = std::min(n_slots == 0 ? LSG_SLOTS : n_slots, LSG_SLOTS);
+  for (int d = 0; d < c->n_dev; d++) {
+    LSG_HIPC(c, hipSetDevice(c->dev[d]->device));
+    for (int i = 0; i < ns; i++) {
+      Slot* s = &c->dev[d]->slots[i];
+      if (s->kind != SLOT_FREE) continue;
+      LSG_RC(size_inputs(s, max_sets, max_pks, max_msg_bytes));
+      // groups: as many as sets (the per-job phase of a failing package of single-set jobs)
+      LSG_RC(size_state(s, max_sets, max_pks, max_sets, max_sets / 256 + 1, true));
+      LSG_RC(ensure_host(s, s->h_mode, std::max(max_sets, (size_t)1)));
+      const size_t plan_words = 16 * max_sets + 4 * max_pks + 64 * 1024;
+      LSG_RC(ensure_host(s, s->h_plan, 4 * plan_words));
+      LSG_RC(ensure(s, s->d_plan, 4 * plan_words));
+      s->plan.reserve(plan_words);
+      for (int u = 0; u < 3; u++) {
+        const size_t W = u == 0 ? W_G1P : (u == 1 ? W_G2P : W_F12);
+        const size_t items = std::max(max_sets / 8 + 64, std::max(max_pks, max_sets) / 8 + 64);
+        for (int k = 0; k < 2; k++) LSG_RC(ensure(s, s->seg_tmp[u][k], 4 * W * items));
+      }
+      // timing events for a full submission, created up front
+      while (s->timers.size() < 192) {
+        Timer t;
+        LSG_HIPC(c, hipEventCreate(&t.a));
+        LSG_HIPC(c, hipEventCreate(&t.b));
+        s->timers.push_back(t);
+      }
+    }
+  }
+  LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
+  return LSG_OK;
+}
+
+int lsg_allocation_count(lsg_ctx* c, uint64_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  *n = g_allocs.load();
+  return LSG_OK;
+}
+
+int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_jobs && !jobs)) return LSG_ERR_INVALID_ARG;
+  for (size_t j = 0; j < n_jobs; j++)
+    if (jobs[j].n_sets && !jobs[j].sets) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  return submit_pkg(c, jobs, n_jobs, seed, ticket);
+}
+
+int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results, lsg_stats* stats) {
+  if (!c) return LSG_ERR_INVALID_ARG;
+  if (int prc = presync_pkg(c, ticket, false)) return prc;
+  LSG_ENTER(c);
+  const int p = ticket_pkg(c, ticket);
+  if (p < 0) return LSG_ERR_INVALID_ARG;
+  const uint32_t nj = c->dev[0]->slots[p].stats.reserved;
+  if (nj && !results) return LSG_ERR_INVALID_ARG;
+  if (node_valid != -1 && c->n_dev > 1) {
+    c->err = "lsg_wait_jobs_node: a multi-device context runs its own node check";
+    return LSG_ERR_INVALID_ARG;
+  }
+  return wait_pkg(c, p, node_valid == -1 ? -2 : (node_valid ? 1 : 0), results, stats);
+}
+
+int lsg_wait_jobs(lsg_ctx* c, lsg_ticket ticket, lsg_job_result* results, lsg_stats* stats) {
+  return lsg_wait_jobs_node(c, ticket, -1, results, stats);
+}
+
+int lsg_jobs_partial(lsg_ctx* c, lsg_ticket ticket, uint8_t* out576, int32_t* has_batch) {
+  if (!c || !out576) return LSG_ERR_INVALID_ARG;
+  if (c->n_dev > 1) {
+    c->err = "lsg_jobs_partial: a multi-device context exchanges its partials itself";
+    return LSG_ERR_INVALID_ARG;
+  }
+  if (int prc = presync_pkg(c, ticket, true)) return prc;
+  LSG_ENTER(c);
+  const int p = ticket_pkg(c, ticket);
+  if (p < 0) return LSG_ERR_INVALID_ARG;
+  Slot* s = &c->dev[0]->slots[p];
+  const bool has = !s->phA.groups.empty() && s->big_g >= 0;
+  if (has)
+    memcpy(out576, H_<uint8_t>(s->h_blob) + 576 * (size_t)s->big_g, 576);
+  else
+    memcpy(out576, fp12_one_blob(), 576);
+  if (has_batch) *has_batch = has ? 1 : 0;
+  return LSG_OK;
+}
+
+int lsg_verify_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_job_result* results,
+                    lsg_stats* stats) {
+  if (!c || (n_jobs && (!jobs || !results))) return LSG_ERR_INVALID_ARG;
+  lsg_ticket t;
+  int rc = lsg_submit_jobs(c, jobs, n_jobs, seed, &t);
+  if (rc) return rc;
+  return lsg_wait_jobs(c, t, results, stats);
+}
+
+int lsg_verify_sets(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, lsg_job_result* result) {
+  if (!c || !result || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+  lsg_job job;
+  job.sets = sets;
+  job.n_sets = (uint32_t)n_sets;
+  job.flags = 0;
+  return lsg_verify_jobs(c, &job, 1, seed, result, nullptr);
+}
+
+int lsg_pipeline_slots(lsg_ctx* c, int32_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  *n = LSG_SLOTS;
+  return LSG_OK;
+}
+
+int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
+  if (!c || !done) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  std::vector<hipEvent_t> evs;
+  if (Slot* f = ticket_final(c, ticket)) {
+    evs.push_back(f->ev_done);
+  } else {
+    const int p = ticket_pkg(c, ticket);
+    if (p < 0) return LSG_ERR_INVALID_ARG;
+    for (int d = 0; d < c->n_dev; d++) evs.push_back(c->dev[d]->slots[p].ev_done);
+  }
+  *done = 1;
+  for (hipEvent_t e : evs) {
+    hipError_t r = hipEventQuery(e);
+    if (r == hipErrorNotReady) {
+      *done = 0;
+      return LSG_OK;
+    }
+    if (r != hipSuccess) return fail_c(c, "hipEventQuery", r);
+  }
+  return LSG_OK;
+}
+
+// one shard's partial (sync): all sets as one batchable job
+int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t seed, uint8_t* out576,
+                      int32_t* set_err, int32_t* any_error) {
+  if (!c || !out576 || !any_error || (n_sets && !sets)) return LSG_ERR_INVALID_ARG;
+  if (c->n_dev > 1) {
+    c->err = "lsg_batch_partial: single-device contexts only";
+    return LSG_ERR_INVALID_ARG;
+  }
+  lsg_ticket t;
+  {
+    LSG_ENTER(c);
+    lsg_job job;
+    job.sets = sets;
+    job.n_sets = (uint32_t)n_sets;
+    job.flags = LSG_JOB_BATCHABLE;
+    int rc = submit_pkg(c, &job, 1, seed, &t);
+    if (rc) return rc;
+  }
+  if (int prc = presync_pkg(c, t, false)) return prc;
+  LSG_ENTER(c);
+  const int p = ticket_pkg(c, t);
+  if (p < 0) return LSG_ERR_INVALID_ARG;
+  Slot* s = &c->dev[0]->slots[p];
+  const SetStatus ss = read_status(s);
+  *any_error = 0;
+  for (size_t i = 0; i < n_sets; i++) {
+    const int32_t e = set_error(ss, i);
+    if (set_err) set_err[i] = e;
+    if (e) *any_error = 1;
+  }
+  for (size_t k = 0; k < s->n_pks; k++)
+    if (ss.pkerr[k]) *any_error = 1;
+  if (s->big_g >= 0)
+    memcpy(out576, H_<uint8_t>(s->h_blob) + 576 * (size_t)s->big_g, 576);
+  else
+    memcpy(out576, fp12_one_blob(), 576);
+  s->kind = SLOT_FREE;
+  c->dev[0]->last = s;
+  return LSG_OK;
+}
+
+int lsg_final_submit_groups(lsg_ctx* c, const uint8_t* partials576, size_t n_groups, size_t per_group,
+                            lsg_ticket* ticket) {
+  if (!c || !ticket || (n_groups && per_group && !partials576) || (n_groups && !per_group)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = nullptr;
+  for (int i = 0; i < LSG_FINALS && !s; i++)
+    if (c->dev[0]->finals[i].kind == SLOT_FREE) s = &c->dev[0]->finals[i];
+  if (!s) {
+    c->err = "all final-exponentiation entries are busy";
+    return LSG_ERR_BUSY;
+  }
+  int rc = submit_final(s, partials576, n_groups, per_group);
+  if (rc) {
+    sync_slot(s);
+    return rc;
+  }
+  uint64_t serial;
+  *ticket = make_ticket(c, SLOT_FINAL, s->index, &serial);
+  s->kind = SLOT_FINAL;
+  s->serial = serial;
+  return LSG_OK;
+}
+
+int lsg_final_submit(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+  return lsg_final_submit_groups(c, partials576, n_partials ? 1 : 0, n_partials, ticket);
+}
+
+static int final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid, bool single) {
+  if (!c || !valid) return LSG_ERR_INVALID_ARG;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    Slot* s = ticket_final(c, ticket);
+    if (!s) return LSG_ERR_INVALID_ARG;
+    ev = s->ev_done;
+  }
+  (void)hipSetDevice(c->dev[0]->device);
+  hipError_t e = hipEventSynchronize(ev);
+  if (e != hipSuccess) return fail_c(c, "hipEventSynchronize", e);
+  LSG_ENTER(c);
+  Slot* s = ticket_final(c, ticket);
+  if (!s) return LSG_ERR_INVALID_ARG;
+  if (single && s->n_sets > 1) {
+    c->err = "ticket carries several groups: use lsg_final_wait_groups";
+    return LSG_ERR_INVALID_ARG;
+  }
+  if (!s->n_sets) valid[0] = 0;
+  for (size_t g = 0; g < s->n_sets; g++) valid[g] = H_<int32_t>(s->h_verdict)[g];
+  s->kind = SLOT_FREE;
+  c->dev[0]->last = s;
+  return LSG_OK;
+}
+
+int lsg_final_wait_groups(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) { return final_wait(c, ticket, valid, false); }
+int lsg_final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid) { return final_wait(c, ticket, valid, true); }
+
+int lsg_final_verify(lsg_ctx* c, const uint8_t* partials576, size_t n_partials, int32_t* valid) {
+  if (!c || !valid || (n_partials && !partials576)) return LSG_ERR_INVALID_ARG;
+  lsg_ticket t;
+  int rc = lsg_final_submit(c, partials576, n_partials, &t);
+  if (rc) return rc;
+  return lsg_final_wait(c, t, valid);
+}
+
+int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96,
+                          int32_t* err_code) {
+  if (!c || !out96 || !err_code || (n && !pks)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  timer_reset(s);
+  *err_code = 0;
+  if (n == 0) {
+    *err_code = LSG_ERR_EMPTY_AGGREGATE;
+    return LSG_OK;
+  }
+  s->plan.clear();
+  LSG_RC(util_stage_keys(s, pks, pk_len, n));
+  std::vector<int32_t> off{0}, len{(int32_t)n};
+  SegPlan P = plan_seg(s->plan, 0, off, len, false, 0, 0);
+  LSG_RC(upload_plan(s));
+  const int np = (int)n;
+  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen),
+                                       P_<uint32_t>(s->d_pkp), P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab),
+                                       P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
+  LSG_RC(run_seg(s, 0, "g1_aggregate", P, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
+  KL(s, "k_g1p_to_bytes", lsgk::g1p_to_bytes(S_(s), 1, P_<uint32_t>(s->d_agg), P_<uint8_t>(s->d_Fb)));
+  std::vector<int32_t> pkerr(n);
+  LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_Fb.p, 96, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  d->last = s;
+  for (size_t k = 0; k < n; k++)
+    if (pkerr[k]) {
+      *err_code = pkerr[k];
+      break;
+    }
+  return LSG_OK;
+}
+
+int lsg_pubkey_table_set(lsg_ctx* c, size_t first, const uint8_t* pks, uint32_t pk_len, size_t n, int32_t* err) {
+  if (!c || (n && !pks) || (pk_len != 48 && pk_len != 96) || first + n > 0xffffffffull) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  if (n == 0) return LSG_OK;
+  std::vector<int32_t> pkerr;
+  for (int d = 0; d < c->n_dev; d++) LSG_RC(dev_pktab_set(c->dev[d], first, pks, pk_len, n, pkerr));
+  (void)hipSetDevice(c->dev[0]->device);
+  if (err)
+    for (size_t k = 0; k < n; k++) err[k] = pkerr[k];
+  return LSG_OK;
+}
+
+int lsg_pubkey_table_size(lsg_ctx* c, size_t* n) {
+  if (!c || !n) return LSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *n = c->dev[0]->pktab_n;
+  return LSG_OK;
+}
+
+int lsg_pubkey_validate(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96, int32_t* err) {
+  if (!c || !err || (n && !pks) || (pk_len != 48 && pk_len != 96) || n > 0x7fffffffull) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  LSG_RC(util_stage_keys(s, pks, pk_len, n));
+  LSG_RC(ensure(s, s->d_ub, 96 * n));
+  KL(s, "k_pk_validate", lsgk::pk_validate(S_(s), (int)n, P_<uint8_t>(s->d_pk), pk_len, P_<uint32_t>(s->d_pkp),
+                                           P_<int32_t>(s->d_pkerr)));
+  LSG_HIP(s, hipMemcpyAsync(err, s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  if (out96) {
+    KL(s, "k_g1p_to_bytes", lsgk::g1p_to_bytes(S_(s), (int)n, P_<uint32_t>(s->d_pkp), P_<uint8_t>(s->d_ub)));
+    LSG_HIP(s, hipMemcpyAsync(out96, s->d_ub.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  }
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  d->last = s;
+  return LSG_OK;
+}
+
+int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst,
+                   uint32_t dst_len, uint8_t* out192) {
+  if (!c || !out192 || (n && msg_len && !msgs) || dst_len > 255 || (dst_len && !dst)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  LSG_RC(util_hash(s, msgs, msg_len, n, dst, dst_len));
+  LSG_RC(ensure(s, s->d_aux, 192 * n));
+  const int nn = (int)n;
+  KL(s, "k_g2a_to_bytes",
+     lsgk::g2a_to_bytes(S_(s), nn, P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf), P_<uint8_t>(s->d_aux)));
+  LSG_HIP(s, hipMemcpyAsync(out192, s->d_aux.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  d->last = s;
+  return LSG_OK;
+}
+
+// Signature.fromBytes(sig, affine, validate) for n signatures (subgroup check when validate)
+static int sig_decode_impl(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, bool validate, Slot** out) {
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  *out = s;
+  std::vector<lsg_set> sets(n);
+  std::vector<const lsg_set*> sp(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&sets[i], 0, sizeof(lsg_set));
+    sets[i].sig = sigs + (size_t)sig_len * i;
+    sets[i].sig_len = sig_len;
+    sp[i] = &sets[i];
+  }
+  LSG_RC(stage_sets(s, sp.data(), n, 0, false));
+  LSG_RC(size_state(s, n, 0, 1, 0));
+  const int nn = (int)n;
+  KL(s, "k_sig_decode", lsgk::sig_decode(S_(s), nn, P_<uint8_t>(s->d_sig), P_<uint32_t>(s->d_siglen),
+                                         P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf), P_<int32_t>(s->d_seterr)));
+  if (validate)
+    KL(s, "k_sig_subgroup", lsgk::sig_subgroup(S_(s), nn, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                               P_<int32_t>(s->d_seterr)));
+  return LSG_OK;
+}
+
+int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, uint8_t* out192, int32_t* err) {
+  if (!c || !out192 || !err || (n && !sigs)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  timer_reset(&c->dev[0]->util);
+  if (n == 0) return LSG_OK;
+  Slot* s;
+  LSG_RC(sig_decode_impl(c, sigs, sig_len, n, true, &s));
+  LSG_RC(ensure(s, s->d_aux, 192 * n));
+  KL(s, "k_g2a_to_bytes", lsgk::g2a_to_bytes(S_(s), (int)n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                             P_<uint8_t>(s->d_aux)));
+  LSG_HIP(s, hipMemcpyAsync(out192, s->d_aux.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(err, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->dev[0]->last = s;
+  return LSG_OK;
+}
+
+// G2 signature aggregation for the op pools: n_groups Signature.aggregate
+// calls in one pass -- decode without the subgroup check (signatureFromBytesNoCheck,
+// opPools/utils.ts:32-34), one segmented reduction, one compression per group
+int lsg_aggregate_signatures(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, const uint32_t* offsets,
+                             size_t n_groups, uint8_t* out96, int32_t* err) {
+  if (!c || !offsets || (n_groups && (!out96 || !err)) || offsets[0] != 0 || n_groups > 0x7fffffffull)
+    return LSG_ERR_INVALID_ARG;
+  for (size_t g = 0; g < n_groups; g++)
+    if (offsets[g + 1] < offsets[g]) return LSG_ERR_INVALID_ARG;
+  const size_t n = offsets[n_groups];
+  if (n && !sigs) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  timer_reset(&c->dev[0]->util);
+  for (size_t g = 0; g < n_groups; g++) {
+    err[g] = offsets[g + 1] == offsets[g] ? LSG_ERR_EMPTY_AGGREGATE : 0;
+    memset(out96 + 96 * g, 0, 96);
+  }
+  if (n == 0) return LSG_OK;
+  Slot* s;
+  LSG_RC(sig_decode_impl(c, sigs, sig_len, n, false, &s));
+  LSG_RC(size_state(s, n, 0, n_groups, 0));
+  s->plan.clear();
+  std::vector<int32_t> off(n_groups), len(n_groups);
+  for (size_t g = 0; g < n_groups; g++) {
+    off[g] = (int32_t)offsets[g];
+    len[g] = (int32_t)(offsets[g + 1] - offsets[g]);
+  }
+  SegPlan P = plan_seg(s->plan, 1, off, len, false, 0, 0);
+  LSG_RC(upload_plan(s));
+  LSG_RC(ensure(s, s->d_aux, 96 * n_groups));
+  const int nn = (int)n;
+  KL(s, "k_sig_prep", lsgk::sig_prep(S_(s), nn, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                     P_<int32_t>(s->d_seterr), nullptr, nullptr, nullptr, P_<uint32_t>(s->d_rs)));
+  LSG_RC(run_seg(s, 1, "g2_aggregate", P, P_<uint32_t>(s->d_rs), P_<uint32_t>(s->d_S)));
+  KL(s, "k_g2p_compress",
+     lsgk::g2p_compress(S_(s), (int)n_groups, P_<uint32_t>(s->d_S), P_<uint8_t>(s->d_aux)));
+  std::vector<int32_t> serr(n);
+  std::vector<uint8_t> blob(96 * n_groups);
+  LSG_HIP(s, hipMemcpyAsync(serr.data(), s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(blob.data(), s->d_aux.p, 96 * n_groups, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  c->dev[0]->last = s;
+  // Signature.aggregate throws on the first signature that fails to deserialize
+  for (size_t g = 0; g < n_groups; g++) {
+    if (offsets[g + 1] == offsets[g]) continue;
+    for (uint32_t i = offsets[g]; i < offsets[g + 1] && !err[g]; i++) err[g] = serr[i];
+    if (!err[g]) memcpy(out96 + 96 * g, blob.data() + 96 * g, 96);
+  }
+  return LSG_OK;
+}
+
+// SSZ signing roots; kind 0: object roots given, 1: AttestationData bytes
+static int signing_roots(lsg_ctx* c, int kind, const uint8_t* objs, size_t n, const uint8_t* domain, uint32_t dstride,
+                         uint8_t* out32) {
+  const size_t ob = kind ? 128 : 32;
+  if (!c || !domain || (dstride != 0 && dstride != 32) || (n && (!objs || !out32)) || n > 0x7fffffffull)
+    return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  const size_t nd = dstride ? n : 1;
+  LSG_RC(ensure(s, s->d_aux, ob * n + 32 * nd));
+  LSG_RC(ensure(s, s->d_Fb, 32 * n));
+  uint8_t* d_obj = P_<uint8_t>(s->d_aux);
+  uint8_t* d_dom = d_obj + ob * n;
+  LSG_HIP(s, hipMemcpyAsync(d_obj, objs, ob * n, hipMemcpyHostToDevice, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(d_dom, domain, 32 * nd, hipMemcpyHostToDevice, s->st[0]));
+  const int nn = (int)n;
+  if (kind)
+    KL(s, "k_attestation_signing_root",
+       lsgk::attestation_signing_root(S_(s), nn, d_obj, d_dom, dstride, P_<uint8_t>(s->d_Fb)));
+  else
+    KL(s, "k_signing_root", lsgk::signing_root(S_(s), nn, d_obj, d_dom, dstride, P_<uint8_t>(s->d_Fb)));
+  LSG_HIP(s, hipMemcpyAsync(out32, s->d_Fb.p, 32 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  d->last = s;
+  return LSG_OK;
+}
+
+int lsg_signing_roots(lsg_ctx* c, const uint8_t* roots32, size_t n, const uint8_t* domain32, uint32_t domain_stride,
+                      uint8_t* out32) {
+  return signing_roots(c, 0, roots32, n, domain32, domain_stride, out32);
+}
+
+int lsg_attestation_signing_roots(lsg_ctx* c, const uint8_t* data128, size_t n, const uint8_t* domain32,
+                                  uint32_t domain_stride, uint8_t* out32) {
+  return signing_roots(c, 1, data128, n, domain32, domain_stride, out32);
+}
+
+int lsg_sign(lsg_ctx* c, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96) {
+  if (!c || !out96 || (n && (!sks32 || !msgs))) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->dev[0]->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  LSG_RC(util_hash(s, msgs, msg_len, n, DST_POP, DST_POP_LEN));
+  LSG_RC(ensure(s, s->d_aux, 96 * n));
+  LSG_RC(ensure(s, s->d_Fb, 32 * n));
+  LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, sks32, 32 * n, hipMemcpyHostToDevice, s->st[0]));
+  KL(s, "k_sign", lsgk::sign(S_(s), (int)n, P_<uint8_t>(s->d_Fb), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_aux)));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_aux.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  return LSG_OK;
+}
+
+int lsg_sk_to_pk(lsg_ctx* c, const uint8_t* sks32, size_t n, uint8_t* out96) {
+  if (!c || !out96 || (n && !sks32)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->dev[0]->util;
+  timer_reset(s);
+  if (n == 0) return LSG_OK;
+  LSG_RC(ensure(s, s->d_aux, 96 * n));
+  LSG_RC(ensure(s, s->d_Fb, 32 * n));
+  LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, sks32, 32 * n, hipMemcpyHostToDevice, s->st[0]));
+  KL(s, "k_sk_to_pk", lsgk::sk_to_pk(S_(s), (int)n, P_<uint8_t>(s->d_Fb), P_<uint8_t>(s->d_aux)));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_aux.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  return LSG_OK;
+}
+
+int lsg_probe_fp_mul_rate(lsg_ctx* c, double* fp_mul_per_s, double* mad_per_s) {
+  if (!c || !fp_mul_per_s || !mad_per_s) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->dev[0]->util;
+  hipDeviceProp_t prop;
+  LSG_HIP(s, hipGetDeviceProperties(&prop, c->dev[0]->device));
+  const int items = prop.multiProcessorCount * 32 * 32;  // 32 waves per CU, 32 pair items each
+  LSG_RC(ensure(s, s->d_aux, 4 * W_FP * (size_t)items));
+  std::vector<uint32_t> init(W_FP * (size_t)items, 0);
+  for (size_t i = 0; i < init.size(); i += 4) init[i] = (uint32_t)(i * 2654435761u) & 0x1fffffffu;  // small values < p
+  LSG_HIP(s, hipMemcpy(s->d_aux.p, init.data(), 4 * init.size(), hipMemcpyHostToDevice));
+  const int iters = 64;
+  hipStream_t S = s->st[0];
+  LSG_HIP(s, lsgk::probe_fp_mul(S, items, 2, P_<uint32_t>(s->d_aux)));
+  hipEvent_t a, b;
+  LSG_HIP(s, hipEventCreate(&a));
+  LSG_HIP(s, hipEventCreate(&b));
+  LSG_HIP(s, hipEventRecord(a, S));
+  LSG_HIP(s, lsgk::probe_fp_mul(S, items, iters, P_<uint32_t>(s->d_aux)));
+  LSG_HIP(s, hipEventRecord(b, S));
+  LSG_HIP(s, hipEventSynchronize(b));
+  float ms = 0;
+  LSG_HIP(s, hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *fp_mul_per_s = (double)items * iters * 4.0 / (ms * 1e-3);
+  *mad_per_s = *fp_mul_per_s * 300.0;
+  return LSG_OK;
+}
+
+int lsg_probe_mad_peak(lsg_ctx* c, double* mad_per_s) {
+  if (!c || !mad_per_s) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = &c->dev[0]->util;
+  hipDeviceProp_t prop;
+  LSG_HIP(s, hipGetDeviceProperties(&prop, c->dev[0]->device));
+  const int blocks = prop.multiProcessorCount * 32;  // 32 waves per CU (8 per SIMD)
+  const size_t threads = (size_t)blocks * 256;
+  LSG_RC(ensure(s, s->d_aux, 8 * threads));
+  hipStream_t S = s->st[0];
+  const int iters = 4096;
+  LSG_HIP(s, lsgk::probe_mad(S, blocks, 16, 3u, P_<uint64_t>(s->d_aux)));
+  hipEvent_t a, b;
+  LSG_HIP(s, hipEventCreate(&a));
+  LSG_HIP(s, hipEventCreate(&b));
+  LSG_HIP(s, hipEventRecord(a, S));
+  LSG_HIP(s, lsgk::probe_mad(S, blocks, iters, 5u, P_<uint64_t>(s->d_aux)));
+  LSG_HIP(s, hipEventRecord(b, S));
+  LSG_HIP(s, hipEventSynchronize(b));
+  float ms = 0;
+  LSG_HIP(s, hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *mad_per_s = (double)threads * iters * 16.0 / (ms * 1e-3);
+  return LSG_OK;
+}
+
+int lsg_last_kernel_times(lsg_ctx* c, const char** names, double* ms, int max) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const Slot* s = c->dev[0]->last;
+  if (!s) return 0;
+  for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(s->st[k]);
+  int n = 0;
+  for (size_t i = 0; i < s->ntimers && n < max; i++) {
+    float t = 0;
+    if (hipEventElapsedTime(&t, s->timers[i].a, s->timers[i].b) != hipSuccess) t = -1;
+    if (names) names[n] = s->timers[i].name;
+    if (ms) ms[n] = t;
+    n++;
+  }
+  return n;
+}
+
+int lsg_assign_jobs(const uint32_t* job_sets, size_t n_jobs, int32_t n_devices, int32_t* owner) {
+  if ((n_jobs && (!job_sets || !owner)) || n_devices < 1) return LSG_ERR_INVALID_ARG;
+  assign_jobs(job_sets, n_jobs, n_devices, owner);
+  return LSG_OK;
+}
+
+}  // extern "C"

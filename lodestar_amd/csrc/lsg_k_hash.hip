@@ -1,0 +1,202 @@
+// lsg_k_hash.hip -- hash_to_G2 kernels (RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_ with the POP
+// DST, blst's Hash_to_G2 inside Pairing.mul_n_aggregate under
+// packages/beacon-node/src/chain/bls/maybeBatch.ts:18,37) and the SSZ
+// signing roots of SURVEY.md 8f(3) (util/signingRoot.ts:7-13).
+//
+//   k_expand_msg   expand_message_xmd(msg_i, DST, 256), one thread per set (SHA-256)
+//   k_h2c_prep     hash_to_field -> u0, u1; norms N(tv1(u0)), N(tv1(u1)) for one batched inversion
+//   k_h2c_map      SSWU x2 (shared-norm square root) -> 3-isogeny -> Q0 + Q1
+//   k_h2c_clear    clear_cofactor (psi form); N(Z) for the second batched inversion
+//   k_h2c_affine   (X, Y) * conj(Z) / N(Z)
+#include "lsg_kcommon.hpp"
+
+// expand_message_xmd(msg_i, DST, 256): one thread per set (byte-serial SHA-256)
+__global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restrict__ msg,
+                                                    const uint32_t* __restrict__ msg_off,
+                                                    const uint32_t* __restrict__ msg_len,
+                                                    const uint8_t* __restrict__ dst, uint32_t dst_len,
+                                                    uint8_t* __restrict__ ub) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  uint8_t out[256];
+  expand_message_xmd_256(out, msg + msg_off[i], msg_len[i], dst, dst_len);
+  uint32_t* o = (uint32_t*)(ub + 256 * i);
+  for (int k = 0; k < 64; k++) {
+    uint32_t w;
+    __builtin_memcpy(&w, out + 4 * k, 4);
+    o[k] = w;
+  }
+}
+
+// stage 1: u0, u1 = hash_to_field(expand_message_xmd); norms N(tv1(u0)), N(tv1(u1)) at slots
+// 2i, 2i+1 for the batched inversion
+struct h2c_u_t {
+  fp2_t u0, u1;
+};
+static_assert(lane_words<h2c_u_t>() == lsgl::W_H2CU, "layout: hash_to_field");
+
+__global__ void LSG_KERNEL_ATTR k_h2c_prep(int n, const uint8_t* __restrict__ ub, uint32_t* __restrict__ U,
+                                           uint32_t* __restrict__ norms) {
+  LANE_ITEM(n);
+  (void)lead;
+  const uint8_t* b = ub + 256 * item;
+  h2c_u_t u;
+  u.u0 = fp2_make(fp_from_be64_mod(b), fp_from_be64_mod(b + 64));
+  u.u1 = fp2_make(fp_from_be64_mod(b + 128), fp_from_be64_mod(b + 192));
+  lane_store(U, item, u);
+  lane_store(norms, 2 * item, fp2_norm(sswu_tv1(u.u0)));
+  lane_store(norms, 2 * item + 1, fp2_norm(sswu_tv1(u.u1)));
+}
+
+// stage 2: SSWU x2 (with the batched 1/N(tv1)) -> 3-isogeny -> add, projective.  Split from
+// the cofactor clearing so that neither kernel holds the other's live state (the fused kernel
+// spilled 757 registers).
+__global__ void LSG_KERNEL_ATTR k_h2c_map(int n, const uint32_t* __restrict__ U, const uint32_t* __restrict__ ninv,
+                                          uint32_t* __restrict__ Hp) {
+  LANE_ITEM(n);
+  (void)lead;
+  h2c_u_t u = lane_load<h2c_u_t>(U, item);
+  g2p_t q0 = iso_map3(map_to_curve_sswu_ni(u.u0, lane_load<fp_t>(ninv, 2 * item)));
+  g2p_t q1 = iso_map3(map_to_curve_sswu_ni(u.u1, lane_load<fp_t>(ninv, 2 * item + 1)));
+  lane_store(Hp, item, g2_add(q0, q1));
+}
+
+// stage 2b: clear_cofactor in place; zN_i = N(Z) (0 at infinity) for the batched inversion
+__global__ void LSG_KERNEL_ATTR k_h2c_clear(int n, uint32_t* __restrict__ Hp, uint32_t* __restrict__ zN,
+                                            uint8_t* __restrict__ hinf) {
+  LANE_ITEM(n);
+  g2p_t q = clear_cofactor_g2(lane_load<g2p_t>(Hp, item));
+  bool is_inf = proj_is_inf(q);
+  lane_store(Hp, item, q);
+  lane_store(zN, item, is_inf ? fp_zero() : fp2_norm(q.Z));
+  if (lead) hinf[item] = is_inf ? 1 : 0;
+}
+
+// stage 3: H affine = (X, Y) * conj(Z) / N(Z)   (= proj_to_aff, 1/Z = conj(Z) / N(Z))
+__global__ void LSG_KERNEL_ATTR k_h2c_affine(int n, const uint32_t* __restrict__ Hp, const uint32_t* __restrict__ ninv,
+                                             const uint8_t* __restrict__ hinf, uint32_t* __restrict__ H) {
+  LANE_ITEM(n);
+  (void)lead;
+  g2p_t q = lane_load<g2p_t>(Hp, item);
+  g2a_t a;
+  if (hinf[item]) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    fp2_t zi = fp2_inv_with_norm_inv(q.Z, lane_load<fp_t>(ninv, item));
+    a.x = fp2_mul(q.X, zi);
+    a.y = fp2_mul(q.Y, zi);
+  }
+  lane_store(H, item, a);
+}
+
+// ---- SSZ signing roots, one thread per object.  Chunks are 8 big-endian
+// SHA-256 words; every node is SHA-256 of exactly 64 bytes, so its second block is the
+// constant padding block of a 512-bit message.
+LSG_INL void ssz_hash2(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  uint32_t blk[16];
+  for (int k = 0; k < 8; k++) {
+    blk[k] = a[k];
+    blk[8 + k] = b[k];
+  }
+  sha256_compress(st, blk);
+  for (int k = 0; k < 16; k++) blk[k] = 0;
+  blk[0] = 0x80000000u;
+  blk[15] = 512;
+  sha256_compress(st, blk);
+  for (int k = 0; k < 8; k++) out[k] = st[k];
+}
+
+// `len` (<= 32) bytes at p as a zero-padded SSZ chunk
+LSG_INL void ssz_chunk(uint32_t* w, const uint8_t* p, int len) {
+  for (int k = 0; k < 8; k++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4; j++) v = (v << 8) | (4 * k + j < len ? p[4 * k + j] : 0u);
+    w[k] = v;
+  }
+}
+
+LSG_INL void ssz_store(uint8_t* out, const uint32_t* w) { be_words_to_bytes(out, w, 8); }
+
+// hash_tree_root(SigningData{objectRoot, domain}) (util/signingRoot.ts:7-13)
+__global__ void __launch_bounds__(64) k_signing_root(int n, const uint8_t* __restrict__ roots,
+                                                     const uint8_t* __restrict__ domains, uint32_t dstride,
+                                                     uint8_t* __restrict__ out32) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  uint32_t r[8], d[8], o[8];
+  ssz_chunk(r, roots + 32 * i, 32);
+  ssz_chunk(d, domains + dstride * i, 32);
+  ssz_hash2(r, d, o);
+  ssz_store(out32 + 32 * i, o);
+}
+
+// getAttestationDataSigningRoot (signatureSets/indexedAttestation.ts:11-19) from the SSZ
+// serialization of phase0.AttestationData (128 bytes: slot u64, index u64, beaconBlockRoot,
+// source {epoch u64, root}, target {epoch u64, root}): 5 fields -> 8 leaves, 3 levels, then
+// SigningData -- 10 node hashes per object
+__global__ void __launch_bounds__(64) k_attestation_signing_root(int n, const uint8_t* __restrict__ data,
+                                                                 const uint8_t* __restrict__ domains,
+                                                                 uint32_t dstride, uint8_t* __restrict__ out32) {
+  size_t i = gtid();
+  if (i >= (size_t)n) return;
+  const uint8_t* a = data + 128 * i;
+  uint32_t l0[8], l1[8], l2[8], l3[8], l4[8], t[8], z[8], z1[8], h01[8], h23[8], h45[8];
+  for (int k = 0; k < 8; k++) z[k] = 0;
+  ssz_chunk(l0, a, 8);        // slot
+  ssz_chunk(l1, a + 8, 8);    // index
+  ssz_chunk(l2, a + 16, 32);  // beaconBlockRoot
+  ssz_chunk(t, a + 48, 8);    // source = Checkpoint{epoch, root}
+  ssz_chunk(l3, a + 56, 32);
+  ssz_hash2(t, l3, l3);
+  ssz_chunk(t, a + 88, 8);  // target
+  ssz_chunk(l4, a + 96, 32);
+  ssz_hash2(t, l4, l4);
+  ssz_hash2(z, z, z1);  // leaves 5..7 are zero chunks
+  ssz_hash2(l0, l1, h01);
+  ssz_hash2(l2, l3, h23);
+  ssz_hash2(l4, z, h45);
+  ssz_hash2(h01, h23, h01);
+  ssz_hash2(h45, z1, h45);
+  ssz_hash2(h01, h45, t);  // AttestationData.hashTreeRoot
+  ssz_chunk(z, domains + dstride * i, 32);
+  ssz_hash2(t, z, t);
+  ssz_store(out32 + 32 * i, t);
+}
+
+namespace lsgk {
+hipError_t expand_msg(hipStream_t st, int n, const uint8_t* msg, const uint32_t* off, const uint32_t* len,
+                      const uint8_t* dst, uint32_t dst_len, uint8_t* ub) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_expand_msg, dim3((n + 63) / 64), dim3(64), 0, st, n, msg, off, len, dst, dst_len, ub);
+  return hipGetLastError();
+}
+hipError_t h2c_prep(hipStream_t st, int n, const uint8_t* ub, uint32_t* U, uint32_t* norms) {
+  LSG_LAUNCH_ITEMS(k_h2c_prep, n, st, n, ub, U, norms);
+}
+hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* ninv, uint32_t* Hp) {
+  LSG_LAUNCH_ITEMS(k_h2c_map, n, st, n, U, ninv, Hp);
+}
+hipError_t h2c_clear(hipStream_t st, int n, uint32_t* Hp, uint32_t* zN, uint8_t* hinf) {
+  LSG_LAUNCH_ITEMS(k_h2c_clear, n, st, n, Hp, zN, hinf);
+}
+hipError_t h2c_affine(hipStream_t st, int n, const uint32_t* Hp, const uint32_t* ninv, const uint8_t* hinf,
+                      uint32_t* H) {
+  LSG_LAUNCH_ITEMS(k_h2c_affine, n, st, n, Hp, ninv, hinf, H);
+}
+hipError_t signing_root(hipStream_t st, int n, const uint8_t* roots, const uint8_t* domains, uint32_t dstride,
+                        uint8_t* out32) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_signing_root, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, domains, dstride, out32);
+  return hipGetLastError();
+}
+hipError_t attestation_signing_root(hipStream_t st, int n, const uint8_t* data, const uint8_t* domains,
+                                    uint32_t dstride, uint8_t* out32) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_attestation_signing_root, dim3((n + 63) / 64), dim3(64), 0, st, n, data, domains, dstride,
+                     out32);
+  return hipGetLastError();
+}
+}  // namespace lsgk

@@ -1,0 +1,202 @@
+// lsg_k_reduce.hip -- segmented reductions of lane-form values (G1/G2 sums, Fp12 products),
+// batched field inversions, canonical-blob conversions and the roofline probes.
+//
+// The segmented reduction serves every "sum over a list" of the path with one launch per pass:
+//   PublicKey.aggregate of each set's keys      (utils.ts:11)      G1 add
+//   the RLC bucket MSM: buckets, per-bit sums   (blst mul_n_aggregate; 8a M4)      G2 add
+//   small groups' signature sums, op-pool sums  (8a M4, 8f(4))                     G2 add
+//   each group's Miller product                 (blst miller_loop_n/commit; 8a M5) Fp12 mul
+// A chunk (a list of up to ips x F elements) belongs to 2^ips_log2 lane pairs of one wave:
+// pair j folds elements j, j + ips, j + 2 ips, ... serially (every fold is a full-width
+// SIMD operation), then the ips partial values are combined by a butterfly over lanes
+// (shuffles, no LDS round trip).  Segments longer than one chunk get a second pass over the
+// chunk results (lsg_host.hip plan_seg), so a reduction is one or two launches instead of
+// one launch per tree level.
+#include "lsg_kcommon.hpp"
+
+template <class T>
+LSG_DEVI T shfl_xor_t(const T& v, int lane_mask) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = (uint32_t)__shfl_xor((int)w[k], lane_mask, 64);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+
+template <int OP>
+struct seg_op;
+template <>
+struct seg_op<0> {
+  typedef g1p_t T;
+  static LSG_DEVI T ident() { return proj_inf<fp_t>(); }
+  static LSG_DEVI T op(const T& a, const T& b) { return g1_add(a, b); }
+};
+template <>
+struct seg_op<1> {
+  typedef g2p_t T;
+  static LSG_DEVI T ident() { return proj_inf<fp2_t>(); }
+  static LSG_DEVI T op(const T& a, const T& b) { return g2_add(a, b); }
+};
+template <>
+struct seg_op<2> {
+  typedef fp12_t T;
+  static LSG_DEVI T ident() { return fp12_one(); }
+  static LSG_DEVI T op(const T& a, const T& b) { return fp12_mul(a, b); }
+};
+
+// Every lane runs the butterfly (no early return): a chunk's lanes are all active or all
+// inactive, and a chunk never straddles a wave (ips <= 32 pairs, chunk-aligned items).
+template <int OP>
+__global__ void LSG_KERNEL_ATTR_W(OP == 2 ? 1 : LSG_WAVES_PER_EU)
+    k_seg_reduce(int n_chunks, int ips_log2, const int32_t* __restrict__ chunks, const int32_t* __restrict__ idx,
+                 const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t* __restrict__ tmp) {
+  typedef seg_op<OP> O;
+  typedef typename O::T T;
+  lsg_lane_setup();
+  const size_t item = gtid() / LSG_GROUP;
+  const size_t c = item >> ips_log2;
+  const int ips = 1 << ips_log2, j = (int)(item & (size_t)(ips - 1));
+  const bool active = c < (size_t)n_chunks;
+  T acc = O::ident();
+  int out = 0;
+  if (active) {
+    const int off = chunks[3 * c], len = chunks[3 * c + 1];
+    out = chunks[3 * c + 2];
+    if (j < len) {
+      acc = lane_load<T>(src, idx ? (size_t)idx[off + j] : (size_t)(off + j));
+#pragma unroll 1
+      for (int k = j + ips; k < len; k += ips) acc = O::op(acc, lane_load<T>(src, idx ? (size_t)idx[off + k] : (size_t)(off + k)));
+    }
+  }
+#pragma unroll 1
+  for (int o = ips >> 1; o >= 1; o >>= 1) acc = O::op(acc, shfl_xor_t(acc, LSG_GROUP * o));
+  if (active && j == 0) {
+    if (out >= 0)
+      lane_store(dst, (size_t)out, acc);
+    else
+      lane_store(tmp, (size_t)(-out - 1), acc);
+  }
+}
+
+// ---- batched field inversion (Montgomery's trick as a product tree over the batch): every
+// field inversion of a stage -- 1/Z of the scaled pubkeys, 1/N(tv1) of the SSWU maps, 1/N(Z)
+// of the hashed points -- shares one exponentiation per batch instead of one per set.
+// Zero inputs (points at infinity, the SSWU exceptional case) are carried as 1 through the
+// tree and come out as 0, the value fp_inv(0) gives.
+// level up: out[i] = in[2i] * in[2i+1] (a missing right child is 1)
+__global__ void LSG_KERNEL_ATTR k_binv_up(int n_out, int n_in, int zero_to_one, const uint32_t* __restrict__ in,
+                                          uint32_t* __restrict__ out) {
+  LANE_ITEM(n_out);
+  (void)lead;
+  const fp_t one = fp_one();
+  fp_t a = lane_load<fp_t>(in, 2 * item);
+  fp_t b = (2 * (int)item + 1 < n_in) ? lane_load<fp_t>(in, 2 * item + 1) : one;
+  if (zero_to_one) {
+    a = fp_select(fp_is_zero(a), one, a);
+    b = fp_select(fp_is_zero(b), one, b);
+  }
+  lane_store(out, item, fp_mul(a, b));
+}
+__global__ void LSG_KERNEL_ATTR k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
+  LANE_ITEM(1);
+  (void)lead;
+  lane_store(inv, 0, fp_inv(lane_load<fp_t>(top, 0)));
+}
+// level down: inv(child c) = inv(parent c/2) * value(sibling c^1); at level 0 (zero_to_one)
+// zero children get 0
+__global__ void LSG_KERNEL_ATTR k_binv_down(int n_child, int zero_to_one, const uint32_t* __restrict__ vals,
+                                            const uint32_t* __restrict__ pinv, uint32_t* __restrict__ cinv) {
+  LANE_ITEM(n_child);
+  (void)lead;
+  const fp_t one = fp_one();
+  const int sib = (int)item ^ 1;
+  fp_t s = sib < n_child ? lane_load<fp_t>(vals, sib) : one;
+  if (zero_to_one) s = fp_select(fp_is_zero(s), one, s);
+  fp_t r = fp_mul(lane_load<fp_t>(pinv, item >> 1), s);
+  if (zero_to_one) r = fp_select(fp_is_zero(lane_load<fp_t>(vals, item)), fp_zero(), r);
+  lane_store(cinv, item, r);
+}
+
+// partials: canonical big-endian 576-byte Fp12 blobs <-> lane form (one item each)
+__global__ void LSG_KERNEL_ATTR k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs, uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  (void)lead;
+  lane_store(out, item, fp12_from_canon_bytes(blobs + 576 * item));
+}
+__global__ void LSG_KERNEL_ATTR k_fp12_to_canon(int n, const uint32_t* __restrict__ in, uint8_t* __restrict__ out) {
+  LANE_ITEM(n);
+  (void)lead;
+  fp12_to_canon_bytes(out + 576 * item, lane_load<fp12_t>(in, item));
+}
+
+// roofline probe: 4 independent limb-parallel Montgomery chains per pair
+__global__ void LSG_KERNEL_ATTR k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
+  LANE_ITEM(n);
+  (void)lead;
+  fp_t a = lane_load<fp_t>(io, item), b = fp_t(FP_R2), c = fp_t(FP_R3), d = fp_t(FP_HALF);
+  for (int k = 0; k < iters; k++) {
+    a = fp_mul(a, b);
+    b = fp_mul(b, c);
+    c = fp_mul(c, d);
+    d = fp_mul(d, a);
+  }
+  lane_store(io, item, fp_add(fp_add(a, b), fp_add(c, d)));
+}
+
+// roofline probe: raw v_mad_u64_u32 issue rate, 16 independent 64-bit accumulators per lane
+__global__ void __launch_bounds__(256) k_probe_mad(int iters, uint32_t seed, uint64_t* __restrict__ io) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[16];
+  uint32_t x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    acc[k] = t + k;
+    x[k] = (t * 2654435761u) ^ (seed + 977u * k);
+  }
+  const uint32_t y = seed | 1u;
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = (uint64_t)x[k] * y + acc[k];
+  }
+  uint64_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) r ^= acc[k];
+  io[t] = r;
+}
+
+namespace lsgk {
+hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const int32_t* chunks, const int32_t* idx,
+                      const uint32_t* src, uint32_t* dst, uint32_t* tmp) {
+  const size_t items = (size_t)n_chunks << ips_log2;
+  if (op == 0) LSG_LAUNCH_ITEMS(k_seg_reduce<0>, items, st, n_chunks, ips_log2, chunks, idx, src, dst, tmp);
+  if (op == 1) LSG_LAUNCH_ITEMS(k_seg_reduce<1>, items, st, n_chunks, ips_log2, chunks, idx, src, dst, tmp);
+  LSG_LAUNCH_ITEMS(k_seg_reduce<2>, items, st, n_chunks, ips_log2, chunks, idx, src, dst, tmp);
+}
+hipError_t binv_up(hipStream_t st, int n_out, int n_in, int zero_to_one, const uint32_t* in, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_binv_up, n_out, st, n_out, n_in, zero_to_one, in, out);
+}
+hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv) {
+  LSG_LAUNCH_ITEMS(k_binv_root, 1, st, top, inv);
+}
+hipError_t binv_down(hipStream_t st, int n_child, int zero_to_one, const uint32_t* vals, const uint32_t* pinv,
+                     uint32_t* cinv) {
+  LSG_LAUNCH_ITEMS(k_binv_down, n_child, st, n_child, zero_to_one, vals, pinv, cinv);
+}
+hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_blobs_to_fp12, n, st, n, blobs, out);
+}
+hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out576) {
+  LSG_LAUNCH_ITEMS(k_fp12_to_canon, n, st, n, in, out576);
+}
+hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io) {
+  LSG_LAUNCH_ITEMS(k_probe_fp_mul, items, st, items, iters, io);
+}
+hipError_t probe_mad(hipStream_t st, int blocks, int iters, uint32_t seed, uint64_t* io) {
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_mad, dim3(blocks), dim3(256), 0, st, iters, seed, io);
+  return hipGetLastError();
+}
+}  // namespace lsgk

@@ -1,0 +1,73 @@
+// lsg_launch.h -- launch wrappers of the gfx950 kernels, one per kernel, for the host
+// orchestration (lsg_host.hip).  The kernels live in five translation units built in
+// parallel (lsg_k_hash / lsg_k_sig / lsg_k_pk / lsg_k_miller / lsg_k_reduce .hip); each
+// wrapper sizes the grid from its item count, launches on `st` and returns
+// hipGetLastError().  Pointers are device pointers; lane-form arrays use the item-major layout
+// of lsg_layout.h.  Counts of 0 launch nothing.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace lsgk {
+// ---- hash_to_G2 (lsg_k_hash.hip)                                      SURVEY 8a M3
+hipError_t expand_msg(hipStream_t st, int n, const uint8_t* msg, const uint32_t* off, const uint32_t* len,
+                      const uint8_t* dst, uint32_t dst_len, uint8_t* ub);
+hipError_t h2c_prep(hipStream_t st, int n, const uint8_t* ub, uint32_t* U, uint32_t* norms);
+hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* ninv, uint32_t* Hp);
+hipError_t h2c_clear(hipStream_t st, int n, uint32_t* Hp, uint32_t* zN, uint8_t* hinf);
+hipError_t h2c_affine(hipStream_t st, int n, const uint32_t* Hp, const uint32_t* ninv, const uint8_t* hinf,
+                      uint32_t* H);
+hipError_t signing_root(hipStream_t st, int n, const uint8_t* roots, const uint8_t* domains, uint32_t dstride,
+                        uint8_t* out32);
+hipError_t attestation_signing_root(hipStream_t st, int n, const uint8_t* data, const uint8_t* domains,
+                                    uint32_t dstride, uint8_t* out32);
+
+// ---- signatures (lsg_k_sig.hip)                                       SURVEY 8a M2, M4
+hipError_t sig_decode(hipStream_t st, int n, const uint8_t* sig, const uint32_t* sig_len, uint32_t* sig_aff,
+                      uint8_t* inf, int32_t* err);
+hipError_t sig_subgroup(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, int32_t* err);
+// out[i] = the projective point set i adds to its group's RLC signature sum: the identity
+// when the signature did not decode (err), is the point at infinity (inf) or the set's
+// aggregated key is infinity (pinf, may be null); else [r_i] sig_i when rnd is given and
+// (mode == null or mode[i] != 0), else sig_i itself (the bucket MSM scales later).
+hipError_t sig_prep(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                    const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out);
+hipError_t g2a_to_bytes(hipStream_t st, int n, const uint32_t* pts, const uint8_t* inf, uint8_t* out192);
+hipError_t g2p_compress(hipStream_t st, int n, const uint32_t* pts, uint8_t* out96);
+hipError_t g2p_to_canon(hipStream_t st, int n, const uint32_t* pts, uint8_t* out288);
+hipError_t sign(hipStream_t st, int n, const uint8_t* sks, const uint32_t* H, uint8_t* out96);
+
+// ---- public keys (lsg_k_pk.hip)                                       SURVEY 8a H8, M1, M4
+hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, const uint32_t* pk_len, uint32_t* pts,
+                     int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
+hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err);
+hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* rnd, uint32_t* Pp, uint32_t* zP,
+                    uint8_t* pinf);
+hipError_t pk_affine(hipStream_t st, int n, const uint32_t* Pp, const uint32_t* zinv, uint32_t* P);
+hipError_t g1p_to_bytes(hipStream_t st, int n, const uint32_t* pts, uint8_t* out96);
+hipError_t sk_to_pk(hipStream_t st, int n, const uint8_t* sks, uint8_t* out96);
+
+// ---- Miller loop (lsg_k_miller.hip)                                   SURVEY 8a M5
+hipError_t miller_lines(hipStream_t st, int n, const uint32_t* H, uint32_t* lines);
+// K = pairs per item (1, 2 or 4)
+hipError_t miller_accum(hipStream_t st, int K, int n_items, const int32_t* item_first, const int32_t* item_cnt,
+                        const uint32_t* P, const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, int n_sets,
+                        const uint32_t* lines, uint32_t* f);
+
+// ---- reductions, inversions, conversions, probes (lsg_k_reduce.hip)
+// Segmented reduction (op 0: G1 add, 1: G2 add, 2: Fp12 product): chunk c = chunks[3c..3c+2]
+// = {off, len, out} combines elements idx[off .. off+len) of src (idx == null: off .. off+len)
+// into out >= 0 ? dst[out] : tmp[-out-1].  2^ips_log2 lane pairs share a chunk: each folds
+// every 2^ips_log2-th element serially, then a lane butterfly combines them.
+hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const int32_t* chunks, const int32_t* idx,
+                      const uint32_t* src, uint32_t* dst, uint32_t* tmp);
+hipError_t binv_up(hipStream_t st, int n_out, int n_in, int zero_to_one, const uint32_t* in, uint32_t* out);
+hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv);
+hipError_t binv_down(hipStream_t st, int n_child, int zero_to_one, const uint32_t* vals, const uint32_t* pinv,
+                     uint32_t* cinv);
+hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* out);
+hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out576);
+hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io);
+hipError_t probe_mad(hipStream_t st, int blocks, int iters, uint32_t seed, uint64_t* io);
+}  // namespace lsgk

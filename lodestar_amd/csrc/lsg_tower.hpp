@@ -280,7 +280,7 @@ LSG_INL fp6_t fp6_mul_fin(const fp2_t* V) {
   r.c2 = c2;
   return r;
 }
-#ifdef LSG_QUAD_MODE
+#ifdef LSG_LEAN_TOWER
 // Quad backend: an Fp takes three VGPRs, so the products are issued one Fp2 product (three
 // interleaved Montgomery chains) at a time instead of in wide batches; same values.
 LSG_BIGFN fp6_t fp6_mul(fp6_t a, fp6_t b) {
@@ -341,7 +341,7 @@ LSG_INL bool fp12_is_one(const fp12_t& a) {
 }
 LSG_INL fp12_t fp12_conj(const fp12_t& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
-#ifdef LSG_QUAD_MODE
+#ifdef LSG_LEAN_TOWER
 LSG_BIGFN fp12_t fp12_mul(fp12_t a, fp12_t b) {
   fp6_t t0 = fp6_mul(a.c0, b.c0);
   fp6_t t1 = fp6_mul(a.c1, b.c1);
@@ -388,7 +388,7 @@ LSG_INL void fp4_square(fp2_t& c0, fp2_t& c1, const fp2_t& a, const fp2_t& b) {
 // (the three Fp4 squarings = 9 Fp2 squarings issued as one batch)
 LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
   fp2_t z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
-#ifdef LSG_QUAD_MODE
+#ifdef LSG_LEAN_TOWER
   fp2_t t0, t1, u0, u1, t2, t3;
   fp4_square(t0, t1, z0, z1);
   fp4_square(u0, u1, z2, z3);
@@ -441,7 +441,7 @@ LSG_BIGFN fp12_t fp12_cyclotomic_sqr(fp12_t f) {
 // fp6_mul_01(f0, l00, l01), fp6_mul_01(f0 + f1, l00, l01 + l11) and fp6_mul_1(f1, l11):
 // 13 independent Fp2 products issued as one batch.
 LSG_BIGFN fp12_t fp12_mul_line(fp12_t f, fp2_t l00, fp2_t l01, fp2_t l11) {
-#ifdef LSG_QUAD_MODE
+#ifdef LSG_LEAN_TOWER
   fp6_t t0 = fp6_mul_01(f.c0, l00, l01);
   fp6_t u = fp6_mul_01(fp6_add(f.c0, f.c1), l00, fp2_add(l01, l11));
   fp6_t t1 = fp6_mul_1(f.c1, l11);

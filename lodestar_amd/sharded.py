@@ -1,26 +1,29 @@
-"""Node-sharded verification across the GPUs of one node.
+"""Node-sharded verification across the GPUs of one node, one process per GPU.
 
-One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on ROCm, "gloo" in
-the CPU tests).  For one package of jobs (BlsWorkReq[], packages/beacon-node/src/chain/bls/
-multithread/types.ts:14-17) every rank:
+The in-process alternative is one context over every GPU (include/lodestar_bls.h
+lsg_init_devices: RCCL communicators owned by the C side).  This module is the same protocol
+for hosts that run one process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
+ROCm, "gloo" in the CPU tests).  For one package of jobs (BlsWorkReq[],
+packages/beacon-node/src/chain/bls/multithread/types.ts:14-17) every rank:
 
 1. takes its shard: whole jobs, never split, assigned by cumulative set count so that the
-   shards are balanced (``assign_jobs``);
-2. reduces its shard to one un-exponentiated Fp12 Miller product (``backend.batch_partial``:
-   decode + subgroup check, hash_to_G2, RLC scalars, Miller loops, the local
-   ML(-G1, sum r_i sig_i) term);
-3. all-gathers the 576-byte partials (one collective: the path's only exchange step);
-4. multiplies them and runs ONE final exponentiation (``backend.final_verify``).
+   shards are balanced (``assign_jobs``, the same rule as lsg_assign_jobs);
+2. submits it (``backend.submit``): decode + subgroup check, pubkey aggregation, hash_to_G2,
+   RLC scalars, Miller loops, the local ML(-G1, sum r_i sig_i) term -- every batchable set of
+   the shard is one RLC group, including aggregate and multi-key sets;
+3. all-gathers the 576-byte partial of that group (``backend.partial``; one collective, the
+   path's only exchange step);
+4. multiplies the partials and runs ONE final exponentiation (``backend.final_verify``);
+5. resolves its jobs with that node verdict (``backend.resolve``): when the node check fails,
+   the rank's own package check (already computed on its GPU) localises, and only a failing
+   rank runs the reference's chunk / per-job fallback (worker.ts:51-96).  Per-job verdicts
+   are all-gathered.
 
-If that combined check fails, or some shard could not be batched, each rank
-final-exponentiates its own partial to localise the failing shards; only those ranks run the
-per-job path (``backend.verify_jobs``: worker.ts:30-106 batch + per-job retry), and the
-per-job verdicts are all-gathered.  Passing shards report every job valid, exactly what the
-per-job path would give for them (a valid RLC batch implies valid jobs up to the 2^-64
-randomizer soundness bound the reference accepts too).
+Randomizers: seed 0 means the OS CSPRNG on every rank (production); a nonzero seed (tests)
+is offset per rank.
 
-The backend is duck-typed: ``GpuBackend`` (this package, HIP through the C ABI) in
-production, an oracle-backed one in the CPU tests.
+The backend is duck-typed: ``GpuBackend`` (this package, HIP through the C ABI) in production,
+an oracle-backed one in the CPU tests.
 """
 from dataclasses import dataclass
 
@@ -40,11 +43,16 @@ def assign_jobs(job_sizes, world):
     return out
 
 
+def rank_seed(seed, rank):
+    """0 stays 0 (every rank draws from the OS CSPRNG); test seeds differ per rank."""
+    return seed + rank if seed else 0
+
+
 @dataclass
 class ShardOutcome:
     results: list          # per job: (status, err_code)
     combined_ok: bool      # the one-final-exponentiation node check passed
-    retried_ranks: list    # ranks that fell back to the per-job path
+    retried_ranks: list    # ranks that ran the reference's batch-retry fallback
 
 
 class ShardedVerifier:
@@ -67,48 +75,38 @@ class ShardedVerifier:
         Returns a ShardOutcome with per-job (status, err_code) for ALL jobs."""
         owner = assign_jobs([len(s) for s, _ in jobs], self.world)
         mine = [j for j, r in enumerate(owner) if r == self.rank]
-        my_sets = [st for j in mine for st in jobs[j][0]]
-        # a job with an aggregate set, a multi-key set or an empty job goes to the per-job path
-        batchable = all(len(jobs[j][0]) > 0 for j in mine) and all(len(pks) == 1 for pks, _, _ in my_sets)
-        part, any_err = None, True
-        if my_sets and batchable:
-            part, _errs, any_err = self.backend.batch_partial(my_sets, seed=seed + self.rank)
-        elif not my_sets:
-            any_err = False  # nothing to contribute
-        gathered = self._all_gather((part, bool(any_err)))
-        parts = [p for p, _ in gathered if p is not None]
-        node_ok = not any(e for _, e in gathered) and bool(parts) and self.backend.final_verify(parts)
-        if node_ok:
-            return ShardOutcome([(VALID, 0)] * len(jobs), True, [])
-        # localise: a shard passes on its own iff it could be batched and its partial verifies
-        own_ok = (not my_sets) or (part is not None and not any_err and self.backend.final_verify([part]))
-        local = {}
-        if not own_ok:
-            res, _stats = self.backend.verify_jobs([jobs[j] for j in mine], seed=seed + 7919 * (self.rank + 1))
-            local = {j: tuple(r) for j, r in zip(mine, res)}
-        else:
-            local = {j: (VALID, 0) for j in mine}
-        merged = {}
-        retried = []
-        for r, d in enumerate(self._all_gather((own_ok, local))):
-            ok_r, loc = d
-            if not ok_r:
+        h = self.backend.submit([jobs[j] for j in mine], seed=rank_seed(seed, self.rank))
+        part, _has = self.backend.partial(h)
+        parts = self._all_gather(part)
+        node_ok = self.backend.final_verify(parts)
+        res, stats = self.backend.resolve(h, 1 if node_ok else 0)
+        local = {j: tuple(r) for j, r in zip(mine, res)}
+        merged, retried = {}, []
+        for r, (loc, retries) in enumerate(self._all_gather((local, stats.get("batch_retries", 0)))):
+            if retries:
                 retried.append(r)
             merged.update(loc)
-        return ShardOutcome([merged[j] for j in range(len(jobs))], False, retried)
+        return ShardOutcome([merged[j] for j in range(len(jobs))], node_ok, retried)
 
 
 class GpuBackend:
-    """ShardedVerifier backend on one GPU through the C ABI (lodestar_amd._native.Context)."""
+    """ShardedVerifier backend on one GPU through the C ABI (lodestar_amd._native.Context):
+    lsg_submit_jobs, lsg_jobs_partial, lsg_final_verify, lsg_wait_jobs_node."""
 
     def __init__(self, ctx):
         self.ctx = ctx
 
-    def batch_partial(self, sets, seed=0):
-        return self.ctx.batch_partial(sets, seed=seed)
+    def submit(self, jobs, seed=0):
+        t = self.ctx.submit_jobs(jobs, seed=seed)
+        if t is None:
+            raise RuntimeError("every pipeline slot is busy")
+        return t
+
+    def partial(self, handle):
+        return self.ctx.jobs_partial(handle)
 
     def final_verify(self, partials):
         return self.ctx.final_verify(list(partials))
 
-    def verify_jobs(self, jobs, seed=0):
-        return self.ctx.verify_jobs(jobs, seed=seed)
+    def resolve(self, handle, node_valid):
+        return self.ctx.wait_jobs_node(handle, node_valid)

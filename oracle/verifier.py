@@ -183,7 +183,7 @@ def sk_to_pk(sk):
 
 def batch_partial(sets, rands):
     """Per-shard half of verify_multiple for the node-sharded path, with the
-    device's conventions (lodestar_amd/csrc/lsg_bls.hip submit_batch): sets whose signature
+    device's conventions (lodestar_amd/csrc/lsg_host.hip: the package group excludes such sets): sets whose signature
     does not decode (or whose key is infinite) contribute 1 and are reported by error code.
     sets: list of (pk_bytes, msg, sig_bytes).  Returns (partial Fp12, [error codes])."""
     from .curves import BlstError as _BE

@@ -1,0 +1,294 @@
+"""GPU parity at the BASELINE configs' sizes (BASELINE.json configs A-E) and the
+drop-in jobs path's contract, through the C ABI against the C restatement of the oracle
+(tests/cpu_oracle.py) and the Python oracle.  Every test here needs an MI355X.
+
+Inputs: interop keys sk_{v mod 1024} (packages/state-transition/src/util/interop.ts:19-22,
+keypairsMod reuse of state-transition/test/perf/util.ts:47-48), messages
+sha256(b"lodestar-mi355x" || tag || i), signatures made on the GPU (lsg_sign, itself pinned by
+the genesis KAT and golden vectors in test_gpu_parity.py).  Expected verdicts never come from
+the GPU: the oracle verifies every set, and the tests first assert that constructed-valid
+sets are valid to the oracle.
+"""
+import hashlib
+import os
+
+import pytest
+
+from oracle.fields import R
+from oracle.interop import interop_secret_key
+from tests import blsdata as bd
+from tests import cpu_oracle as co
+
+pytestmark = pytest.mark.gpu
+N_KEYS = 1024
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from lodestar_amd._native import Context
+    c = Context(0)  # raises NativeUnavailable loudly if the HIP library or the GPU is missing
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def keys(ctx):
+    sks = [interop_secret_key(i) for i in range(N_KEYS)]
+    return sks, ctx.sk_to_pk(sks)
+
+
+def msgs_for(tag, n, base=0):
+    return [hashlib.sha256(b"lodestar-mi355x" + tag + (base + i).to_bytes(8, "little")).digest() for i in range(n)]
+
+
+def single_sets(ctx, keys, tag, n):
+    sks, pks = keys
+    msgs = msgs_for(tag, n)
+    sigs = ctx.sign([sks[i % N_KEYS] for i in range(n)], msgs)
+    return [([pks[i % N_KEYS]], msgs[i], sigs[i]) for i in range(n)]
+
+
+def corrupt(ctx, keys, sets, frac, seed):
+    """Config E: a fraction of the sets corrupted, split evenly over the five kinds of
+    SURVEY.md 8d (wrong message, flipped x bit, truncated, non-subgroup point, infinity)."""
+    import random
+    rng = random.Random(seed)
+    out = list(sets)
+    idx = sorted(rng.sample(range(len(sets)), max(5, int(len(sets) * frac))))
+    for k, i in enumerate(idx):
+        out[i] = bd.CORRUPTIONS[k % len(bd.CORRUPTIONS)](out[i])
+    return out, idx
+
+
+def oracle_each(sets):
+    return co.verify_each([p[0] for p, _, _ in sets], [m for _, m, _ in sets], [s for _, _, s in sets])
+
+
+def run_jobs(ctx, jobs, seed=0):
+    got, stats = ctx.verify_jobs(jobs, seed=seed)
+    return got, stats
+
+
+def check_against_oracle(ctx, jobs, per_set, seed=0):
+    jsets, pos = [], 0
+    for sets, _ in jobs:
+        jsets.append(list(range(pos, pos + len(sets))))
+        pos += len(sets)
+    exp, retries, success = co.expected_jobs(jsets, [bool(f & 1) for _, f in jobs], per_set)
+    got, stats = run_jobs(ctx, jobs, seed=seed)
+    bad = [(j, g, e) for j, (g, e) in enumerate(zip(got, exp)) if (g[0], g[1] if g[0] == 2 else 0) != e]
+    assert not bad, bad[:10]
+    assert stats["batch_retries"] == retries and stats["batch_sigs_success"] == success, (stats, retries, success)
+    return got, stats
+
+
+# ---- config A: gossip-128 -- 128 single sets (BlsSingleThreadVerifier path, singleThread.ts:14-35)
+def test_config_a_gossip_128(ctx, keys):
+    sets = single_sets(ctx, keys, b"cfgA", 128)
+    per = oracle_each(sets)
+    assert per == [1] * 128
+    assert ctx.verify_sets(sets) == (1, 0)  # maybeBatch over one call (lsg_verify_sets)
+    bad, idx = corrupt(ctx, keys, sets, 0.02, 1)
+    per_bad = oracle_each(bad)
+    exp_err = next((-v for v in per_bad if v < 0), None)
+    assert ctx.verify_sets(bad)[0] == (2 if exp_err else 0)
+    # the same 128 sets as 128 batchable single-set jobs (worker.ts chunks of 16)
+    check_against_oracle(ctx, [([s], 1) for s in sets], per)
+    check_against_oracle(ctx, [([s], 1) for s in bad], per_bad)
+
+
+# ---- config B: sync-committee contribution -- one 512-key aggregate set, same message
+def test_config_b_sync_contribution_512(ctx, keys):
+    from oracle.verifier import sk_to_pk
+    from oracle.curves import g1_serialize
+    sks, pks = keys
+    members = list(range(7, 7 + 512))
+    m = msgs_for(b"cfgB", 1)[0]
+    agg_sk = sum(sks[k % N_KEYS] for k in members) % R
+    sig = ctx.sign([agg_sk], [m])[0]
+    agg_pk = g1_serialize(sk_to_pk(agg_sk))  # the oracle's aggregate key: (sum sk) G1
+    assert co.verify_each([agg_pk], [m], [sig]) == [1]
+    assert ctx.aggregate_pubkeys([pks[k % N_KEYS] for k in members]) == (agg_pk, 0)
+    s = ([pks[k % N_KEYS] for k in members], m, sig)
+    assert ctx.verify_sets([s]) == (1, 0)
+    assert ctx.verify_sets([(s[0][:-1], m, sig)]) == (0, 0)  # one signer missing
+    # verifySignatureSetsSameMessage shape: 32 contributions of one message, one forged
+    ms = [([pks[i]], m, x) for i, x in enumerate(ctx.sign(sks[:32], [m] * 32))]
+    ms[9] = (ms[9][0], m, ms[10][2])
+    per = oracle_each(ms)
+    assert per.count(0) == 1 and per[9] == 0
+    check_against_oracle(ctx, [([x], 1) for x in ms], per)
+
+
+# ---- config C: block body -- 128 aggregate sets of ~450 keys by index, distinct messages
+@pytest.fixture(scope="module")
+def table_ctx(keys):
+    from lodestar_amd._native import Context
+    c = Context(0)
+    assert c.pubkey_table_set(0, keys[1]) == [0] * N_KEYS
+    yield c
+    c.close()
+
+
+def test_config_c_block_128x450(table_ctx, keys):
+    from lodestar_amd._native import PkIndices
+    from oracle.verifier import sk_to_pk
+    from oracle.curves import g1_serialize
+    sks, _ = keys
+    c = table_ctx
+    n = 128
+    idx, agg_sk = [], []
+    for g in range(n):
+        size = 440 + (g * 7) % 21
+        start = (g * 53) % N_KEYS
+        ix = [(start + j) % N_KEYS for j in range(size)]
+        idx.append(ix)
+        agg_sk.append(sum(sks[k] for k in ix) % R)
+    msgs = msgs_for(b"cfgC", n)
+    sigs = c.sign(agg_sk, msgs)
+    agg_pks = [g1_serialize(sk_to_pk(k)) for k in agg_sk]
+    per = co.verify_each(agg_pks, msgs, sigs)
+    assert per == [1] * n
+    sets = [(PkIndices(idx[g]), msgs[g], sigs[g]) for g in range(n)]
+    # verifyBlocksSignatures.ts:37: one non-batchable job per block (<= 128 sets)
+    got, stats = c.verify_jobs([(sets, 0)])
+    assert got == [(1, 0)]
+    wrong = list(sets)
+    wrong[77] = (wrong[77][0], msgs[76], wrong[77][2])
+    assert co.verify_each([agg_pks[77]], [msgs[76]], [sigs[77]]) == [0]
+    got, _ = c.verify_jobs([(wrong[:64], 0), (wrong[64:], 0)])
+    assert got == [(1, 0), (0, 0)]
+    # the aggregated keys themselves, bit-exact against the oracle's (sum sk) G1
+    for g in (0, 77, 127):
+        assert c.aggregate_pubkeys(PkIndices(idx[g])) == (agg_pks[g], 0)
+
+
+# ---- config D: firehose shard -- a 4096-set package, one RLC group
+def test_config_d_4096_package(ctx, keys):
+    sets = single_sets(ctx, keys, b"cfgD", 4096)
+    per = oracle_each(sets)
+    assert per == [1] * 4096
+    got, stats = run_jobs(ctx, [([s], 1) for s in sets])
+    assert got == [(1, 0)] * 4096
+    assert stats["batch_retries"] == 0 and stats["batch_sigs_success"] == 4096
+    assert stats["n_final_exps"] == 1  # the package group answers all 4096 jobs
+    part, errs, anyerr = ctx.batch_partial(sets)
+    assert not anyerr and ctx.final_verify([part])
+    bad = list(sets)
+    bad[3001] = bd.corrupt_wrong_message(bad[3001])
+    per_bad = oracle_each(bad)
+    assert per_bad.count(0) == 1
+    _, stats = check_against_oracle(ctx, [([s], 1) for s in bad], per_bad)
+    assert stats["batch_retries"] == 1 and stats["batch_sigs_success"] == 4096 - 16
+    part_b, _, _ = ctx.batch_partial(bad)
+    assert not ctx.final_verify([part_b])
+
+
+# ---- config E: adversarial -- a 4096-set package at 1% corruption through the retry path
+def test_config_e_adversarial_4096(ctx, keys):
+    sets = single_sets(ctx, keys, b"cfgE", 4096)
+    bad, idx = corrupt(ctx, keys, sets, 0.01, 7)
+    per = oracle_each(bad)
+    assert all(per[i] == 1 for i in range(4096) if i not in set(idx))
+    check_against_oracle(ctx, [([s], 1) for s in bad], per)
+    # mixed shape: multi-set jobs, non-batchable jobs
+    jobs, pos, jper = [], 0, []
+    while pos < 1024:
+        n = 1 + (pos % 3)
+        jobs.append((bad[pos:pos + n], 0 if pos % 5 == 0 else 1))
+        pos += n
+    check_against_oracle(ctx, jobs, per[:pos])
+
+
+def test_package_group_matches_chunk_mode(ctx, keys, monkeypatch):
+    """The one-group phase A (default) and the reference's chunk-16 phase A
+    (LSG_PACKAGE_GROUP=0) give identical per-job verdicts AND batch_retries /
+    batch_sigs_success, on a valid and on an adversarial package."""
+    sets = single_sets(ctx, keys, b"modes", 600)
+    bad, _ = corrupt(ctx, keys, sets, 0.02, 3)
+    for pkg in (sets, bad):
+        jobs = [([s], 1) for s in pkg[:300]] + [(pkg[300 + 2 * k:302 + 2 * k], 1 if k % 4 else 0) for k in range(150)]
+        out = {}
+        for mode in ("1", "0"):
+            monkeypatch.setenv("LSG_PACKAGE_GROUP", mode)
+            got, stats = ctx.verify_jobs(jobs, seed=17)
+            out[mode] = (got, stats["batch_retries"], stats["batch_sigs_success"])
+        assert out["1"] == out["0"]
+
+
+def test_reserve_then_no_allocations(ctx, keys):
+    """lsg_reserve sizes every buffer up front: steady-state submissions allocate nothing
+    (no hipMalloc / hipHostMalloc / hipFree in the submit path)."""
+    sets = single_sets(ctx, keys, b"resv", 2048)
+    from lodestar_amd._native import PreparedJobs
+    pj = PreparedJobs([([s], 1) for s in sets])
+    ctx.reserve(4096, n_slots=4)
+    before = ctx.allocation_count()
+    tickets = [ctx.submit_jobs(pj) for _ in range(4)]
+    for t in tickets:
+        res, stats = ctx.wait_jobs(t)
+        assert res == [(1, 0)] * 2048
+    assert ctx.allocation_count() == before
+
+
+def test_node_mode_partials(ctx, keys):
+    """One-process-per-GPU protocol (lsg_jobs_partial / lsg_wait_jobs_node): the package
+    partial verifies alone, a forged package's does not, and the node verdict drives the
+    resolution exactly as the package's own check would."""
+    sets = single_sets(ctx, keys, b"node", 300)
+    bad = list(sets)
+    bad[10] = bd.corrupt_wrong_message(bad[10])
+    for pkg, ok in ((sets, True), (bad, False)):
+        jobs = [([s], 1) for s in pkg]
+        t = ctx.submit_jobs(jobs)
+        part, has = ctx.jobs_partial(t)
+        assert has and ctx.final_verify([part]) == ok
+        got, stats = ctx.wait_jobs_node(t, 1 if ok else 0)
+        assert [g[0] for g in got] == [0 if (not ok and i == 10) else 1 for i in range(300)]
+    # a package without batchable sets contributes the identity partial
+    t = ctx.submit_jobs([(sets[:3], 0)])
+    part, has = ctx.jobs_partial(t)
+    assert not has and ctx.final_verify([part])
+    assert ctx.wait_jobs_node(t, 1)[0] == [(1, 0)]
+
+
+def test_multi_device_context_duplicate_ids(keys):
+    """lsg_init_devices over [0, 0] (the copy exchange; distinct ids use RCCL): whole jobs per
+    device, the gathered node check, and localisation give the single-device verdicts."""
+    from lodestar_amd._native import Context
+    c1 = Context(0)
+    c2 = Context(devices=[0, 0])
+    try:
+        assert c2.device_count() == 2
+        sets = single_sets(c1, keys, b"multi", 512)
+        bad, _ = corrupt(c1, keys, sets, 0.02, 5)
+        per = oracle_each(bad)
+        jobs = [([s], 1) for s in bad[:256]] + [(bad[256 + 4 * k:260 + 4 * k], 1) for k in range(64)]
+        g1, s1 = c1.verify_jobs(jobs, seed=3)
+        g2, s2 = c2.verify_jobs(jobs, seed=3)
+        assert g1 == g2
+        check_against_oracle(c2, jobs, per)
+        good = [([s], 1) for s in sets]
+        g, st = c2.verify_jobs(good)
+        assert g == [(1, 0)] * 512 and st["batch_retries"] == 0
+    finally:
+        c2.close()
+        c1.close()
+
+
+def test_rccl_exchange_single_device(keys, monkeypatch):
+    """The RCCL all-gather path of lsg_init_devices exercised on one GPU
+    (LSG_FORCE_EXCHANGE=1: a one-rank communicator, the node check on the gathered partial)."""
+    from lodestar_amd._native import Context
+    monkeypatch.setenv("LSG_FORCE_EXCHANGE", "1")
+    c = Context(devices=[0])
+    try:
+        sets = single_sets(c, keys, b"rccl", 256)
+        bad = list(sets)
+        bad[5] = bd.corrupt_wrong_message(bad[5])
+        g, st = c.verify_jobs([([s], 1) for s in sets])
+        assert g == [(1, 0)] * 256 and st["n_final_exps"] == 2  # package FE + node FE
+        g, st = c.verify_jobs([([s], 1) for s in bad])
+        assert [x[0] for x in g] == [0 if i == 5 else 1 for i in range(256)]
+    finally:
+        c.close()

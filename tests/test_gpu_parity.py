@@ -52,13 +52,17 @@ def oracle_job_results(jobs):
 
 
 def check_jobs(ctx, jobs, seed=7):
+    """Per-job verdicts, error messages AND the BlsWorkResult counters against the oracle's
+    worker.ts restatement."""
     from lodestar_amd._native import error_message
     got, stats = ctx.verify_jobs(jobs, seed=seed)
-    exp, _ = oracle_job_results(jobs)
+    exp, out = oracle_job_results(jobs)
     for i, ((gs, gc), (es, emsg)) in enumerate(zip(got, exp)):
         assert gs == es, (i, got, exp)
         if es == 2:
             assert error_message(gc) == emsg or error_message(gc).split(": ")[-1] in emsg, (i, gc, emsg)
+    assert stats["batch_retries"] == out["batch_retries"], (stats, out["batch_retries"])
+    assert stats["batch_sigs_success"] == out["batch_sigs_success"], (stats, out["batch_sigs_success"])
     return got, stats
 
 
@@ -218,31 +222,23 @@ def test_async_jobs_two_slots_match_sync(ctx):
     assert ctx.verify_jobs(pkgs[0], seed=21)[0] == r0
 
 
-def test_staged_batches_and_async_finals(ctx):
+def test_partials_and_async_finals(ctx):
+    """lsg_batch_partial partials and the final-exponentiation entries (lsg_final_*): single,
+    grouped (one launch for several groups) and empty tickets."""
     sets = [bd.single_set(400 + i) for i in range(24)]
-    staged = ctx.stage(sets, seed=77)
-    try:
-        ta, tb = ctx.batch_submit(staged), ctx.batch_submit(staged)
-        extra = []
-        while True:  # every pipeline slot outstanding -> LSG_ERR_BUSY (None)
-            t = ctx.batch_submit(staged)
-            if t is None:
-                break
-            extra.append(t)
-            assert len(extra) < 64
-        assert len(extra) + 2 == ctx.pipeline_slots()
-        pa, ea, aa = ctx.batch_wait(ta)
-        pb, eb, ab = ctx.batch_wait(tb)
-        for t in extra:
-            assert ctx.batch_wait(t)[0] == pa
-        assert pa == pb and not aa and not ab and ea == [0] * 24
-        # the same package through the synchronous path gives the same partial
-        ps, _, _ = ctx.batch_partial(sets, seed=77)
-        assert ps == pa
-        fs = [ctx.final_submit([pa]), ctx.final_submit([pa, pb]), ctx.final_submit([])]
-        assert [ctx.final_wait(t) for t in fs] == [True, True, False]
-    finally:
-        staged.free()
+    bad = list(sets)
+    bad[13] = bd.corrupt_wrong_message(bad[13])
+    parts = [ctx.batch_partial(pkg[8 * g:8 * g + 8], seed=31 + g)[0] for pkg in (sets, bad) for g in range(3)]
+    expect = [True, True, True, True, False, True]
+    assert [ctx.final_verify([p]) for p in parts] == expect
+    assert ctx.final_wait_groups(ctx.final_submit_groups([[p] for p in parts])) == expect
+    pairs = [[parts[g], parts[(g + 1) % 3]] for g in range(3)] + [[parts[3], parts[4]]]
+    assert ctx.final_wait_groups(ctx.final_submit_groups(pairs)) == [True, True, True, False]
+    fs = [ctx.final_submit(parts[:3]), ctx.final_submit(parts[3:]), ctx.final_submit([])]
+    assert [ctx.final_wait(t) for t in fs] == [True, False, False]
+    # the same sets as one partial equal the product of the three (same randomizers)
+    whole = ctx.batch_partial(sets, seed=31)[0]
+    assert ctx.final_verify([whole])
 
 
 def test_batch_partial_excludes_errored_sets(ctx):
@@ -301,31 +297,6 @@ def test_node_host_on_gpu(ctx, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-def test_grouped_batch_submission(ctx):
-    """lsg_batch_submit_groups: one launch, three RLC groups, one partial per group."""
-    sets = [bd.single_set(600 + i) for i in range(20)]
-    bad = list(sets)
-    bad[13] = bd.corrupt_wrong_message(bad[13])  # group 1 (sets 8..15)
-    for pkg, expect in ((sets, [True, True, True]), (bad, [True, False, True])):
-        staged = ctx.stage(pkg, seed=31)
-        try:
-            t = ctx.batch_submit(staged, group_size=8)
-            parts, errs, anyerr = ctx.batch_wait(t)
-            assert len(parts) == 3 and not anyerr and errs == [0] * 20
-            assert [ctx.final_verify([p]) for p in parts] == expect
-            assert ctx.final_verify(parts) == all(expect)
-            # all groups' final checks in one ticket (lsg_final_submit_groups), one and two
-            # partials per group
-            assert ctx.final_wait_groups(ctx.final_submit_groups([[p] for p in parts])) == expect
-            again = ctx.batch_wait(ctx.batch_submit(staged, group_size=8))[0]
-            pairs = [[parts[g], again[g]] for g in range(3)]  # F_g^2: the same verdicts
-            assert ctx.final_wait_groups(ctx.final_submit_groups(pairs)) == expect
-            whole, _, _ = ctx.batch_wait(ctx.batch_submit(staged))  # one group: product of the three
-            assert ctx.final_verify([whole]) == all(expect)
-        finally:
-            staged.free()
-
-
 def test_sharded_verifier_gpu_backend(ctx):
     """lodestar_amd/sharded.py on one GPU: node check passes for a valid package; a corrupted
     set localises to this rank and the per-job fallback matches the worker.ts verdicts."""
@@ -344,12 +315,16 @@ def test_sharded_verifier_gpu_backend(ctx):
     out = sv.verify_jobs(bad, seed=5)
     exp, _ = oracle_job_results(bad)
     assert not out.combined_ok and out.retried_ranks == [0]
+    # aggregate and multi-key sets share the batched shard (no per-job detour)
+    agg = [([bd.aggregate_set(k, list(range(3 * k, 3 * k + 5)), tag="sv")], 1) for k in range(4)]
+    res = sv.verify_jobs(agg + jobs, seed=0)
+    assert res.combined_ok and [r[0] for r in res.results] == [1] * 10
     assert [r[0] for r in out.results] == [e[0] for e in exp]
 
 
 def _splitmix_rands(seed, n):
-    """The randomizers lsg_stage / lsg_batch_partial derive from a nonzero seed
-    (lsg_bls.hip stage_sets: splitmix64, zero draws skipped)."""
+    """The randomizers lsg_batch_partial derives from a nonzero seed on a single-device
+    context (lsg_host.hip stage_sets: splitmix64, zero draws skipped)."""
     M = (1 << 64) - 1
     s, out = seed, []
     while len(out) < n:
@@ -369,24 +344,20 @@ def _f12_bytes(f):
 
 
 def test_msm_signature_sums_match_scalar_path(ctx, monkeypatch):
-    """Bucket MSM (lsg_bls.hip msm_sum) vs per-set [r_i] sig_i: identical partials per group,
-    including an infinite and an undecodable signature (identity contributions)."""
+    """Bucket MSM vs per-set [r_i] sig_i for the package group's signature sum: identical
+    partials, including an infinite and an undecodable signature (identity contributions)."""
     sets = [bd.single_set(700 + i, tag="msm") for i in range(40)]
     sets[5] = bd.corrupt_infinity(sets[5])
     sets[22] = bd.corrupt_truncate(sets[22])
     sets[31] = bd.corrupt_wrong_message(sets[31])
-    staged = ctx.stage(sets, seed=1234)
-    try:
-        out = {}
-        for mode, thr in (("msm", "1"), ("scalar", "1000000")):
-            monkeypatch.setenv("LSG_MSM_MIN_GROUP", thr)
-            parts, errs, anyerr = ctx.batch_wait(ctx.batch_submit(staged, group_size=20))
-            out[mode] = parts
-            assert anyerr and errs[22] == 10 and errs[5] == 0
-        assert out["msm"] == out["scalar"]
-        assert [ctx.final_verify([p]) for p in out["msm"]] == [False, False]  # 5: infinity sig; 31: wrong msg
-    finally:
-        staged.free()
+    out = {}
+    for mode, thr in (("msm", "1"), ("scalar", "1000000")):
+        monkeypatch.setenv("LSG_MSM_MIN_GROUP", thr)
+        part, errs, anyerr = ctx.batch_partial(sets, seed=1234)
+        out[mode] = part
+        assert anyerr and errs[22] == 10 and errs[5] == 0
+    assert out["msm"] == out["scalar"]
+    assert not ctx.final_verify([out["msm"]])  # 5: infinity sig; 31: wrong msg
 
 
 def test_batch_partial_bit_exact_vs_oracle(ctx, monkeypatch):

@@ -10,26 +10,37 @@ import socket
 
 import pytest
 
-from lodestar_amd.sharded import ShardedVerifier, assign_jobs, VALID, INVALID, ERROR
+from lodestar_amd.sharded import ShardedVerifier, assign_jobs, rank_seed, VALID, INVALID, ERROR
 from oracle import verifier as ov
 from tests import blsdata as bd
 
 
 class OracleBackend:
-    """ShardedVerifier backend computed by the oracle (test infrastructure only)."""
+    """ShardedVerifier backend computed by the oracle (test infrastructure only): the same
+    submit / partial / final_verify / resolve protocol as GpuBackend."""
 
     @staticmethod
     def _rands(seed, n):
         rng = random.Random(seed)
         return [rng.getrandbits(64) or 1 for _ in range(n)]
 
-    def batch_partial(self, sets, seed=0):
-        flat = [(pks[0], m, s) for pks, m, s in sets]
-        part, errs = ov.batch_partial(flat, self._rands(seed, len(flat)))
-        return part, errs, any(errs)
+    def submit(self, jobs, seed=0):
+        return (jobs, seed)
+
+    def partial(self, handle):
+        from oracle.curves import g1_serialize
+        jobs, seed = handle
+        flat = [(g1_serialize(ov.aggregate_pubkeys([ov.public_key_from_bytes(p) for p in pks])), m, s)
+                for sets, flags in jobs if flags & 1 for pks, m, s in sets]
+        part, _errs = ov.batch_partial(flat, self._rands(seed, len(flat)))
+        return part, bool(flat)
 
     def final_verify(self, partials):
         return ov.final_verify_partials(list(partials))
+
+    def resolve(self, handle, node_valid):
+        jobs, seed = handle
+        return self.verify_jobs(jobs, seed)
 
     def verify_jobs(self, jobs, seed=0):
         reqs = []
@@ -41,7 +52,7 @@ class OracleBackend:
         res = []
         for kind, val in out["results"]:
             res.append((VALID if val else INVALID, 0) if kind == "success" else (ERROR, val))
-        return res, out
+        return res, {"batch_retries": out["batch_retries"]}
 
 
 def make_jobs(corrupt=None):
@@ -67,6 +78,13 @@ def test_assign_jobs_balanced_and_whole():
     assert assign_jobs([1] * 8, 4) == [0, 0, 1, 1, 2, 2, 3, 3]
     assert assign_jobs([3, 0, 3], 8) == [0, 4, 4]
     assert assign_jobs([], 2) == [] and assign_jobs([2, 2], 1) == [0, 0]
+
+
+def test_rank_seed_keeps_os_randomness():
+    """seed 0 (production) must reach every rank unchanged, so that the RLC
+    randomizers come from the OS CSPRNG on every rank, never from a public splitmix sequence."""
+    assert [rank_seed(0, r) for r in range(8)] == [0] * 8
+    assert [rank_seed(5, r) for r in range(3)] == [5, 6, 7]
 
 
 def test_sharded_single_rank_matches_worker_semantics():
@@ -99,8 +117,11 @@ def _rank_main(rank, world, port, case, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,retried", [("valid", []), ("wrong_msg", [1]), ("truncated", [0])])
-def test_sharded_gloo_world2(case, retried):
+# the node check covers every set that decodes (an undecodable set contributes nothing and
+# its job errors through the chunk rules), so only the wrong-message case fails it
+@pytest.mark.parametrize("case,retried,combined", [("valid", [], True), ("wrong_msg", [1], False),
+                                                   ("truncated", [0], True)])
+def test_sharded_gloo_world2(case, retried, combined):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -115,7 +136,7 @@ def test_sharded_gloo_world2(case, retried):
     corrupt = {"valid": None, "wrong_msg": (3, 1, bd.corrupt_wrong_message),
                "truncated": (0, 0, bd.corrupt_truncate)}[case]
     exp = expected(make_jobs(corrupt))
-    for rank, results, combined, rr in got:
+    for rank, results, combined_ok, rr in got:
         assert results == exp, (rank, results, exp)
-        assert combined == (case == "valid")
+        assert combined_ok == combined
         assert rr == retried
