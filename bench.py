@@ -332,7 +332,8 @@ def main():
             lat.append(time.perf_counter() - t_sub)
             if not verdict_ok(k, res, t[1]):
                 raise SystemExit(f"rank {rank}: package {k} verdicts differ from the expected ones")
-            stats_acc.update({"batch_retries": st["batch_retries"], "n_final_exps": st["n_final_exps"]})
+            stats_acc.update({"batch_retries": st["batch_retries"], "n_final_exps": st["n_final_exps"],
+                              "submit_us": st["submit_us"], "packages": 1})
             if capture:
                 times.append(ctx.last_kernel_times())
             done += 1
@@ -435,6 +436,7 @@ def main():
             "pipeline_depth": args.depth, "distinct_packages": len(prepared),
             "allocations_in_timed_region": allocs,
             "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
+            "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},

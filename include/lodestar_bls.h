@@ -113,10 +113,10 @@ typedef struct {
 typedef struct {
   uint32_t batch_retries;
   uint32_t batch_sigs_success;
-  uint64_t start_ns;
-  uint64_t end_ns;
-  uint32_t n_final_exps; /* final exponentiations run (package, chunk and job groups; node check) */
-  uint32_t reserved;
+  uint64_t start_ns;      /* CLOCK_MONOTONIC ns (process.hrtime's clock): submit entered */
+  uint64_t end_ns;        /* CLOCK_MONOTONIC ns: verdicts resolved */
+  uint32_t n_final_exps;  /* final exponentiations run (package, chunk and job groups; node check) */
+  uint32_t submit_us;     /* host time inside lsg_submit_jobs (staging, randomizers, plans, launches) */
 } lsg_stats;
 
 /* A context over one or more devices.  Per device it owns 16 pipeline slots (each: a main

@@ -81,7 +81,7 @@ class LsgStats(ctypes.Structure):
     _fields_ = [
         ("batch_retries", ctypes.c_uint32), ("batch_sigs_success", ctypes.c_uint32),
         ("start_ns", ctypes.c_uint64), ("end_ns", ctypes.c_uint64),
-        ("n_final_exps", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+        ("n_final_exps", ctypes.c_uint32), ("submit_us", ctypes.c_uint32),
     ]
 
 
@@ -346,7 +346,7 @@ class Context:
     @staticmethod
     def _results(res, st, n):
         out = [(res[i].status, res[i].err_code) for i in range(n)]
-        stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
+        stats = {k: getattr(st, k) for k, _ in LsgStats._fields_ }
         return out, stats
 
     def wait_jobs(self, ticket, raw=False):
@@ -362,7 +362,7 @@ class Context:
         self._check(self.lib.lsg_wait_jobs_node(self.h, t, int(node_valid), res, ctypes.byref(st)),
                     "lsg_wait_jobs_node")
         if raw:
-            return res, {k: getattr(st, k) for k, _ in LsgStats._fields_ if k != "reserved"}
+            return res, {k: getattr(st, k) for k, _ in LsgStats._fields_ }
         return self._results(res, st, n)
 
     def jobs_partial(self, ticket):

@@ -55,7 +55,7 @@ constexpr int LSG_MILLER_KMAX = 4;
 
 uint64_t now_ns() {
   timespec ts;
-  clock_gettime(CLOCK_REALTIME, &ts);
+  clock_gettime(CLOCK_MONOTONIC, &ts);  // process.hrtime's clock (the Node host's metrics)
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
@@ -83,6 +83,15 @@ bool os_random(void* buf, size_t len) {
 }
 
 std::atomic<uint64_t> g_allocs{0};  // device + pinned allocations made (lsg_allocation_count)
+
+// env LSG_TRACE_ALLOC=1: one stderr line per allocation (size and caller), for steady-state checks
+void trace_alloc(const char* kind, size_t bytes) {
+  static const bool on = [] {
+    const char* e = getenv("LSG_TRACE_ALLOC");
+    return e && atoi(e) != 0;
+  }();
+  if (on) fprintf(stderr, "[lsg alloc] %s %zu bytes\n", kind, bytes);
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -278,6 +287,7 @@ struct Slot {
   std::vector<lsg_job_result> results;
   lsg_stats stats;
   bool has_node = false;  // this slot computed the node check (device 0 of a multi-device ticket)
+  size_t n_jobs = 0;      // device 0: the ticket's job count
 };
 
 struct Dev {
@@ -341,6 +351,7 @@ int ensure(Slot* s, DevBuf& b, size_t bytes) {
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess) return fail(s, "hipMalloc", e);
   g_allocs++;
+  trace_alloc("device", cap);
   b.cap = cap;
   return LSG_OK;
 }
@@ -355,6 +366,7 @@ int ensure_host(Slot* s, HostBuf& b, size_t bytes) {
   hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
   if (e != hipSuccess) return fail(s, "hipHostMalloc", e);
   g_allocs++;
+  trace_alloc("pinned", cap);
   b.cap = cap;
   return LSG_OK;
 }
@@ -487,6 +499,18 @@ bool package_group_mode() {
   return !(e && atoi(e) == 0);
 }
 
+void binv_sizes(size_t n, size_t* lv, size_t* iv);
+size_t binv_lv_words(size_t n) {
+  size_t a, b;
+  binv_sizes(n, &a, &b);
+  return a;
+}
+size_t binv_iv_words(size_t n) {
+  size_t a, b;
+  binv_sizes(n, &a, &b);
+  return b;
+}
+
 // inputs for up to n sets / np keys / mb message bytes
 int size_inputs(Slot* s, size_t n, size_t np, size_t mb) {
   const size_t nn = std::max(n, (size_t)1), pp = std::max(np, (size_t)1);
@@ -534,10 +558,10 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, bool pkg =
              {&s->d_Hp, 4 * W_G2P * nn},
              {&s->d_zN, 4 * W_FP * nn},
              {&s->d_zNi, 4 * W_FP * nn},
-             {&s->binv_lv[0], 4 * W_FP * 2 * nn},
-             {&s->binv_iv[0], 4 * W_FP * 2 * nn},
-             {&s->binv_lv[1], 4 * W_FP * nn},
-             {&s->binv_iv[1], 4 * W_FP * nn},
+             {&s->binv_lv[0], 4 * W_FP * binv_lv_words(2 * nn)},
+             {&s->binv_iv[0], 4 * W_FP * binv_iv_words(2 * nn)},
+             {&s->binv_lv[1], 4 * W_FP * binv_lv_words(nn)},
+             {&s->binv_iv[1], 4 * W_FP * binv_iv_words(nn)},
              {&s->d_S, 4 * W_G2P * gg},
              {&s->d_F, 4 * W_F12 * gg},
              {&s->d_verdict, 4 * gg},
@@ -599,30 +623,54 @@ int run_seg(Slot* s, int use, const char* name, const SegPlan& P, const uint32_t
   return LSG_OK;
 }
 
-// out[i] = 1 / v[i] (0 for v[i] = 0) for n lane-form Fp values, on the current stream: a
-// product tree up, one inversion at the root, products back down (Montgomery's trick).
+// Words (per Fp of W_FP) of the two scratch arrays a batched inversion of n values needs:
+// lv = every level's prefix products plus levels >= 1's values, iv = levels >= 1's inverses
+void binv_sizes(size_t n, size_t* lv, size_t* iv) {
+  size_t a = 0, b = 0;
+  for (size_t m = n; m > 1;) {
+    const size_t up = (m + LSG_BINV_T - 1) / LSG_BINV_T;
+    a += m + up;
+    b += up;
+    m = up;
+  }
+  *lv = std::max(a, (size_t)1);
+  *iv = std::max(b, (size_t)1);
+}
+
+// out[i] = 1 / v[i] (0 for v[i] = 0) for n lane-form Fp values on the current stream
+// (Montgomery's trick in chunks of LSG_BINV_T per lane pair: lsg_k_reduce.hip)
 int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, uint32_t* out) {
   if (n == 0) return LSG_OK;
-  std::vector<size_t> sz{n}, off{0};
-  size_t total = 0;
-  do {
-    size_t m = (sz.back() + 1) / 2;
-    off.push_back(total);
-    sz.push_back(m);
-    total += m;
-  } while (sz.back() > 1);
-  LSG_RC(ensure(s, s->binv_lv[ws], 4 * W_FP * total));
-  LSG_RC(ensure(s, s->binv_iv[ws], 4 * W_FP * total));
+  size_t lvw, ivw;
+  binv_sizes(n, &lvw, &ivw);
+  LSG_RC(ensure(s, s->binv_lv[ws], 4 * W_FP * lvw));
+  LSG_RC(ensure(s, s->binv_iv[ws], 4 * W_FP * ivw));
   uint32_t* lv = P_<uint32_t>(s->binv_lv[ws]);
   uint32_t* iv = P_<uint32_t>(s->binv_iv[ws]);
-  const size_t L = sz.size() - 1;
-  auto lvl = [&](size_t k) { return k == 0 ? (uint32_t*)v : lv + W_FP * off[k]; };
-  for (size_t k = 1; k <= L; k++)
-    KL(s, name, lsgk::binv_up(S_(s), (int)sz[k], (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1), lvl(k)));
-  KL(s, name, lsgk::binv_root(S_(s), lvl(L), iv + W_FP * off[L]));
-  for (size_t k = L; k >= 1; k--)
-    KL(s, name, lsgk::binv_down(S_(s), (int)sz[k - 1], k == 1 ? 1 : 0, lvl(k - 1), iv + W_FP * off[k],
-                                k == 1 ? out : iv + W_FP * off[k - 1]));
+  // level l: values val[l] (val[0] = v), prefix products pre[l], inverses inv[l] (inv[0] = out)
+  std::vector<size_t> cnt{n};
+  std::vector<uint32_t*> val{(uint32_t*)v}, pre, inv{out};
+  size_t lo = 0, io = 0;
+  while (cnt.back() > 1) {
+    const size_t m = cnt.back(), up = (m + LSG_BINV_T - 1) / LSG_BINV_T;
+    pre.push_back(lv + W_FP * lo);
+    lo += m;
+    val.push_back(lv + W_FP * lo);
+    lo += up;
+    inv.push_back(iv + W_FP * io);
+    io += up;
+    cnt.push_back(up);
+  }
+  const size_t L = cnt.size() - 1;
+  if (L == 0) {  // one value: invert it directly (0 stays 0)
+    KL(s, name, lsgk::binv_root(S_(s), v, out));
+    return LSG_OK;
+  }
+  for (size_t l = 0; l < L; l++)
+    KL(s, name, lsgk::binv_fold(S_(s), (int)cnt[l], l == 0 ? 1 : 0, val[l], pre[l], val[l + 1]));
+  KL(s, name, lsgk::binv_root(S_(s), val[L], inv[L]));
+  for (size_t l = L; l-- > 0;)
+    KL(s, name, lsgk::binv_unfold(S_(s), (int)cnt[l], l == 0 ? 1 : 0, val[l], pre[l], inv[l + 1], inv[l]));
   return LSG_OK;
 }
 
@@ -1434,7 +1482,8 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
     s->kind = SLOT_JOBS;
     s->serial = serial;
   }
-  c->dev[0]->slots[p].stats.reserved = (uint32_t)n_jobs;  // the ticket's job count
+  c->dev[0]->slots[p].n_jobs = n_jobs;
+  c->dev[0]->slots[p].stats.submit_us = (uint32_t)((now_ns() - c->dev[0]->slots[p].stats.start_ns) / 1000);
   return LSG_OK;
 }
 
@@ -1452,6 +1501,7 @@ int wait_pkg(lsg_ctx* c, int p, int node_valid, lsg_job_result* results, lsg_sta
   lsg_stats total;
   memset(&total, 0, sizeof(total));
   total.start_ns = s0->stats.start_ns;
+  total.submit_us = s0->stats.submit_us;
   for (int d = 0; d < n && !rc; d++) {
     Slot* s = &c->dev[d]->slots[p];
     (void)hipSetDevice(c->dev[d]->device);
@@ -1780,7 +1830,7 @@ int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_jo
   LSG_ENTER(c);
   const int p = ticket_pkg(c, ticket);
   if (p < 0) return LSG_ERR_INVALID_ARG;
-  const uint32_t nj = c->dev[0]->slots[p].stats.reserved;
+  const size_t nj = c->dev[0]->slots[p].n_jobs;
   if (nj && !results) return LSG_ERR_INVALID_ARG;
   if (node_valid != -1 && c->n_dev > 1) {
     c->err = "lsg_wait_jobs_node: a multi-device context runs its own node check";

@@ -81,43 +81,54 @@ __global__ void LSG_KERNEL_ATTR_W(OP == 2 ? 1 : LSG_WAVES_PER_EU)
   }
 }
 
-// ---- batched field inversion (Montgomery's trick as a product tree over the batch): every
-// field inversion of a stage -- 1/Z of the scaled pubkeys, 1/N(tv1) of the SSWU maps, 1/N(Z)
-// of the hashed points -- shares one exponentiation per batch instead of one per set.
-// Zero inputs (points at infinity, the SSWU exceptional case) are carried as 1 through the
-// tree and come out as 0, the value fp_inv(0) gives.
-// level up: out[i] = in[2i] * in[2i+1] (a missing right child is 1)
-__global__ void LSG_KERNEL_ATTR k_binv_up(int n_out, int n_in, int zero_to_one, const uint32_t* __restrict__ in,
-                                          uint32_t* __restrict__ out) {
-  LANE_ITEM(n_out);
+// ---- batched field inversion (Montgomery's trick, chunked): every field inversion of a
+// stage -- 1/Z of the scaled pubkeys, 1/N(tv1) of the SSWU maps, 1/N(Z) of the hashed points
+// -- shares one exponentiation per batch instead of one per set.  A level folds chunks of
+// LSG_BINV_T consecutive values per lane pair (prefix products, one chunk product each); the
+// chunk products are the next level's values, up to one value, whose inverse unfolds back
+// down (two products per value).  log_T(n) launches each way instead of log_2(n).  Zero
+// inputs (points at infinity, the SSWU exceptional case) are carried as 1 and come out as 0,
+// the value fp_inv(0) gives.
+__global__ void LSG_KERNEL_ATTR k_binv_fold(int n, int zero_to_one, const uint32_t* __restrict__ in,
+                                            uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
+  const int n_chunks = (n + LSG_BINV_T - 1) / LSG_BINV_T;
+  LANE_ITEM(n_chunks);
   (void)lead;
   const fp_t one = fp_one();
-  fp_t a = lane_load<fp_t>(in, 2 * item);
-  fp_t b = (2 * (int)item + 1 < n_in) ? lane_load<fp_t>(in, 2 * item + 1) : one;
-  if (zero_to_one) {
-    a = fp_select(fp_is_zero(a), one, a);
-    b = fp_select(fp_is_zero(b), one, b);
+  const int first = (int)item * LSG_BINV_T, last = min(n, first + LSG_BINV_T);
+  fp_t acc = one;
+#pragma unroll 1
+  for (int k = first; k < last; k++) {
+    fp_t x = lane_load<fp_t>(in, k);
+    if (zero_to_one) x = fp_select(fp_is_zero(x), one, x);
+    acc = k == first ? x : fp_mul(acc, x);
+    lane_store(pre, k, acc);
   }
-  lane_store(out, item, fp_mul(a, b));
+  lane_store(tot, item, acc);
 }
 __global__ void LSG_KERNEL_ATTR k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
   LANE_ITEM(1);
   (void)lead;
   lane_store(inv, 0, fp_inv(lane_load<fp_t>(top, 0)));
 }
-// level down: inv(child c) = inv(parent c/2) * value(sibling c^1); at level 0 (zero_to_one)
-// zero children get 0
-__global__ void LSG_KERNEL_ATTR k_binv_down(int n_child, int zero_to_one, const uint32_t* __restrict__ vals,
-                                            const uint32_t* __restrict__ pinv, uint32_t* __restrict__ cinv) {
-  LANE_ITEM(n_child);
+// out[k] = 1 / in[k] from the chunk's inverse product tinv[chunk] and the prefix products
+__global__ void LSG_KERNEL_ATTR k_binv_unfold(int n, int zero_to_one, const uint32_t* __restrict__ in,
+                                              const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tinv,
+                                              uint32_t* __restrict__ out) {
+  const int n_chunks = (n + LSG_BINV_T - 1) / LSG_BINV_T;
+  LANE_ITEM(n_chunks);
   (void)lead;
   const fp_t one = fp_one();
-  const int sib = (int)item ^ 1;
-  fp_t s = sib < n_child ? lane_load<fp_t>(vals, sib) : one;
-  if (zero_to_one) s = fp_select(fp_is_zero(s), one, s);
-  fp_t r = fp_mul(lane_load<fp_t>(pinv, item >> 1), s);
-  if (zero_to_one) r = fp_select(fp_is_zero(lane_load<fp_t>(vals, item)), fp_zero(), r);
-  lane_store(cinv, item, r);
+  const int first = (int)item * LSG_BINV_T, last = min(n, first + LSG_BINV_T);
+  fp_t acc = lane_load<fp_t>(tinv, item);  // 1 / (in[first] * ... * in[last-1])
+#pragma unroll 1
+  for (int k = last - 1; k >= first; k--) {
+    fp_t x = lane_load<fp_t>(in, k);
+    const bool z = zero_to_one && fp_is_zero(x);
+    fp_t r = k > first ? fp_mul(acc, lane_load<fp_t>(pre, k - 1)) : acc;
+    lane_store(out, k, z ? fp_zero() : r);
+    if (k > first && !z) acc = fp_mul(acc, x);
+  }
 }
 
 // partials: canonical big-endian 576-byte Fp12 blobs <-> lane form (one item each)
@@ -175,15 +186,15 @@ hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const 
   if (op == 1) LSG_LAUNCH_ITEMS(k_seg_reduce<1>, items, st, n_chunks, ips_log2, chunks, idx, src, dst, tmp);
   LSG_LAUNCH_ITEMS(k_seg_reduce<2>, items, st, n_chunks, ips_log2, chunks, idx, src, dst, tmp);
 }
-hipError_t binv_up(hipStream_t st, int n_out, int n_in, int zero_to_one, const uint32_t* in, uint32_t* out) {
-  LSG_LAUNCH_ITEMS(k_binv_up, n_out, st, n_out, n_in, zero_to_one, in, out);
+hipError_t binv_fold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* tot) {
+  LSG_LAUNCH_ITEMS(k_binv_fold, (n + LSG_BINV_T - 1) / LSG_BINV_T, st, n, zero_to_one, in, pre, tot);
 }
 hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv) {
   LSG_LAUNCH_ITEMS(k_binv_root, 1, st, top, inv);
 }
-hipError_t binv_down(hipStream_t st, int n_child, int zero_to_one, const uint32_t* vals, const uint32_t* pinv,
-                     uint32_t* cinv) {
-  LSG_LAUNCH_ITEMS(k_binv_down, n_child, st, n_child, zero_to_one, vals, pinv, cinv);
+hipError_t binv_unfold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, const uint32_t* pre,
+                       const uint32_t* tinv, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_binv_unfold, (n + LSG_BINV_T - 1) / LSG_BINV_T, st, n, zero_to_one, in, pre, tinv, out);
 }
 hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* out) {
   LSG_LAUNCH_ITEMS(k_blobs_to_fp12, n, st, n, blobs, out);

@@ -62,10 +62,12 @@ hipError_t miller_accum(hipStream_t st, int K, int n_items, const int32_t* item_
 // every 2^ips_log2-th element serially, then a lane butterfly combines them.
 hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const int32_t* chunks, const int32_t* idx,
                       const uint32_t* src, uint32_t* dst, uint32_t* tmp);
-hipError_t binv_up(hipStream_t st, int n_out, int n_in, int zero_to_one, const uint32_t* in, uint32_t* out);
+// batched inversion, chunks of LSG_BINV_T values per lane pair: fold (prefix products pre and
+// chunk products tot), root (one inversion), unfold (out = 1/in, 0 for zeros when zero_to_one)
+hipError_t binv_fold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* tot);
 hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv);
-hipError_t binv_down(hipStream_t st, int n_child, int zero_to_one, const uint32_t* vals, const uint32_t* pinv,
-                     uint32_t* cinv);
+hipError_t binv_unfold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, const uint32_t* pre,
+                       const uint32_t* tinv, uint32_t* out);
 hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* out);
 hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out576);
 hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io);

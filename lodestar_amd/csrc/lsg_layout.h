@@ -23,3 +23,4 @@ constexpr int MSM_WINDOWS = 8;       // bucket MSM of the RLC signature sums: 8-
 constexpr int MSM_DIGITS = 255;      // nonzero digits per window
 constexpr int MSM_BITS = 64;         // per-bit sums C_k, S = sum_k 2^k C_k
 }  // namespace lsgl
+#define LSG_BINV_T 16  // values per lane pair in one level of the batched inversion

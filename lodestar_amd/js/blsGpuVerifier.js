@@ -25,6 +25,23 @@
  * worker's batch + per-job retry rules (worker.ts:30-106) itself, so one package costs one
  * round trip.  Aggregate sets send all their pubkeys; the GPU sums them (utils.ts:11).
  *
+ * Node-wide: chain.ts:195-198 builds ONE verifier per node, its pool spanning every core
+ * (multithread/poolSize.ts:7).  options.devices = [0, 1, ...] opens one context over all the
+ * node's GPUs (lsg_init_devices): a package is split into whole jobs per GPU, the GPUs'
+ * partials are all-gathered over RCCL and checked by one final exponentiation (SURVEY 8e).
+ *
+ * BlsGpuSingleThreadVerifier restates BlsSingleThreadVerifier (singleThread.ts:14-35): one
+ * synchronous maybeBatch call per verifySignatureSets, no queue, no retry, opts ignored.
+ * createBlsVerifier picks between the two as chain.ts:196-198 does (blsVerifyAllMainThread).
+ *
+ * Metrics: the reference's names and observation points (metrics/metrics/lodestar.ts:350-430,
+ * multithread/index.ts:319-381): jobWaitTime, totalJobsGroupsStarted, totalJobsStarted,
+ * totalSigSetsStarted, timePerSigSet, jobsWorkerTime{workerId}, latencyToWorker,
+ * latencyFromWorker, successJobsSignatureSetsCount, errorJobsSignatureSetsCount,
+ * batchRetries, batchSigsSuccess, mainThreadDurationInThreadPool, bls.aggregatedPubkeys.
+ * "Worker" times are the GPU package's start/end (lsg_stats, CLOCK_MONOTONIC = the clock of
+ * process.hrtime.bigint()); workerId is the pipeline slot that ran the package.
+ *
  * Extensions required by the north star (SURVEY.md 8b, not in the reference snapshot):
  *   opts.priority                  queue at the head instead of the tail
  *   verifySignatureSetsSameMessage per-set verdicts for sets sharing one message
@@ -145,7 +162,8 @@ function loadAddon() {
 
 class BlsGpuVerifier {
   /**
-   * @param {{blsVerifyAllMultiThread?: boolean, device?: number, seed?: number}} options
+   * @param {{blsVerifyAllMultiThread?: boolean, device?: number, devices?: number[], seed?: number,
+   *          maxSigsPerPackage?: number, reserveSets?: number, reservePubkeys?: number}} options
    * @param {{logger?: object, metrics?: object|null, addon?: object}} modules  addon is
    *        injectable (tests drive the queue logic with a mock of the addon's surface)
    */
@@ -159,8 +177,14 @@ class BlsGpuVerifier {
     // production node sets e.g. 4096.  Per-job verdicts do not depend on it.
     this.maxSigsPerPackage = options.maxSigsPerPackage || MAX_SIGNATURE_SETS_PER_JOB;
     this.addon = modules.addon || loadAddon();
-    this.ctx = this.addon.open(options.device || 0); // throws loudly without a gfx950 device
+    // throws loudly without a gfx950 device
+    this.ctx = this.addon.open(Array.isArray(options.devices) ? options.devices : options.device || 0);
     this.poolSize = this.addon.slots(this.ctx);
+    if (options.reserveSets && this.addon.reserve) {
+      // preallocate every pipeline slot for packages of up to reserveSets sets (lsg_reserve)
+      const pks = options.reservePubkeys || options.reserveSets;
+      this.addon.reserve(this.ctx, options.reserveSets, pks, 32 * options.reserveSets, 0);
+    }
     this.jobs = [];
     this.bufferedJobs = null;
     this.closed = false;
@@ -195,9 +219,15 @@ class BlsGpuVerifier {
 
     if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
       // verifySignatureSetsMaybeBatch on the calling thread: no retry, errors propagate
-      const r = this.addon.verifySets(this.ctx, sets.map(serializeSet), this.seed);
-      if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
-      return r.status === LSG_VALID;
+      const m = this.metrics && this.metrics.blsThreadPool;
+      const timer = m ? m.mainThreadDurationInThreadPool.startTimer() : null;
+      try {
+        const r = this.addon.verifySets(this.ctx, sets.map(serializeSet), this.seed);
+        if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
+        return r.status === LSG_VALID;
+      } finally {
+        if (timer) timer();
+      }
     }
 
     const results = await Promise.all(
@@ -303,9 +333,11 @@ class BlsGpuVerifier {
           sets: job.workReq.sets,
           flags: (job.workReq.opts.batchable ? JOB_BATCHABLE : 0) | (job.workReq.opts.priority ? JOB_PRIORITY : 0),
         }));
+        const jobStartNs = process.hrtime.bigint();
         const ticket = this.addon.submitJobs(this.ctx, pkg, this.seed);
         if (ticket === null) throw Error("BlsGpuVerifier: every pipeline slot is busy");
         const workResult = await this.addon.waitJobs(this.ctx, ticket);
+        const jobEndNs = process.hrtime.bigint();
         let successCount = 0;
         let errorCount = 0;
         for (let i = 0; i < jobs.length; i++) {
@@ -324,8 +356,14 @@ class BlsGpuVerifier {
           }
         }
         if (m) {
+          // index.ts:362-381, with the GPU package in the worker's place
           const workerJobTimeSec = (workResult.endNs - workResult.startNs) / 1e9;
+          const latencyToWorkerSec = (workResult.startNs - Number(jobStartNs)) / 1e9;
+          const latencyFromWorkerSec = (Number(jobEndNs) - workResult.endNs) / 1e9;
           m.timePerSigSet.observe(workerJobTimeSec / startedSigSets);
+          m.jobsWorkerTime.inc({workerId: workResult.workerId || 0}, workerJobTimeSec);
+          m.latencyToWorker.observe(latencyToWorkerSec);
+          m.latencyFromWorker.observe(latencyFromWorkerSec);
           m.successJobsSignatureSetsCount.inc(successCount);
           m.errorJobsSignatureSetsCount.inc(errorCount);
           m.batchRetries.inc(workResult.batchRetries);
@@ -364,8 +402,65 @@ class BlsGpuVerifier {
   }
 }
 
+/**
+ * BlsSingleThreadVerifier (chain/bls/singleThread.ts:14-35) on the GPU: each call is one
+ * verifySignatureSetsMaybeBatch (lsg_verify_sets) made synchronously from the calling thread,
+ * with no queue and no retry; opts are ignored, errors propagate as throws.  The duration is
+ * observed after the call as the reference does (it observes the total and the per-set time;
+ * its startNs - endNs has the sign inverted, here the duration is positive).
+ */
+class BlsGpuSingleThreadVerifier {
+  /**
+   * @param {{device?: number, devices?: number[], seed?: number}} options
+   * @param {{metrics?: object|null, addon?: object}} modules
+   */
+  constructor(options = {}, modules = {}) {
+    this.metrics = modules.metrics || null;
+    this.seed = options.seed || 0;
+    this.addon = modules.addon || loadAddon();
+    this.ctx = this.addon.open(Array.isArray(options.devices) ? options.devices : options.device || 0);
+  }
+
+  async verifySignatureSets(sets) {
+    if (this.metrics && this.metrics.bls) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
+    const setsAggregated = sets.map(serializeSet);
+    // Count time after aggregating
+    const startNs = process.hrtime.bigint();
+    const r = this.addon.verifySets(this.ctx, setsAggregated, this.seed);
+    if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
+    // Don't use a try/catch, only count run without exceptions
+    const endNs = process.hrtime.bigint();
+    const totalSec = Number(endNs - startNs) / 1e9;
+    const m = this.metrics && this.metrics.blsThreadPool;
+    if (m) {
+      m.mainThreadDurationInThreadPool.observe(totalSec);
+      m.mainThreadDurationInThreadPool.observe(totalSec / sets.length);
+    }
+    return r.status === LSG_VALID;
+  }
+
+  async close() {
+    if (this.ctx) {
+      this.addon.close(this.ctx);
+      this.ctx = null;
+    }
+  }
+
+  canAcceptWork() {
+    // Since sigs are verified blocking the main thread, there's no mechanism to throttle
+    return true;
+  }
+}
+
+/** chain.ts:195-198: opts.blsVerifyAllMainThread selects the single-thread verifier. */
+function createBlsVerifier(opts = {}, modules = {}) {
+  return opts.blsVerifyAllMainThread ? new BlsGpuSingleThreadVerifier(opts, modules) : new BlsGpuVerifier(opts, modules);
+}
+
 module.exports = {
   BlsGpuVerifier,
+  BlsGpuSingleThreadVerifier,
+  createBlsVerifier,
   QueueError,
   QueueErrorCode,
   SignatureSetType,

@@ -11,7 +11,10 @@
  * the JS main thread never blocks on the GPU.  Nothing here does arithmetic.
  *
  * JS surface (all synchronous unless noted):
- *   open(device) -> ctx                     lsg_init
+ *   open(device | devices[]) -> ctx         lsg_init / lsg_init_devices (one context over the
+ *                                           node's GPUs: chain.ts:195-198 builds one verifier)
+ *   reserve(ctx, maxSets, maxPks, maxMsgBytes, nSlots)                  lsg_reserve
+ *   deviceCount(ctx) -> n                   lsg_device_count
  *   close(ctx)                              lsg_destroy
  *   slots(ctx) -> n                         lsg_pipeline_slots
  *   deviceName(ctx) -> string               lsg_device_name
@@ -19,7 +22,10 @@
  *       jobs = [{sets: [{pubkeys: Uint8Array[], message: Uint8Array, signature: Uint8Array}],
  *                flags: number}]
  *   waitJobs(ctx, ticket) -> Promise<{results: [{status, errCode}], batchRetries,
- *                                     batchSigsSuccess, startNs, endNs}>   lsg_wait_jobs
+ *                                     batchSigsSuccess, startNs, endNs, finalExps,
+ *                                     workerId}>   lsg_wait_jobs
+ *       startNs / endNs are CLOCK_MONOTONIC nanoseconds (process.hrtime.bigint()'s clock);
+ *       workerId is the pipeline slot that ran the package (the reference's workerId label)
  *   verifySets(ctx, sets, seed) -> {status, errCode}                   lsg_verify_sets
  *   aggregatePubkeys(ctx, pubkeys[]) -> {errCode, bytes: Uint8Array(96)} lsg_aggregate_pubkeys
  *   pubkeyTableSet(ctx, firstIndex, pubkeys[]) -> errCodes[]          lsg_pubkey_table_set
@@ -224,10 +230,30 @@ static napi_value js_open(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  int32_t dev = 0;
-  if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
   lsg_ctx* ctx = NULL;
-  int rc = lsg_init(dev, &ctx);
+  int rc;
+  bool is_arr = false;
+  if (argc >= 1) napi_is_array(env, argv[0], &is_arr);
+  if (is_arr) {
+    uint32_t n = array_len(env, argv[0]);
+    if (n == 0 || n > 64) {
+      napi_throw_range_error(env, NULL, "lsg_napi: open() expects 1..64 device ids");
+      return NULL;
+    }
+    int ids[64];
+    for (uint32_t k = 0; k < n; k++) {
+      napi_value e;
+      napi_get_element(env, argv[0], k, &e);
+      int32_t d = 0;
+      napi_get_value_int32(env, e, &d);
+      ids[k] = d;
+    }
+    rc = lsg_init_devices(ids, (int)n, &ctx);
+  } else {
+    int32_t dev = 0;
+    if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
+    rc = lsg_init(dev, &ctx);
+  }
   if (rc != LSG_OK) return throw_lsg(env, NULL, "lsg_init (no gfx950 device?)", rc);
   napi_value ext;
   NAPI_CALL(env, napi_create_external(env, ctx, finalize_noop, NULL, &ext));
@@ -242,6 +268,31 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   if (!ctx) return NULL;
   lsg_destroy(ctx);
   return NULL;
+}
+
+static napi_value js_reserve(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  double v[4] = {0, 0, 0, 0};
+  for (size_t k = 1; k < argc && k < 5; k++) napi_get_value_double(env, argv[k], &v[k - 1]);
+  int rc = lsg_reserve(ctx, (size_t)v[0], (size_t)v[1], (size_t)v[2], (int32_t)v[3]);
+  if (rc) return throw_lsg(env, ctx, "lsg_reserve", rc);
+  return NULL;
+}
+
+static napi_value js_device_count(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t n = 0;
+  int rc = lsg_device_count(ctx, &n);
+  if (rc) return throw_lsg(env, ctx, "lsg_device_count", rc);
+  return make_int(env, n);
 }
 
 static napi_value js_slots(napi_env env, napi_callback_info info) {
@@ -359,6 +410,7 @@ static void wait_complete(napi_env env, napi_status status, void* data) {
     set_int(env, o, "startNs", (int64_t)w->stats.start_ns);
     set_int(env, o, "endNs", (int64_t)w->stats.end_ns);
     set_int(env, o, "finalExps", w->stats.n_final_exps);
+    set_int(env, o, "workerId", (int64_t)(w->ticket & 0xff));
     napi_resolve_deferred(env, w->deferred, o);
   }
   napi_delete_async_work(env, w->work);
@@ -633,6 +685,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"open", NULL, js_open, NULL, NULL, NULL, napi_enumerable, NULL},
       {"close", NULL, js_close, NULL, NULL, NULL, napi_enumerable, NULL},
       {"slots", NULL, js_slots, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"reserve", NULL, js_reserve, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceName", NULL, js_device_name, NULL, NULL, NULL, napi_enumerable, NULL},
       {"submitJobs", NULL, js_submit_jobs, NULL, NULL, NULL, napi_enumerable, NULL},
       {"waitJobs", NULL, js_wait_jobs, NULL, NULL, NULL, napi_enumerable, NULL},

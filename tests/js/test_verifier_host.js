@@ -22,9 +22,15 @@ function mockAddon(slots = 2, {holdWaits = false} = {}) {
     opened: 0,
     closed: 0,
     pending: [],
-    open() {
+    openedWith: [],
+    reserved: null,
+    open(dev) {
       m.opened++;
+      m.openedWith.push(dev);
       return {ctx: true};
+    },
+    reserve(ctx, sets, pks, bytes, slotsN) {
+      m.reserved = [sets, pks, bytes, slotsN];
     },
     close() {
       m.closed++;
@@ -56,7 +62,9 @@ function mockAddon(slots = 2, {holdWaits = false} = {}) {
     },
     waitJobs(ctx, t) {
       const results = t.jobs.map((j) => m.jobVerdict(j.sets));
-      const done = {results, batchRetries: 0, batchSigsSuccess: 0, startNs: 0, endNs: 1000};
+      // GPU package start/end on process.hrtime's clock (lsg_stats is CLOCK_MONOTONIC)
+      const startNs = Number(process.hrtime.bigint());
+      const done = {results, batchRetries: 0, batchSigsSuccess: 0, startNs, endNs: startNs + 1e6, workerId: t.ticket % 3};
       const finish = () => {
         m.pending.splice(m.pending.indexOf(t), 1);
         return done;
@@ -298,6 +306,82 @@ test("verifySignatureSetsSameMessage returns per-set verdicts (north-star extens
   const badSig = {publicKey: new Uint8Array(96), signature: new Uint8Array(96).fill(5)};
   const badLen = {publicKey: new Uint8Array(96), signature: new Uint8Array(20)};
   assert.deepStrictEqual(await pool.verifySignatureSetsSameMessage([good, badSig, good, badLen], msg), [true, false, true, false]);
+  await pool.close();
+});
+
+/** A stand-in for the reference's metrics registry (gauges / histograms with the same method
+ * names as prom-client's, metrics/metrics/lodestar.ts:350-430), recording every observation. */
+function mockMetrics() {
+  const rec = {};
+  const gauge = (name) => ({
+    inc(a, b) {
+      (rec[name] = rec[name] || []).push(b === undefined ? a : [a, b]);
+    },
+  });
+  const hist = (name) => ({
+    observe(v) {
+      (rec[name] = rec[name] || []).push(v);
+    },
+    startTimer() {
+      const t0 = process.hrtime.bigint();
+      return () => (rec[name] = rec[name] || []).push(Number(process.hrtime.bigint() - t0) / 1e9);
+    },
+  });
+  const blsThreadPool = {};
+  for (const g of ["jobsWorkerTime", "successJobsSignatureSetsCount", "errorJobsSignatureSetsCount", "totalJobsGroupsStarted",
+                   "totalJobsStarted", "totalSigSetsStarted", "batchRetries", "batchSigsSuccess"])
+    blsThreadPool[g] = gauge(g);
+  for (const h of ["jobWaitTime", "latencyToWorker", "latencyFromWorker", "mainThreadDurationInThreadPool", "timePerSigSet"])
+    blsThreadPool[h] = hist(h);
+  return {rec, metrics: {bls: {aggregatedPubkeys: gauge("aggregatedPubkeys")}, blsThreadPool}};
+}
+
+test("metrics: the reference's names and observation points (index.ts:319-381, lodestar.ts:350-430)", async () => {
+  const a = mockAddon();
+  const {rec, metrics} = mockMetrics();
+  const pool = new V.BlsGpuVerifier({}, {addon: a, metrics});
+  const sets = [0, 1, 2].map((i) => set(i));
+  await Promise.all([pool.verifySignatureSets(sets), pool.verifySignatureSets([set(4, false)])]);
+  for (const k of ["jobWaitTime", "totalJobsGroupsStarted", "totalJobsStarted", "totalSigSetsStarted", "timePerSigSet",
+                   "jobsWorkerTime", "latencyToWorker", "latencyFromWorker", "successJobsSignatureSetsCount",
+                   "errorJobsSignatureSetsCount", "batchRetries", "batchSigsSuccess"])
+    assert.ok(rec[k] && rec[k].length > 0, k);
+  const [labels, sec] = rec.jobsWorkerTime[0];
+  assert.ok("workerId" in labels && Math.abs(sec - 1e-3) < 1e-9, JSON.stringify(rec.jobsWorkerTime));
+  assert.ok(rec.latencyToWorker.every((x) => x >= 0 && x < 1), rec.latencyToWorker);
+  assert.ok(rec.latencyFromWorker.every((x) => x < 1), rec.latencyFromWorker);
+  assert.ok(!rec.mainThreadDurationInThreadPool);
+  assert.strictEqual(await pool.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  assert.strictEqual(rec.mainThreadDurationInThreadPool.length, 1);
+  await pool.close();
+});
+
+test("BlsGpuSingleThreadVerifier: one maybeBatch per call, no retry, throws (singleThread.ts:14-35)", async () => {
+  const a = mockAddon();
+  const {rec, metrics} = mockMetrics();
+  const v = V.createBlsVerifier({blsVerifyAllMainThread: true}, {addon: a, metrics});
+  assert.ok(v instanceof V.BlsGpuSingleThreadVerifier);
+  assert.strictEqual(v.canAcceptWork(), true);
+  const sets = [0, 1, 2].map((i) => set(i));
+  assert.strictEqual(await v.verifySignatureSets(sets), true);
+  assert.strictEqual(await v.verifySignatureSets([set(0), set(1, false)], {batchable: true}), false);
+  const bad = set(2);
+  bad.signature = new Uint8Array(32);
+  await assert.rejects(v.verifySignatureSets([bad]), /BLST_INVALID_SIZE/);
+  assert.strictEqual(a.syncCalls, 3);
+  assert.strictEqual(a.packages.length, 0, "no queue, no worker packages");
+  assert.strictEqual(rec.mainThreadDurationInThreadPool.length, 4, "total and per-set time of the two successful calls");
+  assert.ok(rec.mainThreadDurationInThreadPool.every((x) => x >= 0));
+  await v.close();
+  assert.strictEqual(a.closed, 1);
+  assert.ok(V.createBlsVerifier({}, {addon: mockAddon()}) instanceof V.BlsGpuVerifier);
+});
+
+test("devices / reserveSets open one context over the node's GPUs and preallocate (chain.ts:195-198)", async () => {
+  const a = mockAddon();
+  const pool = new V.BlsGpuVerifier({devices: [0, 1, 2, 3], reserveSets: 32768, maxSigsPerPackage: 32768}, {addon: a});
+  assert.deepStrictEqual(a.openedWith, [[0, 1, 2, 3]]);
+  assert.deepStrictEqual(a.reserved, [32768, 32768, 32 * 32768, 0]);
   await pool.close();
 });
 
