@@ -86,11 +86,10 @@ std::atomic<uint64_t> g_allocs{0};  // device + pinned allocations made (lsg_all
 
 // env LSG_TRACE_ALLOC=1: one stderr line per allocation (size and caller), for steady-state checks
 void trace_alloc(const char* kind, size_t bytes) {
-  static const bool on = [] {
-    const char* e = getenv("LSG_TRACE_ALLOC");
-    return e && atoi(e) != 0;
-  }();
+  const char* e = getenv("LSG_TRACE_ALLOC");  // read per allocation: allocations are rare
+  const bool on = e && atoi(e) != 0;
   if (on) fprintf(stderr, "[lsg alloc] %s %zu bytes\n", kind, bytes);
+  (void)on;
 }
 
 struct DevBuf {
@@ -134,11 +133,14 @@ struct SegPlan {
   std::vector<SegPass> passes;
   size_t tmp_items = 0;  // per tmp buffer
 };
-constexpr int SEG_FOLD = 8;  // serial folds per lane pair within one pass
+constexpr int SEG_FOLD = 16;  // at most this many serial folds per lane pair within one pass
 
-int ips_for(double avg) {
+// lane pairs per chunk (log2): enough that the longest segment fits one chunk of SEG_FOLD
+// folds per pair (one pass), and at least a quarter of the mean length (latency: folds are
+// serial, the butterfly is log2(ips) steps); at most a wave's 32 pairs
+int ips_for(double avg, int32_t max_len) {
   int l = 0;
-  while (l < 5 && (double)(2 << l) * 4.0 <= avg) l++;
+  while (l < 5 && ((int32_t)(SEG_FOLD << l) < max_len || (double)(2 << l) * 4.0 <= avg)) l++;
   return l;
 }
 
@@ -164,7 +166,9 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
   int src = 0, tmp_out = 1;
   while (!cur.empty()) {
     SegPass pass;
-    pass.ips_log2 = ips_for(avg);
+    int32_t max_len = 0;
+    for (const Pend& p : cur) max_len = std::max(max_len, p.len);
+    pass.ips_log2 = ips_for(avg, max_len);
     pass.src = src;
     pass.tmp_out = tmp_out;
     const int32_t cap = (int32_t)((1 << pass.ips_log2) * SEG_FOLD);

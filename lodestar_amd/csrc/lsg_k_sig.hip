@@ -38,20 +38,31 @@ __global__ void LSG_KERNEL_ATTR k_sig_subgroup(int n, const uint32_t* __restrict
 
 // The point set i adds to its group's signature sum S_g = sum r_i sig_i: the identity for a
 // set that cannot contribute (undecodable or infinite signature, infinite aggregated key: the
-// verdict rules exclude such sets, lsg_host.hip), else sig_i (bucket MSM groups scale later)
-// or [r_i] sig_i (4-bit windows, groups below the MSM threshold).
-__global__ void LSG_KERNEL_ATTR k_sig_prep(int n, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
+// verdict rules exclude such sets, lsg_host.hip), else sig_i (k_sig_proj: bucket MSM groups
+// scale later) or [r_i] sig_i (k_sig_scale, 4-bit windows: groups below the MSM threshold,
+// sets whose mode byte is set).  Two kernels, so that the MSM path never carries the scaled
+// path's window table (3 KB of scratch per lane).
+LSG_DEVI bool sig_usable(size_t i, const uint8_t* inf, const int32_t* err, const uint8_t* pinf) {
+  return err[i] == 0 && !inf[i] && !(pinf && pinf[i]);
+}
+__global__ void LSG_KERNEL_ATTR k_sig_proj(int n, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
                                            const int32_t* __restrict__ err, const uint8_t* __restrict__ pinf,
-                                           const uint64_t* __restrict__ rnd, const uint8_t* __restrict__ mode,
                                            uint32_t* __restrict__ out) {
   LANE_ITEM(n);
   (void)lead;
   g2p_t r = proj_inf<fp2_t>();
-  const bool use = err[item] == 0 && !inf[item] && !(pinf && pinf[item]);
-  if (use) {
-    r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
-    if (rnd && (!mode || mode[item])) r = proj_mul_u64(r, rnd[item]);
-  }
+  if (sig_usable(item, inf, err, pinf)) r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
+  lane_store(out, item, r);
+}
+__global__ void LSG_KERNEL_ATTR k_sig_scale(int n, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
+                                            const int32_t* __restrict__ err, const uint8_t* __restrict__ pinf,
+                                            const uint64_t* __restrict__ rnd, const uint8_t* __restrict__ mode,
+                                            uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  (void)lead;
+  if (mode && !mode[item]) return;  // a set of an MSM group: k_sig_proj wrote its point
+  g2p_t r = proj_inf<fp2_t>();
+  if (sig_usable(item, inf, err, pinf)) r = proj_mul_u64(proj_from_aff(lane_load<g2a_t>(sig_aff, item)), rnd[item]);
   lane_store(out, item, r);
 }
 
@@ -130,7 +141,13 @@ hipError_t sig_subgroup(hipStream_t st, int n, const uint32_t* sig_aff, const ui
 }
 hipError_t sig_prep(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
                     const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out) {
-  LSG_LAUNCH_ITEMS(k_sig_prep, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
+  if (n <= 0) return hipSuccess;
+  if (!rnd || mode) {  // unscaled points for every set (mode: the scaled sets are overwritten next)
+    hipLaunchKernelGGL(k_sig_proj, dim3(lane_blocks((size_t)n)), dim3(LSG_TPB), 0, st, n, sig_aff, inf, err, pinf, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !rnd) return e;
+  }
+  LSG_LAUNCH_ITEMS(k_sig_scale, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
 }
 hipError_t g2a_to_bytes(hipStream_t st, int n, const uint32_t* pts, const uint8_t* inf, uint8_t* out192) {
   LSG_LAUNCH_ITEMS(k_g2a_to_bytes, n, st, n, pts, inf, out192);

@@ -216,19 +216,24 @@ def test_package_group_matches_chunk_mode(ctx, keys, monkeypatch):
         assert out["1"] == out["0"]
 
 
-def test_reserve_then_no_allocations(ctx, keys):
+def test_reserve_then_no_allocations(ctx, keys, capfd, monkeypatch):
     """lsg_reserve sizes every buffer up front: steady-state submissions allocate nothing
-    (no hipMalloc / hipHostMalloc / hipFree in the submit path)."""
+    (no hipMalloc / hipHostMalloc / hipFree in the submit path).  Any
+    allocation is traced (LSG_TRACE_ALLOC) into the failure message."""
     sets = single_sets(ctx, keys, b"resv", 2048)
     from lodestar_amd._native import PreparedJobs
     pj = PreparedJobs([([s], 1) for s in sets])
-    ctx.reserve(4096, n_slots=4)
+    ctx.reserve(4096, n_slots=0)
+    monkeypatch.setenv("LSG_TRACE_ALLOC", "1")
+    capfd.readouterr()
     before = ctx.allocation_count()
-    tickets = [ctx.submit_jobs(pj) for _ in range(4)]
-    for t in tickets:
-        res, stats = ctx.wait_jobs(t)
-        assert res == [(1, 0)] * 2048
-    assert ctx.allocation_count() == before
+    for rep in range(2):
+        tickets = [ctx.submit_jobs(pj) for _ in range(4)]
+        for t in tickets:
+            res, stats = ctx.wait_jobs(t)
+            assert res == [(1, 0)] * 2048
+    trace = [ln for ln in capfd.readouterr().err.splitlines() if "lsg alloc" in ln]
+    assert ctx.allocation_count() == before, trace
 
 
 def test_node_mode_partials(ctx, keys):
