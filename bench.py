@@ -15,9 +15,9 @@ Workloads:
   jobs         config D shape (default, the headline): 32,768 single-pubkey gossip sets per
                package = one mainnet slot of unaggregated attestations per GPU (weak scaling:
                at 8 GPUs the node takes 8 slots' worth per step); one batchable job per set
-  block        config C: 32 blocks per package, each one non-batchable job of 128 aggregate
+  block        config C: 64 blocks per package, each one non-batchable job of 128 aggregate
                sets of 440-460 signers named by index into the device pubkey table
-  sync         config B: 64 sync-committee contributions per package, each one batchable
+  sync         config B: 256 sync-committee contributions per package, each one batchable
                job of one 512-signer aggregate set
   gossip       config A: one job of 128 single sets per package (latency-bound)
   adversarial  config E: the jobs workload with 1% of the sets corrupted over the five kinds
@@ -90,7 +90,7 @@ class Workload:
             errs = ctx.pubkey_table_set(0, pks)
             if any(errs):
                 raise SystemExit("pubkey table load failed")
-            blocks, per_block = 32, 128
+            blocks, per_block = 64, 128
             for p in range(n_packages):
                 jobs, npk = [], 0
                 for b in range(blocks):
@@ -113,7 +113,7 @@ class Workload:
             errs = ctx.pubkey_table_set(0, pks)
             if any(errs):
                 raise SystemExit("pubkey table load failed")
-            contributions, size = 64, 512
+            contributions, size = 256, 512
             for p in range(n_packages):
                 jobs = []
                 for c in range(contributions):
@@ -254,9 +254,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.depth is None:
-        args.depth = {"jobs": 3, "adversarial": 3, "block": 4, "sync": 6, "gossip": 8}[args.workload]
-    if args.packages is None:
-        args.packages = args.depth + 1
+        args.depth = {"jobs": 4, "adversarial": 4, "block": 4, "sync": 6, "gossip": 8}[args.workload]
+    if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
+        args.packages = 2 if args.workload == "block" else args.depth + 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -305,6 +305,8 @@ def main():
     def run(n_pkgs, depth, capture=False, seq0=0):
         """n_pkgs packages, `depth` in flight; returns per-package submit->verdict latencies and
         (capture) per-package HIP-event kernel times"""
+        if dist is None:
+            return run_threaded(n_pkgs, depth, capture)
         lat, times = [], []
         pend = collections.deque()
         done = 0
@@ -339,6 +341,45 @@ def main():
             done += 1
             if done + len(pend) < n_pkgs:
                 submit()
+        return lat, times
+
+    def run_threaded(n_pkgs, depth, capture):
+        """One GPU, no collective: each ticket is waited on its own thread (as the Node host's
+        libuv pool does), so a package in its fallback phases never holds back the submission
+        of the next ones (the C side releases its lock while a fallback phase runs)."""
+        from concurrent.futures import ThreadPoolExecutor
+        lat, times = [], []
+
+        def wait(t, k, t_sub):
+            res, st = ctx.wait_jobs(t, raw=True)
+            return time.perf_counter() - t_sub, k, t, res, st
+
+        with ThreadPoolExecutor(max_workers=depth) as ex:
+            inflight = collections.deque()
+            seq = 0
+
+            def submit():
+                nonlocal seq
+                k = seq % len(prepared)
+                t = ctx.submit_jobs(prepared[k])
+                if t is None:
+                    raise SystemExit("pipeline slots exhausted: lower --depth")
+                inflight.append(ex.submit(wait, t, k, time.perf_counter()))
+                seq += 1
+
+            while seq < min(depth, n_pkgs):
+                submit()
+            while inflight:
+                dt, k, t, res, st = inflight.popleft().result()
+                lat.append(dt)
+                if not verdict_ok(k, res, t[1]):
+                    raise SystemExit(f"rank {rank}: package {k} verdicts differ from the expected ones")
+                stats_acc.update({"batch_retries": st["batch_retries"], "n_final_exps": st["n_final_exps"],
+                                  "submit_us": st["submit_us"], "packages": 1})
+                if capture:
+                    times.append(ctx.last_kernel_times())
+                if seq < n_pkgs:
+                    submit()
         return lat, times
 
     def barrier():
@@ -417,9 +458,9 @@ def main():
                     "single-pubkey gossip sets, one batchable job each, through lsg_submit_jobs/lsg_wait_jobs",
             "adversarial": "adversarial (SURVEY 8d config E): the firehose package with 1% corrupted sets, "
                            "batch failure + chunk/per-job retry, every verdict checked",
-            "block": "block-body (SURVEY 8d config C): 32 blocks per package, each a non-batchable job of 128 "
+            "block": "block-body (SURVEY 8d config C): 64 blocks per package, each a non-batchable job of 128 "
                      "aggregate sets of 440-460 signers named by index into the device pubkey table",
-            "sync": "sync-committee contributions (SURVEY 8d config B): 64 batchable jobs per package, each one "
+            "sync": "sync-committee contributions (SURVEY 8d config B): 256 batchable jobs per package, each one "
                     "512-signer aggregate set (keys by index)",
             "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
         }[args.workload]

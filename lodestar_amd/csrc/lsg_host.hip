@@ -232,6 +232,14 @@ struct PhasePlan {
   SegPlan buckets, bits, sums, prod;
   size_t n_items = 0;   // Miller items of the phase's groups (fall slots 0 .. n_items-1)
   size_t item_off = 0;  // item_first / item_cnt in the plan arena
+  size_t term_base = 0;  // fall slot of group g's ML(-G1, S_g) term: term_base + g
+  // per group, optional set sub-ranges items must not cross (the package group's 16-job
+  // chunks); sub_items = the item range of every sub-range, in order
+  std::vector<std::vector<std::pair<size_t, size_t>>> sub;
+  std::vector<std::pair<int32_t, int32_t>> sub_items;
+  // reuse: the groups' products take their items from an earlier phase (given item ranges)
+  bool reuse_items = false;
+  std::vector<std::pair<int32_t, int32_t>> given;
 };
 
 struct JobRec {
@@ -285,6 +293,8 @@ struct Slot {
   size_t nb_sets = 0;               // sets of the batchable jobs (staged first)
   std::vector<Grp> groups;          // phase-A groups (MSM groups first)
   int big_g = -1;                   // the package group's index in groups
+  int K = 4;                        // Miller pairs per item for this package
+  std::vector<std::pair<int32_t, int32_t>> chunk_items;  // package mode: per chunk, its phase-A items
   bool chunk_mode = false;          // phase A ran one group per 16-job chunk (LSG_PACKAGE_GROUP=0)
   std::vector<int> chunk_group;     // chunk mode: per chunk of batch_order, its phase-A group
   std::vector<int> job_group;       // per job: its phase-A group (non-batchable), else -1
@@ -477,14 +487,16 @@ void slot_destroy(Slot* s) {
 }
 
 // ---- sizes
-int miller_k() {
-  static int k = [] {
-    const char* e = getenv("LSG_MILLER_K");
-    // K=4 since the tower is inlined: 2.45M vs 2.35M sets/s at 12x3 (profiles/r01_inline_ab.txt)
-    int v = e ? atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 4) ? v : 4;
-  }();
-  return k;
+// Miller pairs per item (one shared f and its squarings): K = 4 does the least work per set,
+// but one item is one lane pair, so a small package has few items and its accumulation wave
+// runs alone for ~14 ms; smaller K trades work for latency there.  Env LSG_MILLER_K forces K.
+int miller_k_for(size_t n_sets) {
+  const char* e = getenv("LSG_MILLER_K");
+  if (e) {
+    const int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4) return v;
+  }
+  return n_sets >= 8192 ? 4 : (n_sets >= 1024 ? 2 : 1);
 }
 
 // Minimum RLC group size for the bucket MSM (env LSG_MSM_MIN_GROUP): below ~150 sets the
@@ -535,7 +547,9 @@ int size_inputs(Slot* s, size_t n, size_t np, size_t mb) {
 
 // per-set state and group buffers for n sets / np keys / ng groups (n_msm of them bucket-MSM
 // groups) in any phase
-int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, bool pkg = false) {
+// pkg: 0 utility calls; 1 phase A of a package (every per-set buffer); 2 a fallback phase
+// (only its own buffers: the per-set state of phase A stays resident and is never moved)
+int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, int pkg = 0) {
   const size_t nn = std::max(n, (size_t)1), pp = std::max(np, (size_t)1), gg = std::max(ng, (size_t)1);
   const size_t g_msm = std::max(n_msm, (size_t)1);
   struct {
@@ -578,9 +592,11 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, bool pkg =
              {&s->d_nodeF, 4 * W_F12 * (LSG_MAX_DEVICES + 1)},
              {&s->d_nodeV, 64}};
   for (auto& x : dev) LSG_RC(ensure(s, *x.b, x.bytes));
-  if (pkg) {  // package slots: Miller lines and items, fallback signature sums
+  if (pkg == 1) {  // Miller lines and items; fall also holds phase B's chunk terms
     LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
-    LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg)));
+    LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg + nn / 16 + 1)));
+  }
+  if (pkg) {  // fallback signature sums and Miller items
     LSG_RC(ensure(s, s->d_fall2, 4 * W_F12 * (nn + gg)));
     LSG_RC(ensure(s, s->d_rs2, 4 * W_G2P * nn));
   }
@@ -786,7 +802,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
 // the arena.  Returns the number of items; set_item (optional) maps set -> item.
 size_t plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges, size_t* off,
                   std::vector<int32_t>* set_item, std::vector<std::pair<int32_t, int32_t>>* range_items) {
-  const size_t K = (size_t)miller_k();
+  const size_t K = (size_t)s->K;
   std::vector<int32_t> first, cnt;
   for (auto& r : ranges) {
     const int32_t i0 = (int32_t)first.size();
@@ -863,12 +879,30 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
     }
     Ph.sums = plan_seg(A, 1, off, len, false, 0, (int32_t)Ph.n_msm);
   }
-  // Miller items of this phase: <= K consecutive sets, never crossing a group
+  // Miller items of this phase: <= K consecutive sets, never crossing a group (nor one of its
+  // sub-ranges), unless the groups reuse an earlier phase's items
   std::vector<std::pair<int32_t, int32_t>> gi;
-  {
+  if (Ph.reuse_items) {
+    gi = Ph.given;
+  } else {
     std::vector<std::pair<size_t, size_t>> ranges;
-    for (auto& g : Ph.groups) ranges.push_back({g.first, g.first + g.len});
-    Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &gi);
+    std::vector<size_t> nsub(ng, 1);
+    for (size_t g = 0; g < ng; g++) {
+      if (g < Ph.sub.size() && !Ph.sub[g].empty()) {
+        ranges.insert(ranges.end(), Ph.sub[g].begin(), Ph.sub[g].end());
+        nsub[g] = Ph.sub[g].size();
+      } else {
+        ranges.push_back({Ph.groups[g].first, Ph.groups[g].first + Ph.groups[g].len});
+      }
+    }
+    Ph.sub_items.clear();
+    Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &Ph.sub_items);
+    Ph.term_base = Ph.n_items;
+    size_t r = 0;
+    for (size_t g = 0; g < ng; g++) {
+      gi.push_back({Ph.sub_items[r].first, Ph.sub_items[r + nsub[g] - 1].second});
+      r += nsub[g];
+    }
   }
   // F_g = f_g * prod of the group's items; element ids index fall
   const size_t pidx = A.size();
@@ -876,7 +910,7 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
   for (size_t g = 0; g < ng; g++) {
     poff.push_back((int32_t)(A.size() - pidx));
     for (int32_t it = gi[g].first; it < gi[g].second; it++) A.push_back(it);
-    A.push_back((int32_t)(Ph.n_items + g));
+    A.push_back((int32_t)(Ph.term_base + g));
     plen.push_back((int32_t)(A.size() - pidx) - poff.back());
   }
   Ph.prod = plan_seg(A, 2, poff, plen, true, pidx, 0);
@@ -888,7 +922,7 @@ int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall) {
   const int ni = (int)n_items;
   const int32_t* items = PL(s, item_off);
   KL(s, "k_miller_accum",
-     lsgk::miller_accum(S_(s), miller_k(), ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
+     lsgk::miller_accum(S_(s), s->K, ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
                         P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), (int)s->n_sets, P_<uint32_t>(s->d_lines),
                         fall));
   return LSG_OK;
@@ -898,8 +932,7 @@ int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall) {
 int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fall, bool export_blobs) {
   const size_t ng = Ph.groups.size();
   if (ng == 0) return LSG_OK;
-  LSG_RC(size_state(s, s->n_sets, s->n_pks, ng, Ph.n_msm, true));
-  const size_t n = Ph.n_items;
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, ng, Ph.n_msm, 2));
   s->cur = 1;
   if (Ph.n_msm) {
     LSG_RC(run_seg(s, 1, "msm_buckets", Ph.buckets, rs, P_<uint32_t>(s->d_bkt)));
@@ -917,7 +950,7 @@ int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fal
     KL(s, "k_row_miller_neg_g1",
        lsg_row_miller_neg_g1(S_(s), nsm, sb, P_<uint8_t>(s->d_fgb) + 576 * Ph.n_msm));
   }
-  KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S_(s), (int)ng, P_<uint8_t>(s->d_fgb), fall + W_F12 * n));
+  KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S_(s), (int)ng, P_<uint8_t>(s->d_fgb), fall + W_F12 * Ph.term_base));
   LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[1]));
   s->cur = 0;
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_grp, 0));
@@ -1103,6 +1136,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     }
   s->nb_sets = 0;
   for (size_t k : s->batch_order) s->nb_sets += s->jobs[k].count;
+  s->K = miller_k_for(flat.size());
   LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true));
   // phase-A groups, MSM groups first: the package group, then one per non-batchable job
   PhasePlan& A = s->phA;
@@ -1140,6 +1174,25 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   A.groups = gm;
   A.groups.insert(A.groups.end(), gs.begin(), gs.end());
   om.insert(om.end(), os.begin(), os.end());
+  // the package group's items never cross a 16-job chunk: if the group fails, each chunk's
+  // check (phase B) reuses them instead of re-running the Miller accumulation
+  std::vector<size_t> chunk_sub;  // chunks with sets, in order
+  if (!s->chunk_mode && s->nb_sets) {
+    chunks = chunkify(s->batch_order.size(), 16);
+    A.sub.assign(om.size(), {});
+    for (size_t g = 0; g < om.size(); g++) {
+      if (om[g] != -2) continue;
+      for (size_t c = 0; c < chunks.size(); c++) {
+        const size_t first = s->jobs[s->batch_order[chunks[c].first]].first;
+        size_t len = 0;
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
+        if (len) {
+          A.sub[g].push_back({first, first + len});
+          chunk_sub.push_back(c);
+        }
+      }
+    }
+  }
   for (size_t g = 0; g < om.size(); g++) {
     if (om[g] == -2)
       s->big_g = (int)g;
@@ -1148,9 +1201,19 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     else
       s->job_group[(size_t)om[g]] = (int)g;
   }
-  LSG_RC(size_state(s, s->n_sets, s->n_pks, A.groups.size(), gm.size(), true));
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, A.groups.size(), gm.size(), 1));
   if (!s->single_keys) s->pkagg = plan_pk_agg(s);
   LSG_RC(plan_phase(s, A));
+  s->chunk_items.assign(chunks.size(), {-1, -1});
+  if (!chunk_sub.empty()) {  // sub_items of the package group, in chunk order
+    size_t r = 0;
+    for (size_t g = 0; g < om.size(); g++) {
+      const size_t ns = g < A.sub.size() && !A.sub[g].empty() ? A.sub[g].size() : 1;
+      if (om[g] == -2)
+        for (size_t k = 0; k < ns; k++) s->chunk_items[chunk_sub[k]] = A.sub_items[r + k];
+      r += ns;
+    }
+  }
   SegPlan node;
   if (n_node > 0) {
     std::vector<int32_t> off{0}, len{(int32_t)n_node};
@@ -1209,7 +1272,16 @@ int pkg_part2(Slot* s) {
 
 // One fallback phase (worker.ts:74-96) over `groups` (scaled signature sums, own Miller items
 // into fall2), synchronous; verdicts into v.
-int run_fallback_phase(Slot* s, const std::vector<Grp>& groups, std::vector<int32_t>& v) {
+// The context mutex is released while a fallback phase runs on the device (the ticket's slots
+// stay claimed, so no other caller touches them): other threads keep submitting and resolving.
+typedef std::unique_lock<std::mutex> CtxLock;
+
+// One fallback phase (worker.ts:74-96) over `groups` (scaled signature sums), synchronous;
+// verdicts into v.  given: per group, its items among phase A's resident Miller items (the
+// package group's chunk-aligned items: no new Miller accumulation); else the phase plans and
+// accumulates its own items (into fall2).
+int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
+                       const std::vector<std::pair<int32_t, int32_t>>* given, std::vector<int32_t>& v) {
   v.assign(groups.size(), 0);
   if (groups.empty()) return LSG_OK;
   timer_reset(s);
@@ -1217,6 +1289,12 @@ int run_fallback_phase(Slot* s, const std::vector<Grp>& groups, std::vector<int3
   PhasePlan Ph;
   Ph.groups = groups;
   for (auto& g : Ph.groups) g.msm = false;
+  if (given) {
+    Ph.reuse_items = true;
+    Ph.given = *given;
+    Ph.n_items = s->phA.n_items;
+    Ph.term_base = s->phA.n_items + s->phA.groups.size();  // after phase A's own terms
+  }
   LSG_RC(plan_phase(s, Ph));
   LSG_RC(upload_plan(s));
   std::vector<uint8_t> mode(s->n_sets, 0);
@@ -1226,11 +1304,19 @@ int run_fallback_phase(Slot* s, const std::vector<Grp>& groups, std::vector<int3
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
   LSG_RC(launch_sig_prep(s, true, &mode, P_<uint32_t>(s->d_rs2)));
   s->cur = 0;
-  LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, P_<uint32_t>(s->d_fall2)));
-  LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), P_<uint32_t>(s->d_fall2), false));
+  uint32_t* fall = given ? P_<uint32_t>(s->d_fall) : P_<uint32_t>(s->d_fall2);
+  if (!given) LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, fall));
+  LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), fall, false));
   LSG_RC(launch_fe(s, groups.size()));
   LSG_RC(launch_readback(s, false));
-  LSG_HIP(s, hipEventSynchronize(s->ev_done));
+  const int dev = s->d->device;
+  if (lk) lk->unlock();
+  hipError_t e = hipEventSynchronize(s->ev_done);
+  if (lk) {
+    lk->lock();
+    (void)hipSetDevice(dev);
+  }
+  if (e != hipSuccess) return fail(s, "hipEventSynchronize", e);
   s->stats.n_final_exps += (uint32_t)groups.size();
   memcpy(v.data(), s->h_verdict.p, 4 * groups.size());
   return LSG_OK;
@@ -1239,7 +1325,7 @@ int run_fallback_phase(Slot* s, const std::vector<Grp>& groups, std::vector<int3
 // The reference's verdict rules for this device's share of the package (worker.ts:30-106),
 // after ev_done.  node_valid: 1 = the node-wide check of all devices' partials passed, 0 = it
 // failed (this device's own package check localises), -1 = no node check (single device).
-int pkg_resolve(Slot* s, int node_valid) {
+int pkg_resolve(Slot* s, CtxLock* lk, int node_valid) {
   const SetStatus ss = read_status(s);
   const PhasePlan& A = s->phA;
   std::vector<int32_t> vA(H_<int32_t>(s->h_verdict), H_<int32_t>(s->h_verdict) + A.groups.size());
@@ -1267,6 +1353,7 @@ int pkg_resolve(Slot* s, int node_valid) {
   std::vector<size_t> retry;  // jobs verified individually (phase C)
   std::vector<Grp> chk;       // chunks checked on their own (phase B)
   std::vector<std::pair<size_t, size_t>> chk_jobs;
+  std::vector<std::pair<int32_t, int32_t>> chk_items;  // their resident phase-A items
   bool any_err_chunk = false;
   std::vector<uint8_t> chunk_err(chunks.size(), 0);
   for (size_t c = 0; c < chunks.size(); c++) {
@@ -1312,6 +1399,7 @@ int pkg_resolve(Slot* s, int node_valid) {
         g.len = len;
         chk.push_back(g);
         chk_jobs.push_back(chunks[c]);
+        chk_items.push_back(c < s->chunk_items.size() ? s->chunk_items[c] : std::make_pair(-1, -1));
       }
     } else {  // the chunk throws (worker.ts:79-85): every job is verified on its own
       s->stats.batch_retries++;
@@ -1329,7 +1417,9 @@ int pkg_resolve(Slot* s, int node_valid) {
   }
   std::vector<int32_t> v;
   if (!chk.empty()) {  // phase B
-    LSG_RC(run_fallback_phase(s, chk, v));
+    bool reuse = true;
+    for (auto& r : chk_items) reuse = reuse && r.first >= 0;
+    LSG_RC(run_fallback_phase(s, lk, chk, reuse ? &chk_items : nullptr, v));
     for (size_t c = 0; c < chk.size(); c++) {
       if (v[c]) {
         for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
@@ -1355,7 +1445,7 @@ int pkg_resolve(Slot* s, int node_valid) {
       g3.push_back(g);
       g3job.push_back(j);
     }
-    LSG_RC(run_fallback_phase(s, g3, v));
+    LSG_RC(run_fallback_phase(s, lk, g3, nullptr, v));
     for (size_t g = 0; g < g3.size(); g++) s->results[g3job[g]] = {v[g] ? LSG_VALID : LSG_INVALID, 0};
   }
   return LSG_OK;
@@ -1492,7 +1582,7 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
 }
 
 // resolve a package: node_valid as pkg_resolve (-2: the ticket's own node check)
-int wait_pkg(lsg_ctx* c, int p, int node_valid, lsg_job_result* results, lsg_stats* stats) {
+int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* results, lsg_stats* stats) {
   const int n = c->n_dev;
   int rc = LSG_OK;
   for (int d = 0; d < n && !rc; d++) {
@@ -1509,7 +1599,7 @@ int wait_pkg(lsg_ctx* c, int p, int node_valid, lsg_job_result* results, lsg_sta
   for (int d = 0; d < n && !rc; d++) {
     Slot* s = &c->dev[d]->slots[p];
     (void)hipSetDevice(c->dev[d]->device);
-    rc = pkg_resolve(s, node_valid);
+    rc = pkg_resolve(s, lk, node_valid);
     if (rc) break;
     for (size_t k = 0; k < s->jobs.size(); k++) results[s->job_ids[k]] = s->results[k];
     total.batch_retries += s->stats.batch_retries;
@@ -1790,7 +1880,7 @@ int lsg_reserve(lsg_ctx* c, size_t max_sets, size_t max_pks, size_t max_msg_byte
       if (s->kind != SLOT_FREE) continue;
       LSG_RC(size_inputs(s, max_sets, max_pks, max_msg_bytes));
       // groups: as many as sets (the per-job phase of a failing package of single-set jobs)
-      LSG_RC(size_state(s, max_sets, max_pks, max_sets, max_sets / 256 + 1, true));
+      LSG_RC(size_state(s, max_sets, max_pks, max_sets, max_sets / 256 + 1, 1));
       LSG_RC(ensure_host(s, s->h_mode, std::max(max_sets, (size_t)1)));
       const size_t plan_words = 16 * max_sets + 4 * max_pks + 64 * 1024;
       LSG_RC(ensure_host(s, s->h_plan, 4 * plan_words));
@@ -1831,7 +1921,8 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
 int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results, lsg_stats* stats) {
   if (!c) return LSG_ERR_INVALID_ARG;
   if (int prc = presync_pkg(c, ticket, false)) return prc;
-  LSG_ENTER(c);
+  CtxLock lk(c->mu);
+  LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
   const int p = ticket_pkg(c, ticket);
   if (p < 0) return LSG_ERR_INVALID_ARG;
   const size_t nj = c->dev[0]->slots[p].n_jobs;
@@ -1840,7 +1931,7 @@ int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_jo
     c->err = "lsg_wait_jobs_node: a multi-device context runs its own node check";
     return LSG_ERR_INVALID_ARG;
   }
-  return wait_pkg(c, p, node_valid == -1 ? -2 : (node_valid ? 1 : 0), results, stats);
+  return wait_pkg(c, &lk, p, node_valid == -1 ? -2 : (node_valid ? 1 : 0), results, stats);
 }
 
 int lsg_wait_jobs(lsg_ctx* c, lsg_ticket ticket, lsg_job_result* results, lsg_stats* stats) {

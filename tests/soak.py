@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Verdict soak on the GPU (north_star: "zero verdict mismatches over 10^7 valid plus
+adversarially corrupted sets").  Test infrastructure (tests/).
+
+Every set is distinct: each package draws fresh messages (a global counter), signs them on the
+GPU with the interop keys sk_{v mod 1024}, corrupts --bad-rate of them (default 1%) split
+evenly over the config E kinds, cuts them into worker jobs of mixed sizes (gossip singles,
+2-16-set batches, 128-set chunks; 90% batchable) and streams the packages through the
+asynchronous jobs path (lsg_submit_jobs / lsg_wait_jobs: one RLC group per package, then the
+chunk and per-job fallback of worker.ts:30-106), with fresh OS-CSPRNG randomizers.
+Expected verdicts never come from the GPU:
+  - valid sets: true by construction (and a sample per package is checked by the C oracle);
+  - wrong message / infinity signature: false; truncated: BLST_INVALID_SIZE; non-subgroup
+    point (the committed decode fixtures, tests/golden/sig_decode.json): BLST_POINT_NOT_IN_GROUP;
+  - flipped x bit: the C oracle's decode outcome (tests/cpu_oracle.py);
+  - a job: maybeBatch.ts:16-39 -- the first set whose signature does not decode rejects the job
+    with its code, else false if any set is false, else true.
+Prints a progress line every ~10 s and a final JSON summary line.
+"""
+import argparse
+import hashlib
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
+sys.path.insert(0, ROOT)
+
+from lodestar_amd import _native as N  # noqa: E402
+from tests import cpu_oracle as co  # noqa: E402
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def interop_sk(i):
+    return int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R_ORDER
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sets", type=int, default=10_000_000)
+    ap.add_argument("--bad-rate", type=float, default=0.01)
+    ap.add_argument("--package", type=int, default=32768, help="sets per package (lsg_submit_jobs call)")
+    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+    rng = random.Random(args.seed)
+    import numpy as np
+
+    ctx = N.Context(0)
+    ctx.reserve(args.package + 256, n_slots=args.depth + 1)
+    sks = [interop_sk(i) for i in range(1024)]
+    pks = ctx.sk_to_pk(sks)
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sig_decode.json")))
+    non_subgroup = [bytes.fromhex(c["sig"]) for c in gold["cases"] if c["err"] == 3 and len(c["sig"]) == 192]
+    counter = 0
+
+    def make_package():
+        nonlocal counter
+        n = args.package
+        base = counter
+        counter += n
+        msgs = [hashlib.sha256(b"lodestar-mi355x" + b"soak" + (base + i).to_bytes(8, "little")).digest()
+                for i in range(n)]
+        keys = [(base + i) % 1024 for i in range(n)]
+        sigs = ctx.sign([sks[k] for k in keys], msgs)
+        sets = [([pks[keys[i]]], msgs[i], sigs[i]) for i in range(n)]
+        exp = [(N.LSG_VALID, 0)] * n
+        bad = sorted(rng.sample(range(n), int(n * args.bad_rate)))
+        flips = []
+        for q, i in enumerate(bad):
+            pk, m, sg = sets[i]
+            kind = q % 5
+            if kind == 0:
+                sets[i], exp[i] = (pk, hashlib.sha256(m).digest(), sg), (N.LSG_INVALID, 0)
+            elif kind == 1:
+                b = bytearray(sg)
+                b[40 + rng.randrange(8)] ^= 1 << rng.randrange(8)
+                sets[i] = (pk, m, bytes(b))
+                flips.append(i)
+            elif kind == 2:
+                sets[i], exp[i] = (pk, m, sg[:32]), (N.LSG_ERROR, 10)
+            elif kind == 3:
+                sets[i], exp[i] = (pk, m, rng.choice(non_subgroup)), (N.LSG_ERROR, 3)
+            else:
+                sets[i], exp[i] = (pk, m, bytes([0xC0]) + bytes(95)), (N.LSG_INVALID, 0)
+        check = flips + rng.sample(range(n), 16)  # the flipped sets + a sample of the valid ones
+        per = co.verify_each([sets[i][0][0] for i in check], [sets[i][1] for i in check], [sets[i][2] for i in check])
+        for i, v in zip(check, per):
+            e = (N.LSG_ERROR, -v) if v < 0 else ((N.LSG_VALID if v else N.LSG_INVALID), 0)
+            if i in flips:
+                exp[i] = e
+            elif e != exp[i]:
+                raise SystemExit(f"oracle disagrees with the construction of set {base + i}: {e} vs {exp[i]}")
+        jobs, jexp, pos = [], [], 0
+        while pos < n:
+            u = rng.random()
+            size = min(n - pos, 1 if u < 0.5 else (rng.randrange(2, 17) if u < 0.75 else 128))
+            idx = list(range(pos, pos + size))
+            pos += size
+            jobs.append(([sets[i] for i in idx], N.LSG_JOB_BATCHABLE if rng.random() < 0.9 else 0))
+            v = (N.LSG_VALID, 0)
+            err = next((exp[i] for i in idx if exp[i][0] == N.LSG_ERROR), None)
+            if err:
+                v = err
+            elif any(exp[i][0] == N.LSG_INVALID for i in idx):
+                v = (N.LSG_INVALID, 0)
+            jexp.append(v)
+        return N.PreparedJobs(jobs), np.array(jexp, dtype=np.int32), n
+
+    done_sets = done_jobs = mismatches = retries = n_false = n_err = 0
+    pend = []
+    t_start = t_last = time.time()
+
+    def drain_one():
+        nonlocal done_sets, done_jobs, mismatches, retries, n_false, n_err
+        t, exp, n, _pj = pend.pop(0)
+        res, st = ctx.wait_jobs(t, raw=True)
+        got = np.frombuffer(res, dtype=np.int32, count=2 * len(exp)).reshape(-1, 2).copy()
+        got[got[:, 0] != N.LSG_ERROR, 1] = 0
+        bad = np.nonzero((got != exp).any(axis=1))[0]
+        for k in bad[:max(0, 10 - mismatches)]:
+            print(f"MISMATCH job {done_jobs + int(k)}: got {tuple(got[k])} expected {tuple(exp[k])}", flush=True)
+        mismatches += len(bad)
+        n_false += int((got[:, 0] == N.LSG_INVALID).sum())
+        n_err += int((got[:, 0] == N.LSG_ERROR).sum())
+        retries += st["batch_retries"]
+        done_sets += n
+        done_jobs += len(exp)
+
+    submitted = 0
+    while submitted < args.sets or pend:
+        if submitted < args.sets and len(pend) < args.depth:
+            pj, exp, n = make_package()
+            t = ctx.submit_jobs(pj)
+            if t is None:
+                drain_one()
+                t = ctx.submit_jobs(pj)
+            pend.append((t, exp, n, pj))
+            submitted += n
+            continue
+        drain_one()
+        if time.time() - t_last > 10:
+            t_last = time.time()
+            el = t_last - t_start
+            print(f"{done_sets} sets / {done_jobs} jobs verified, {mismatches} mismatches, {n_false} false, "
+                  f"{n_err} rejected, {retries} batch retries ({el:.0f} s, generation included)", flush=True)
+    el = time.time() - t_start
+    print(json.dumps({"sets": done_sets, "distinct_sets": done_sets, "jobs": done_jobs, "mismatches": mismatches,
+                      "jobs_false": n_false, "jobs_rejected": n_err, "batch_retries": retries,
+                      "bad_rate": args.bad_rate, "seconds_incl_generation": round(el, 1),
+                      "path": "lsg_submit_jobs/lsg_wait_jobs (one RLC group per package + worker.ts fallback)",
+                      "package_sets": args.package, "depth": args.depth}), flush=True)
+    ctx.close()
+    return 1 if mismatches else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
