@@ -252,6 +252,8 @@ def main():
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
+                    help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     args = ap.parse_args()
     if args.depth is None:
         args.depth = {"jobs": 4, "adversarial": 4, "block": 4, "sync": 6, "gossip": 8}[args.workload]
@@ -301,11 +303,12 @@ def main():
         return ft
 
     stats_acc = collections.Counter()
+    submit_wall = []  # wall time of each lsg_submit_jobs call (lock wait + staging + enqueue)
 
     def run(n_pkgs, depth, capture=False, seq0=0):
         """n_pkgs packages, `depth` in flight; returns per-package submit->verdict latencies and
         (capture) per-package HIP-event kernel times"""
-        if dist is None:
+        if dist is None and args.waits == "thread":
             return run_threaded(n_pkgs, depth, capture)
         lat, times = [], []
         pend = collections.deque()
@@ -315,7 +318,9 @@ def main():
         def submit():
             nonlocal seq
             k = seq % len(prepared)
+            t0 = time.perf_counter()
             t = ctx.submit_jobs(prepared[k])
+            submit_wall.append(time.perf_counter() - t0)
             if t is None:
                 raise SystemExit("pipeline slots exhausted: lower --depth")
             pend.append((t, k, time.perf_counter()))
@@ -361,7 +366,9 @@ def main():
             def submit():
                 nonlocal seq
                 k = seq % len(prepared)
+                t0 = time.perf_counter()
                 t = ctx.submit_jobs(prepared[k])
+                submit_wall.append(time.perf_counter() - t0)
                 if t is None:
                     raise SystemExit("pipeline slots exhausted: lower --depth")
                 inflight.append(ex.submit(wait, t, k, time.perf_counter()))
@@ -391,7 +398,9 @@ def main():
     stats_acc.clear()
     barrier()
     t0 = time.perf_counter()
+    submit_wall.clear()
     lat, ktimes = run(args.steps, args.depth, capture=True)
+    submit_wall_timed = sorted(submit_wall)
     barrier()
     elapsed = time.perf_counter() - t0
     allocs = ctx.allocation_count() - allocs0
@@ -478,6 +487,8 @@ def main():
             "allocations_in_timed_region": allocs,
             "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
             "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),
+            "submit_call_ms_p50_max": [round(1e3 * statistics.median(submit_wall_timed), 3),
+                                       round(1e3 * submit_wall_timed[-1], 3)],
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},

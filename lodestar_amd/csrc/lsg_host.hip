@@ -316,7 +316,9 @@ struct Dev {
   // validator pubkey table (lsg_pubkey_table_set): projective lane-form keys + validity bytes
   DevBuf d_pktab, d_pktab_ok;
   size_t pktab_n = 0, pktab_cap = 0;
-  const Slot* last = nullptr;  // slot whose timers lsg_last_kernel_times reports
+  // kernel times of the last package / call completed on this device (lsg_last_kernel_times),
+  // read from the slot's timing events when it completed, before the slot can be reused
+  std::vector<std::pair<const char*, float>> last_times;
 };
 
 }  // namespace
@@ -439,6 +441,23 @@ void timer_end(Slot* s) {
 // device pointer of arena word `off`
 inline const int32_t* PL(Slot* s, size_t off) { return P_<int32_t>(s->d_plan) + off; }
 
+// snapshot a completed slot's kernel times for lsg_last_kernel_times (-1: not measured)
+void keep_times(Slot* s) {
+  auto& v = s->d->last_times;
+  v.clear();
+  for (size_t i = 0; i < s->ntimers; i++) {
+    float t = 0;
+    if (hipEventElapsedTime(&t, s->timers[i].a, s->timers[i].b) != hipSuccess) t = -1;
+    v.push_back({s->timers[i].name, t});
+  }
+}
+
+// LSG_BLOCKING_WAITS=1: waiters sleep on the completion events (hipEventBlockingSync)
+bool blocking_waits() {
+  const char* e = getenv("LSG_BLOCKING_WAITS");
+  return e && atoi(e) != 0;
+}
+
 int slot_create(Dev* d, Slot* s, int index, hipStream_t shared) {
   s->d = d;
   s->index = index;
@@ -450,6 +469,12 @@ int slot_create(Dev* d, Slot* s, int index, hipStream_t shared) {
   }
   hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_part, &s->ev_done, &s->ev_node};
   for (hipEvent_t* e : evs) LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (blocking_waits()) {  // the events a waiter blocks on: sleep instead of spinning
+    for (hipEvent_t* e : {&s->ev_part, &s->ev_done}) {
+      LSG_HIP(s, hipEventDestroy(*e));
+      LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventBlockingSync));
+    }
+  }
   LSG_RC(ensure(s, s->d_dst, 256));
   LSG_HIP(s, hipMemcpy(s->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice));
   return LSG_OK;
@@ -1613,7 +1638,7 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
     Slot* s = &c->dev[d]->slots[p];
     if (rc) sync_slot(s);
     s->kind = SLOT_FREE;
-    c->dev[d]->last = s;
+    keep_times(s);
   }
   (void)hipSetDevice(c->dev[0]->device);
   return rc;
@@ -1790,7 +1815,7 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
   for (size_t k = 0; k < n; k++) ok[k] = pkerr[k] == 0 ? 1 : 0;
   LSG_HIP(s, hipMemcpy(P_<uint8_t>(d->d_pktab_ok) + first, ok.data(), n, hipMemcpyHostToDevice));
   d->pktab_n = std::max(d->pktab_n, need);
-  d->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2042,7 +2067,7 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
   else
     memcpy(out576, fp12_one_blob(), 576);
   s->kind = SLOT_FREE;
-  c->dev[0]->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2096,7 +2121,7 @@ static int final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid, bool single
   if (!s->n_sets) valid[0] = 0;
   for (size_t g = 0; g < s->n_sets; g++) valid[g] = H_<int32_t>(s->h_verdict)[g];
   s->kind = SLOT_FREE;
-  c->dev[0]->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2138,7 +2163,7 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
   LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipMemcpyAsync(out96, s->d_Fb.p, 96, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  d->last = s;
+  keep_times(s);
   for (size_t k = 0; k < n; k++)
     if (pkerr[k]) {
       *err_code = pkerr[k];
@@ -2183,7 +2208,7 @@ int lsg_pubkey_validate(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_t 
     LSG_HIP(s, hipMemcpyAsync(out96, s->d_ub.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
   }
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  d->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2202,7 +2227,7 @@ int lsg_hash_to_g2(lsg_ctx* c, const uint8_t* msgs, uint32_t msg_len, size_t n, 
      lsgk::g2a_to_bytes(S_(s), nn, P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf), P_<uint8_t>(s->d_aux)));
   LSG_HIP(s, hipMemcpyAsync(out192, s->d_aux.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  d->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2243,7 +2268,7 @@ int lsg_sig_decode(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, size_t n, 
   LSG_HIP(s, hipMemcpyAsync(out192, s->d_aux.p, 192 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipMemcpyAsync(err, s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  c->dev[0]->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2288,7 +2313,7 @@ int lsg_aggregate_signatures(lsg_ctx* c, const uint8_t* sigs, uint32_t sig_len, 
   LSG_HIP(s, hipMemcpyAsync(serr.data(), s->d_seterr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipMemcpyAsync(blob.data(), s->d_aux.p, 96 * n_groups, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  c->dev[0]->last = s;
+  keep_times(s);
   // Signature.aggregate throws on the first signature that fails to deserialize
   for (size_t g = 0; g < n_groups; g++) {
     if (offsets[g + 1] == offsets[g]) continue;
@@ -2324,7 +2349,7 @@ static int signing_roots(lsg_ctx* c, int kind, const uint8_t* objs, size_t n, co
     KL(s, "k_signing_root", lsgk::signing_root(S_(s), nn, d_obj, d_dom, dstride, P_<uint8_t>(s->d_Fb)));
   LSG_HIP(s, hipMemcpyAsync(out32, s->d_Fb.p, 32 * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
-  d->last = s;
+  keep_times(s);
   return LSG_OK;
 }
 
@@ -2429,16 +2454,11 @@ int lsg_probe_mad_peak(lsg_ctx* c, double* mad_per_s) {
 int lsg_last_kernel_times(lsg_ctx* c, const char** names, double* ms, int max) {
   if (!c) return 0;
   std::lock_guard<std::mutex> lk(c->mu);
-  const Slot* s = c->dev[0]->last;
-  if (!s) return 0;
-  for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(s->st[k]);
+  const auto& v = c->dev[0]->last_times;
   int n = 0;
-  for (size_t i = 0; i < s->ntimers && n < max; i++) {
-    float t = 0;
-    if (hipEventElapsedTime(&t, s->timers[i].a, s->timers[i].b) != hipSuccess) t = -1;
-    if (names) names[n] = s->timers[i].name;
-    if (ms) ms[n] = t;
-    n++;
+  for (size_t i = 0; i < v.size() && n < max; i++, n++) {
+    if (names) names[n] = v[i].first;
+    if (ms) ms[n] = v[i].second;
   }
   return n;
 }
