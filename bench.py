@@ -425,11 +425,13 @@ def main():
     mk = os.environ.get("LSG_MILLER_K", "4")
     accum_key = f"miller_accum{mk}_per_set" if f"miller_accum{mk}_per_set" in opc["stage_fp_muls"] \
         else "miller_accum2_per_set"
-    stage_of = {"k_miller_accum": accum_key, "k_miller_lines": "miller_lines", "k_sig_subgroup": "sig_subgroup",
-                "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale", "k_h2c_map": "hash_map"}
+    stage_of = {"k_miller_accum": [accum_key], "k_miller_lines": ["miller_lines"],
+                "k_miller_fused": ["miller_lines", "miller_accum4_per_set"], "k_sig_subgroup": ["sig_subgroup"],
+                "k_sig_decode": ["sig_decode"], "k_pk_scale": ["pk_scale"], "k_h2c_map": ["hash_map"]}
     per_set = {k: v for k, v in agg.items() if k in stage_of and k != "k_h2c_map"}
     dom = max(per_set, key=per_set.get)
-    muls = opc["stage_fp_muls"][stage_of[dom]] * n_sets  # one launch covers the package's sets
+    # one launch covers the package's sets
+    muls = sum(opc["stage_fp_muls"][st] for st in stage_of[dom]) * n_sets
     achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] / max(calls[dom], 1) * 1e-3) / 1e12
     peak = peak_mad / 1e12
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),

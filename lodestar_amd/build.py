@@ -47,11 +47,19 @@ def needs_rebuild():
 CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DLSG_BIGFN=__host__ __device__ __forceinline__"]
 
 
+def _obj_dir(extra):
+    """objects of the default build in _obj/; A/B builds (extra flags) in their own directory"""
+    if not extra:
+        return OBJ
+    import hashlib
+    return OBJ + "_" + hashlib.sha1(" ".join(extra).encode()).hexdigest()[:10]
+
+
 def _compile(src, verbose, extra):
-    obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    obj = os.path.join(_obj_dir(extra), os.path.splitext(src)[0] + ".o")
     srcp = os.path.join(CSRC, src)
     dep_t = max(os.path.getmtime(d) for d in [srcp] + _deps() if os.path.exists(d))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= dep_t and not extra:
+    if os.path.exists(obj) and os.path.getmtime(obj) >= dep_t:
         return obj
     cmd = [hipcc()] + CFLAGS + extra + ["-I", CSRC, "-I", os.path.join(ROOT, "include"), "-c", srcp, "-o", obj + ".tmp"]
     if verbose:
@@ -74,10 +82,11 @@ def build(force=False, verbose=True, extra=None, out=None):
     out = out or OUT
     if not force and not extra and out == OUT and not needs_rebuild():
         return OUT
-    os.makedirs(OBJ, exist_ok=True)
+    odir = _obj_dir(extra)
+    os.makedirs(odir, exist_ok=True)
     if force:
-        for f in os.listdir(OBJ):
-            os.remove(os.path.join(OBJ, f))
+        for f in os.listdir(odir):
+            os.remove(os.path.join(odir, f))
     jobs = int(os.environ.get("LSG_BUILD_JOBS", str(min(8, os.cpu_count() or 4))))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose, extra), SOURCES))

@@ -274,6 +274,53 @@ LSG_INL proj_t<F> proj_mul_u64(const proj_t<F>& p, uint64_t k) {
   return jac_to_proj(acc);
 }
 
+// [k]P for a 64-bit scalar k, signed 3-bit windows: k = sum_{i<22} d_i 8^i with d_i in
+// [-4, 3] (d_21 in [0, 2]), table T[1..4] = [1..4]P held in registers and picked with selects
+// (a per-lane indexed table lives in scratch).  63 Jacobian doublings and 21 complete
+// additions, plus 2 doublings and 1 addition for the table (the 4-bit form: 61 + 29).
+template <class F>
+LSG_INL proj_t<F> proj_pick_signed(const proj_t<F>& T1, const proj_t<F>& T2, const proj_t<F>& T3,
+                                   const proj_t<F>& T4, int d) {
+  const int a = d < 0 ? -d : d;
+  proj_t<F> r = proj_inf<F>();
+  auto take = [&](bool s, const proj_t<F>& t) {
+    r.X = fselect(s, t.X, r.X);
+    r.Y = fselect(s, t.Y, r.Y);
+    r.Z = fselect(s, t.Z, r.Z);
+  };
+  take(a == 1, T1);
+  take(a == 2, T2);
+  take(a == 3, T3);
+  take(a == 4, T4);
+  r.Y = fselect(d < 0, fneg(r.Y), r.Y);
+  return r;
+}
+template <class F>
+LSG_INL proj_t<F> proj_mul_u64_s3(const proj_t<F>& p, uint64_t k) {
+  const proj_t<F> T2 = gdbl(p);
+  const proj_t<F> T3 = gadd(T2, p);
+  const proj_t<F> T4 = gdbl(T2);
+  // carry into window i (bit i): windows of value >= 4 borrow 8 from the next one
+  uint32_t cm = 0;
+#pragma unroll
+  for (int i = 0; i < 21; i++) {
+    const uint32_t v = (uint32_t)((k >> (3 * i)) & 7u) + ((cm >> i) & 1u);
+    cm |= (v >= 4u ? 1u : 0u) << (i + 1);
+  }
+  auto digit = [&](int i) {
+    return (int)((k >> (3 * i)) & 7u) + (int)((cm >> i) & 1u) - (i < 21 ? 8 * (int)((cm >> (i + 1)) & 1u) : 0);
+  };
+  jac_t<F> acc = jac_from_proj(proj_pick_signed(p, T2, T3, T4, digit(21)));
+#pragma unroll 1
+  for (int i = 20; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    acc = jac_dbl(acc);
+    acc = jac_dbl(acc);
+    acc = jac_add_proj(acc, proj_pick_signed(p, T2, T3, T4, digit(i)));
+  }
+  return jac_to_proj(acc);
+}
+
 // [|x|]P for the BLS parameter |x| = 0xd201000000010000 (public, uniform branch):
 // 63 Jacobian doublings, 5 complete additions
 template <class F>

@@ -221,15 +221,16 @@ LSG_BIGFN g2p_t iso_map3(g2a_t p) {
   return r;
 }
 
-// h_eff * P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)   (RFC 9380 appendix G.3)
+// h_eff * P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)   (RFC 9380 appendix G.3), as
+// c + [x]([x]P + psi(P)) with c = psi^2(2P) - psi(P) - P - [x]P: the terms are folded into c
+// as soon as they exist, so each [x] chain runs with one other point live (registers, not
+// scratch).
 LSG_BIGFN g2p_t clear_cofactor_g2(g2p_t p) {
-  g2p_t t1 = proj_neg(proj_mul_xabs(p));  // [x]P
-  g2p_t t2 = g2_psi(p);
-  g2p_t t3 = g2_psi2(g2_dbl(p));
-  t3 = g2_add(t3, proj_neg(t2));
-  t2 = g2_add(t1, t2);
-  t2 = proj_neg(proj_mul_xabs(t2));
-  t3 = g2_add(t3, t2);
-  t3 = g2_add(t3, proj_neg(t1));
-  return g2_add(t3, proj_neg(p));
+  const g2p_t u = g2_psi(p);
+  g2p_t c = g2_add(g2_psi2(g2_dbl(p)), proj_neg(u));
+  c = g2_add(c, proj_neg(p));
+  const g2p_t t1 = proj_neg(proj_mul_xabs(p));  // [x]P
+  c = g2_add(c, proj_neg(t1));
+  const g2p_t t2 = proj_neg(proj_mul_xabs(g2_add(t1, u)));  // [x]([x]P + psi(P))
+  return g2_add(c, t2);
 }

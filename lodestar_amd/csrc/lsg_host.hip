@@ -515,7 +515,15 @@ void slot_destroy(Slot* s) {
 // Miller pairs per item (one shared f and its squarings): K = 4 does the least work per set,
 // but one item is one lane pair, so a small package has few items and its accumulation wave
 // runs alone for ~14 ms; smaller K trades work for latency there.  Env LSG_MILLER_K forces K.
+// The fused Miller kernel (k_miller_fused: lines in LDS, four waves per item of four pairs) is
+// the default; LSG_MILLER_FUSED=0 selects the split pair k_miller_lines / k_miller_accum<K>.
+bool miller_fused() {
+  const char* e = getenv("LSG_MILLER_FUSED");
+  return !(e && atoi(e) == 0);
+}
+
 int miller_k_for(size_t n_sets) {
+  if (miller_fused()) return 4;  // an item is four waves' lane pairs, whatever the package size
   const char* e = getenv("LSG_MILLER_K");
   if (e) {
     const int v = atoi(e);
@@ -617,8 +625,8 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, int pkg = 
              {&s->d_nodeF, 4 * W_F12 * (LSG_MAX_DEVICES + 1)},
              {&s->d_nodeV, 64}};
   for (auto& x : dev) LSG_RC(ensure(s, *x.b, x.bytes));
-  if (pkg == 1) {  // Miller lines and items; fall also holds phase B's chunk terms
-    LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
+  if (pkg == 1) {  // Miller lines (split kernels only) and items; fall also holds phase B's chunk terms
+    if (!miller_fused()) LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
     LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg + nn / 16 + 1)));
   }
   if (pkg) {  // fallback signature sums and Miller items
@@ -946,6 +954,12 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
 int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall) {
   const int ni = (int)n_items;
   const int32_t* items = PL(s, item_off);
+  if (miller_fused()) {
+    KL(s, "k_miller_fused", lsgk::miller_fused(S_(s), ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
+                                              P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_H),
+                                              fall));
+    return LSG_OK;
+  }
   KL(s, "k_miller_accum",
      lsgk::miller_accum(S_(s), s->K, ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
                         P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), (int)s->n_sets, P_<uint32_t>(s->d_lines),
@@ -997,7 +1011,7 @@ int launch_fe(Slot* s, size_t ng) {
 
 // Per-set stages of the slot's package (no host synchronisation):
 //   side: pubkeys -> aggregation -> [r_i] scaling -> signature decode -> subgroup check (ev_sig)
-//   main: expand_message -> hash_to_G2 -> lines -> wait ev_sig -> Miller items f (fall)
+//   main: expand_message -> hash_to_G2 [-> lines] -> wait ev_sig -> Miller items f (fall)
 int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item_off, uint32_t* fall) {
   const int n = (int)s->n_sets, np = (int)s->n_pks;
   if (n == 0) return LSG_OK;
@@ -1027,7 +1041,8 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item
                                          P_<uint32_t>(s->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN,
                                          P_<uint8_t>(s->d_ub)));
   LSG_RC(launch_hash(s, n));
-  KL(s, "k_miller_lines", lsgk::miller_lines(S_(s), n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
+  if (!miller_fused())
+    KL(s, "k_miller_lines", lsgk::miller_lines(S_(s), n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
   if (n_items) LSG_RC(launch_accum(s, n_items, item_off, fall));
   return LSG_OK;

@@ -10,6 +10,12 @@
 //   k_h2c_affine   (X, Y) * conj(Z) / N(Z)
 #include "lsg_kcommon.hpp"
 
+// waves per SIMD for the SSWU map and the cofactor clearing: 2 (256 registers, some scratch)
+// or 1 (512 registers, none)
+#ifndef LSG_H2C_WAVES
+#define LSG_H2C_WAVES 2
+#endif
+
 // expand_message_xmd(msg_i, DST, 256): one thread per set (byte-serial SHA-256)
 __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restrict__ msg,
                                                     const uint32_t* __restrict__ msg_off,
@@ -51,7 +57,7 @@ __global__ void LSG_KERNEL_ATTR k_h2c_prep(int n, const uint8_t* __restrict__ ub
 // stage 2: SSWU x2 (with the batched 1/N(tv1)) -> 3-isogeny -> add, projective.  Split from
 // the cofactor clearing so that neither kernel holds the other's live state (the fused kernel
 // spilled 757 registers).
-__global__ void LSG_KERNEL_ATTR k_h2c_map(int n, const uint32_t* __restrict__ U, const uint32_t* __restrict__ ninv,
+__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_map(int n, const uint32_t* __restrict__ U, const uint32_t* __restrict__ ninv,
                                           uint32_t* __restrict__ Hp) {
   LANE_ITEM(n);
   (void)lead;
@@ -62,7 +68,7 @@ __global__ void LSG_KERNEL_ATTR k_h2c_map(int n, const uint32_t* __restrict__ U,
 }
 
 // stage 2b: clear_cofactor in place; zN_i = N(Z) (0 at infinity) for the batched inversion
-__global__ void LSG_KERNEL_ATTR k_h2c_clear(int n, uint32_t* __restrict__ Hp, uint32_t* __restrict__ zN,
+__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, uint32_t* __restrict__ Hp, uint32_t* __restrict__ zN,
                                             uint8_t* __restrict__ hinf) {
   LANE_ITEM(n);
   g2p_t q = clear_cofactor_g2(lane_load<g2p_t>(Hp, item));

@@ -67,7 +67,271 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
              }));
 }
 
+// ---- Fused Miller kernel: lines computed and consumed in LDS (north_star: "line coefficients
+// staged in LDS"), the Fp12 accumulator of each item shared by four waves.
+//
+// A workgroup is 4 waves and owns 32 items of <= 4 sets (MF_ITEMS).  Lane pair q of every
+// wave works on item q; wave w is "pair w" of its item:
+//   L phase   wave w advances its set's G2 point T (doubling or addition step), evaluates the
+//             line at its P and writes it to LDS (the identity line (1, 0, 0) for a set that
+//             does not contribute) -- the four lines of an item come out in parallel;
+//   S phase   f <- f^2: the 12 Fp2 products of (a + b w)^2 = (u - t - v t) + 2t w,
+//             t = a b, u = (a + b)(a + v b), three per wave, then the six output
+//             coefficients combined by the waves in parallel;
+//   M phase   f <- f * line_k for k = 0..3: the 13 Fp2 products of fp12_mul_line split 4/3/3/3
+//             over the waves, then the six output coefficients.
+// f, the lines, the products and the G2 points live in LDS only (154 KB per workgroup), so a set's HBM
+// traffic is its inputs (Q, P, flags) and 1/4 of its item's f: no line round trip.  The
+// operation order differs from miller_accum_multi (every product is issued as an Fp2
+// product of the same Karatsuba form), the field element is the same: the host-checked
+// split loop and the GPU parity tests pin it.
+constexpr int MF_ITEMS = 32;
+// LDS components (one Fp of 32 items each): f, the four lines, the products, the four G2 points T
+constexpr int MF_F = 0, MF_L = 12, MF_V = 36, MF_T = 62, MF_COMPS = 86;
+constexpr size_t MF_LDS_BYTES = (size_t)MF_COMPS * 7 * 64 * 4;  // 154,112 B: one workgroup per CU
+
+LSG_DEVI uint32_t* mf_slot(uint32_t* lds, int c) { return lds + (size_t)c * 7 * 64 + (threadIdx.x & 63); }
+LSG_DEVI void mf_put(uint32_t* lds, int c, const fp_t& v) {
+  uint32_t* p = mf_slot(lds, c);
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) p[k * 64] = v.l[k];
+}
+LSG_DEVI fp_t mf_get(uint32_t* lds, int c) {
+  const uint32_t* p = mf_slot(lds, c);
+  fp_t v;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) v.l[k] = p[k * 64];
+  return v;
+}
+LSG_DEVI void mf_put2(uint32_t* lds, int c, const fp2_t& v) {
+  mf_put(lds, c, v.c0);
+  mf_put(lds, c + 1, v.c1);
+}
+LSG_DEVI fp2_t mf_get2(uint32_t* lds, int c) { return fp2_t(mf_get(lds, c), mf_get(lds, c + 1)); }
+// Fp2 coefficient j (0..5: c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2) of f, product p, line k
+#define MF_FC(j) (MF_F + 2 * (j))
+#define MF_VC(p) (MF_V + 2 * (p))
+#define MF_LC(k, j) (MF_L + 6 * (k) + 2 * (j))
+
+// f <- f^2 (S phase).  V0..5: t = a b (v0, v1, v2, m0, m1, m2 of the Karatsuba Fp6 product),
+// V6..11: u = (a + b)(a + v b).
+LSG_DEVI void mf_sqr(uint32_t* lds, int w) {
+  {
+    fp6_t x, y;
+    const fp6_t a = fp6_make(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(1)), mf_get2(lds, MF_FC(2)));
+    const fp6_t b = fp6_make(mf_get2(lds, MF_FC(3)), mf_get2(lds, MF_FC(4)), mf_get2(lds, MF_FC(5)));
+    if (w < 2) {
+      x = a;
+      y = b;
+    } else {
+      x = fp6_add(a, b);
+      y = fp6_add(a, fp6_mul_v(b));
+    }
+    fp2_t p0, p1, p2;
+    if ((w & 1) == 0) {  // v0, v1, v2
+      p0 = fp2_mul(x.c0, y.c0);
+      p1 = fp2_mul(x.c1, y.c1);
+      p2 = fp2_mul(x.c2, y.c2);
+    } else {  // m0 = (x1 + x2)(y1 + y2), m1 = (x0 + x1)(y0 + y1), m2 = (x0 + x2)(y0 + y2)
+      p0 = fp2_mul(fp2_add(x.c1, x.c2), fp2_add(y.c1, y.c2));
+      p1 = fp2_mul(fp2_add(x.c0, x.c1), fp2_add(y.c0, y.c1));
+      p2 = fp2_mul(fp2_add(x.c0, x.c2), fp2_add(y.c0, y.c2));
+    }
+    mf_put2(lds, MF_VC(3 * w), p0);
+    mf_put2(lds, MF_VC(3 * w + 1), p1);
+    mf_put2(lds, MF_VC(3 * w + 2), p2);
+  }
+  __syncthreads();
+  // Karatsuba Fp6 combination of t (V0..5): c0 = v0 + xi (m0 - v1 - v2), c1 = m1 - v0 - v1 + xi v2,
+  // c2 = m2 - v0 - v2 + v1; likewise u (V6..11).  New f: c0 = u - t - v t, c1 = 2t.
+  auto fin = [&](int base, int j) {
+    const fp2_t v0 = mf_get2(lds, MF_VC(base)), v1 = mf_get2(lds, MF_VC(base + 1)), v2 = mf_get2(lds, MF_VC(base + 2));
+    if (j == 0) return fp2_add(v0, fp2_mul_xi(fp2_sub(fp2_sub(mf_get2(lds, MF_VC(base + 3)), v1), v2)));
+    if (j == 1) return fp2_add(fp2_sub(fp2_sub(mf_get2(lds, MF_VC(base + 4)), v0), v1), fp2_mul_xi(v2));
+    return fp2_add(fp2_sub(fp2_sub(mf_get2(lds, MF_VC(base + 5)), v0), v2), v1);
+  };
+  fp2_t o0, o1, o2;
+  if (w == 0) {  // c1 = 2t
+    o0 = fin(0, 0);
+    o1 = fin(0, 1);
+    o2 = fin(0, 2);
+  } else if (w == 1) {  // c0.c0 = u0 - t0 - xi t2
+    o0 = fp2_sub(fp2_sub(fin(6, 0), fin(0, 0)), fp2_mul_xi(fin(0, 2)));
+  } else if (w == 2) {  // c0.c1 = u1 - t1 - t0
+    o0 = fp2_sub(fp2_sub(fin(6, 1), fin(0, 1)), fin(0, 0));
+  } else {  // c0.c2 = u2 - t2 - t1
+    o0 = fp2_sub(fp2_sub(fin(6, 2), fin(0, 2)), fin(0, 1));
+  }
+  __syncthreads();  // every wave has read the products it needs before f is overwritten
+  if (w == 0) {
+    mf_put2(lds, MF_FC(3), fp2_add(o0, o0));
+    mf_put2(lds, MF_FC(4), fp2_add(o1, o1));
+    mf_put2(lds, MF_FC(5), fp2_add(o2, o2));
+  } else {
+    mf_put2(lds, MF_FC(w - 1), o0);
+  }
+  __syncthreads();
+}
+
+// f <- f * line_k (M phase): fp12_mul_line's 13 Fp2 products (lsg_tower.hpp), with a = f.c0,
+// b = f.c1, s = a + b, m = l01 + l11:
+//   P0 a0 l00  P1 a1 l01  P2 a2 l01  P3 (a0+a1)(l00+l01)  P4 a2 l00          (t0 = a (l00, l01))
+//   P5 s0 l00  P6 s1 m    P7 s2 m    P8 (s0+s1)(l00+m)    P9 s2 l00          (u = s (l00, m))
+//   P10 b2 l11 P11 b0 l11 P12 b1 l11                                         (t1 = b (l11 v))
+// new f: c0 = t0 + v t1, c1 = u - t0 - t1, i.e.
+//   c0.c0 = P0 + xi (P2 + P12)        c1.c0 = P5 - P0 + xi (P7 - P2 - P10)
+//   c0.c1 = P3 - P0 - P1 + xi P10     c1.1  = P8 - P5 - P6 - P3 + P0 + P1 - P11
+//   c0.c2 = P4 + P1 + P11             c1.2  = P9 + P6 - P4 - P1 - P12
+LSG_DEVI void mf_mul_line(uint32_t* lds, int w, int k) {
+  {
+    const fp2_t l00 = mf_get2(lds, MF_LC(k, 0)), l01 = mf_get2(lds, MF_LC(k, 1)), l11 = mf_get2(lds, MF_LC(k, 2));
+    if (w == 0) {
+      const fp2_t a0 = mf_get2(lds, MF_FC(0)), a1 = mf_get2(lds, MF_FC(1)), a2 = mf_get2(lds, MF_FC(2));
+      mf_put2(lds, MF_VC(0), fp2_mul(a0, l00));
+      mf_put2(lds, MF_VC(1), fp2_mul(a1, l01));
+      mf_put2(lds, MF_VC(2), fp2_mul(a2, l01));
+      mf_put2(lds, MF_VC(3), fp2_mul(fp2_add(a0, a1), fp2_add(l00, l01)));
+    } else if (w == 1) {
+      const fp2_t a2 = mf_get2(lds, MF_FC(2));
+      const fp2_t s0 = fp2_add(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(3)));
+      const fp2_t s1 = fp2_add(mf_get2(lds, MF_FC(1)), mf_get2(lds, MF_FC(4)));
+      mf_put2(lds, MF_VC(4), fp2_mul(a2, l00));
+      mf_put2(lds, MF_VC(5), fp2_mul(s0, l00));
+      mf_put2(lds, MF_VC(6), fp2_mul(s1, fp2_add(l01, l11)));
+    } else if (w == 2) {
+      const fp2_t s0 = fp2_add(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(3)));
+      const fp2_t s1 = fp2_add(mf_get2(lds, MF_FC(1)), mf_get2(lds, MF_FC(4)));
+      const fp2_t s2 = fp2_add(mf_get2(lds, MF_FC(2)), mf_get2(lds, MF_FC(5)));
+      const fp2_t m = fp2_add(l01, l11);
+      mf_put2(lds, MF_VC(7), fp2_mul(s2, m));
+      mf_put2(lds, MF_VC(8), fp2_mul(fp2_add(s0, s1), fp2_add(l00, m)));
+      mf_put2(lds, MF_VC(9), fp2_mul(s2, l00));
+    } else {
+      mf_put2(lds, MF_VC(10), fp2_mul(mf_get2(lds, MF_FC(5)), l11));
+      mf_put2(lds, MF_VC(11), fp2_mul(mf_get2(lds, MF_FC(3)), l11));
+      mf_put2(lds, MF_VC(12), fp2_mul(mf_get2(lds, MF_FC(4)), l11));
+    }
+  }
+  __syncthreads();
+  auto V = [&](int p) { return mf_get2(lds, MF_VC(p)); };
+  fp2_t o0, o1;
+  int j0, j1 = -1;
+  if (w == 0) {  // c0.c0, c0.c2
+    o0 = fp2_add(V(0), fp2_mul_xi(fp2_add(V(2), V(12))));
+    o1 = fp2_add(fp2_add(V(4), V(1)), V(11));
+    j0 = 0;
+    j1 = 2;
+  } else if (w == 1) {  // c0.c1
+    o0 = fp2_add(fp2_sub(fp2_sub(V(3), V(0)), V(1)), fp2_mul_xi(V(10)));
+    j0 = 1;
+  } else if (w == 2) {  // c1.c0, c1.c2
+    o0 = fp2_add(fp2_sub(V(5), V(0)), fp2_mul_xi(fp2_sub(fp2_sub(V(7), V(2)), V(10))));
+    o1 = fp2_sub(fp2_sub(fp2_sub(fp2_add(V(9), V(6)), V(4)), V(1)), V(12));
+    j0 = 3;
+    j1 = 5;
+  } else {  // c1.c1
+    o0 = fp2_sub(fp2_add(fp2_add(fp2_sub(fp2_sub(fp2_sub(V(8), V(5)), V(6)), V(3)), V(0)), V(1)), V(11));
+    j0 = 4;
+  }
+  // f's coefficients are not read in this half: write them at once
+  mf_put2(lds, MF_FC(j0), o0);
+  if (j1 >= 0) mf_put2(lds, MF_FC(j1), o1);
+  __syncthreads();
+}
+
+#ifndef LSG_MF_WAVES
+#define LSG_MF_WAVES 2  // waves per SIMD the register budget is sized for (256 VGPR + AGPR)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSG_MF_WAVES)))
+k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_t* __restrict__ item_cnt,
+               const uint32_t* __restrict__ P, const uint8_t* __restrict__ pinf, const uint8_t* __restrict__ hinf,
+               const int32_t* __restrict__ err, const uint32_t* __restrict__ H, uint32_t* __restrict__ f_out) {
+  // dynamic LDS (MF_LDS_BYTES at launch): the compiler then sizes registers for
+  // LSG_MF_WAVES waves per SIMD instead of the one workgroup per CU the LDS allows, so the
+  // other kernels of the pipeline can share the SIMDs while this one waits at its barriers
+  extern __shared__ uint32_t lds[];
+  const int w = (int)(threadIdx.x >> 6);
+  const size_t it = (size_t)blockIdx.x * MF_ITEMS + ((threadIdx.x & 63) >> 1);
+  const bool live = it < (size_t)n_items;  // lanes past the end run item 0's data and store nothing
+  const size_t itc = live ? it : 0;
+  const int first = item_first[itc], cnt = item_cnt[itc];
+  const int si = first + (w < cnt ? w : cnt - 1);
+  const bool use = live && w < cnt && err[si] == 0 && !pinf[si] && !hinf[si];
+  // nothing stays in registers across the loop: T lives in LDS, Q (addition steps) and P are
+  // re-read from global memory (L2 hits)
+  {
+    const g2p_t T = proj_from_aff(lane_load<g2a_t>(H, (size_t)si));
+    mf_put2(lds, MF_T + 6 * w, T.X);
+    mf_put2(lds, MF_T + 6 * w + 2, T.Y);
+    mf_put2(lds, MF_T + 6 * w + 4, T.Z);
+  }
+  auto line_phase = [&](bool add) {
+    g2p_t T;  // this wave's own slots: no other wave touches them
+    T.X = mf_get2(lds, MF_T + 6 * w);
+    T.Y = mf_get2(lds, MF_T + 6 * w + 2);
+    T.Z = mf_get2(lds, MF_T + 6 * w + 4);
+    line_t L = add ? ml_add_step_raw(T, lane_load<g2a_t>(H, (size_t)si)) : ml_dbl_step_raw(T);
+    mf_put2(lds, MF_T + 6 * w, T.X);
+    mf_put2(lds, MF_T + 6 * w + 2, T.Y);
+    mf_put2(lds, MF_T + 6 * w + 4, T.Z);
+    const g1a_t Pk = lane_load<g1a_t>(P, (size_t)si);
+    L = line_eval(L, Pk.x, Pk.y);
+    mf_put2(lds, MF_LC(w, 0), fp2_select(use, L.l00, fp2_one()));
+    mf_put2(lds, MF_LC(w, 1), fp2_select(use, L.l01, fp2_zero()));
+    mf_put2(lds, MF_LC(w, 2), fp2_select(use, L.l11, fp2_zero()));
+    __syncthreads();
+  };
+  // f = 1 (each wave writes a third of the coefficients' limbs: c0.c0 = 1, the rest 0)
+  if (w < 2) {
+    mf_put2(lds, MF_FC(3 * w), w == 0 ? fp2_one() : fp2_zero());
+    mf_put2(lds, MF_FC(3 * w + 1), fp2_zero());
+    mf_put2(lds, MF_FC(3 * w + 2), fp2_zero());
+  }
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  line_phase(false);  // the first doubling
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
+  line_phase(true);  // bit 62 of |x|
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
+#pragma unroll 1
+  for (int b = 61; b >= 0; b--) {
+    mf_sqr(lds, w);
+    line_phase(false);
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
+    if ((xa >> b) & 1u) {
+      line_phase(true);
+#pragma unroll 1
+      for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
+    }
+  }
+  // f_item = conj(f): wave w stores Fp components 3w..3w+2 (components 6..11 negated)
+  if (live) {
+    uint32_t* o = f_out + it * (size_t)lsgl::W_F12 + pair_h();  // W_F12: words per item (both lanes)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int c = 3 * w + j;
+      fp_t v = mf_get(lds, MF_F + c);
+      if (c >= 6) v = fp_neg(v);
+#pragma unroll
+      for (int k = 0; k < LSG_PL; k++) o[(7 * c + k) * LSG_GROUP] = v.l[k];
+    }
+  }
+}
+
 namespace lsgk {
+hipError_t miller_fused(hipStream_t st, int n_items, const int32_t* item_first, const int32_t* item_cnt,
+                        const uint32_t* P, const uint8_t* pinf, const uint8_t* hinf, const int32_t* err,
+                        const uint32_t* H, uint32_t* f) {
+  if (n_items <= 0) return hipSuccess;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_miller_fused,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)MF_LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_miller_fused, dim3((n_items + MF_ITEMS - 1) / MF_ITEMS), dim3(256), MF_LDS_BYTES, st, n_items, item_first,
+                     item_cnt, P, pinf, hinf, err, H, f);
+  return hipGetLastError();
+}
 hipError_t miller_lines(hipStream_t st, int n, const uint32_t* H, uint32_t* lines) {
   LSG_LAUNCH_ITEMS(k_miller_lines, n, st, n, H, lines);
 }

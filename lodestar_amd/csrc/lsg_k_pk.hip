@@ -59,7 +59,7 @@ __global__ void LSG_KERNEL_ATTR k_pk_scale(int n, const uint32_t* __restrict__ a
   g1p_t acc = lane_load<g1p_t>(agg, item);
   uint64_t r = rnd[item];
   bool is_inf = proj_is_inf(acc);
-  if (r != 0 && !is_inf) acc = proj_mul_u64(acc, r);
+  if (r != 0 && !is_inf) acc = proj_mul_u64_s3(acc, r);
   lane_store(Pp, item, acc);
   lane_store(zP, item, is_inf ? fp_zero() : acc.Z);
   if (lead) pinf[item] = is_inf ? 1 : 0;

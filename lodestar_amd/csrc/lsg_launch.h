@@ -49,6 +49,10 @@ hipError_t g1p_to_bytes(hipStream_t st, int n, const uint32_t* pts, uint8_t* out
 hipError_t sk_to_pk(hipStream_t st, int n, const uint8_t* sks, uint8_t* out96);
 
 // ---- Miller loop (lsg_k_miller.hip)                                   SURVEY 8a M5
+// lines in LDS, four waves per item of <= 4 sets (f_item = prod of the item's pairs)
+hipError_t miller_fused(hipStream_t st, int n_items, const int32_t* item_first, const int32_t* item_cnt,
+                        const uint32_t* P, const uint8_t* pinf, const uint8_t* hinf, const int32_t* err,
+                        const uint32_t* H, uint32_t* f);
 hipError_t miller_lines(hipStream_t st, int n, const uint32_t* H, uint32_t* lines);
 // K = pairs per item (1, 2 or 4)
 hipError_t miller_accum(hipStream_t st, int K, int n_items, const int32_t* item_first, const int32_t* item_cnt,

@@ -106,7 +106,7 @@ void hc_g1_mul_u64(const uint8_t* in96, uint64_t k, uint8_t* out96) {
   g1a_t p;
   bool inf;
   g1_deserialize(p, inf, in96, 96);
-  g1p_t r = proj_mul_u64(proj_from_aff(p), k);
+  g1p_t r = proj_mul_u64_s3(proj_from_aff(p), k);
   bool rinf = proj_is_inf(r);
   g1a_t a = rinf ? g1a_t{fp_zero(), fp_zero()} : proj_to_aff(r);
   g1_serialize(out96, a, rinf);
@@ -189,10 +189,10 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
   lsg_mul_count = 0;
   g1_deserialize(pk, inf, pk96, 96);
   counts[2] = lsg_mul_count;
-  g1a_t P = proj_to_aff(proj_mul_u64(proj_from_aff(pk), r));  // value (inversion not counted:)
+  g1a_t P = proj_to_aff(proj_mul_u64_s3(proj_from_aff(pk), r));  // value (inversion not counted:)
   lsg_mul_count = 0;
   {  // device: projective [r]PK, 1/Z from the batched inversion (3 M per element), 2 M to affine
-    g1p_t Pp = proj_mul_u64(proj_from_aff(pk), r);
+    g1p_t Pp = proj_mul_u64_s3(proj_from_aff(pk), r);
     fp_t zi = fp_one();
     (void)fp_mul(Pp.X, zi);
     (void)fp_mul(Pp.Y, zi);

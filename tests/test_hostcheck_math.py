@@ -208,7 +208,8 @@ def test_expand_and_sswu(hc):
 def test_scalar_mul(hc):
     pk = E1.mul(G1_GEN, 0xABCDEF)
     Q = E2.mul(G2_GEN, 12345)
-    for k in [1, 2, 3, (1 << 64) - 1, rng.getrandbits(64), rng.getrandbits(64) | (1 << 63)]:
+    for k in [1, 2, 3, 4, 7, 8, 0x4924924924924924, 0xDB6DB6DB6DB6DB6D, 1 << 63, (1 << 63) - 1, (1 << 64) - 1,
+              rng.getrandbits(64), rng.getrandbits(64) | (1 << 63)]:  # signed 3-bit windows: carries
         hc.hc_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
         hc.hc_g2_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
         o = buf(96)

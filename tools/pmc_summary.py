@@ -65,8 +65,9 @@ def main():
             cnt.setdefault(k, {}).update(cs)
     opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
     mk = os.environ.get("LSG_MILLER_K", "4")
-    stage = {"k_miller_accum<4>": f"miller_accum{mk}_per_set", "k_miller_lines": "miller_lines",
-             "k_sig_subgroup": "sig_subgroup", "k_sig_decode": "sig_decode", "k_pk_scale": "pk_scale"}
+    stage = {"k_miller_accum<4>": [f"miller_accum{mk}_per_set"], "k_miller_lines": ["miller_lines"],
+             "k_miller_fused": ["miller_lines", "miller_accum4_per_set"],
+             "k_sig_subgroup": ["sig_subgroup"], "k_sig_decode": ["sig_decode"], "k_pk_scale": ["pk_scale"]}
     rows, traffic = {}, {}
     for k in sorted(set(dur) | set(cnt), key=lambda x: -dur.get(x, {}).get("avg_ns", 0)):
         d, c = dur.get(k, {}), cnt.get(k, {})
@@ -80,8 +81,8 @@ def main():
             r["hbm_bytes"] = round(b)
             r["hbm_bytes_per_set"] = round(b / a.sets, 1)
             traffic[k.split("<")[0]] = {"hbm_bytes_per_dispatch": round(b)}
-        if k in stage and stage[k] in opc["stage_fp_muls"] and d.get("avg_ns"):
-            mads = opc["stage_fp_muls"][stage[k]] * a.sets * opc["mads_per_fp_mul"]
+        if k in stage and all(x in opc["stage_fp_muls"] for x in stage[k]) and d.get("avg_ns"):
+            mads = sum(opc["stage_fp_muls"][x] for x in stage[k]) * a.sets * opc["mads_per_fp_mul"]
             r["achieved_tmad_s"] = round(mads / (d["avg_ns"] * 1e-9) / 1e12, 3)
             r["frac_of_peak"] = round(mads / (d["avg_ns"] * 1e-9) / a.peak, 4)
         rows[k] = r
