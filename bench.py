@@ -398,11 +398,13 @@ def main():
     stats_acc.clear()
     barrier()
     t0 = time.perf_counter()
+    w0 = time.monotonic_ns()  # CLOCK_MONOTONIC: the clock of rocprofv3's API/kernel timestamps
     submit_wall.clear()
     lat, ktimes = run(args.steps, args.depth, capture=True)
     submit_wall_timed = sorted(submit_wall)
     barrier()
     elapsed = time.perf_counter() - t0
+    w1 = time.monotonic_ns()
     allocs = ctx.allocation_count() - allocs0
     if dist is not None:
         import torch
@@ -486,7 +488,7 @@ def main():
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
             "pipeline_depth": args.depth, "distinct_packages": len(prepared),
-            "allocations_in_timed_region": allocs,
+            "allocations_in_timed_region": allocs, "timed_window_monotonic_ns": [w0, w1],
             "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
             "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),
             "submit_call_ms_p50_max": [round(1e3 * statistics.median(submit_wall_timed), 3),
