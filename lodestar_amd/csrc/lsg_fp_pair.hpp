@@ -147,56 +147,101 @@ extern unsigned long long lsg_mul_count;
 #endif
 
 // ---- Montgomery product (CIOS over the 14 radix-2^29 limbs, i-loop over time)
-LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
-  LSG_COUNT_MUL();
+// N independent products advance step by step together: in-order issue stalls a lone
+// product on its serial chain (t0 mad -> m -> DPP broadcast -> m*p mads -> retire) at the
+// one or two waves per SIMD the per-set kernels run at; N chains fill those stalls.
+template <int N>
+LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
   const bool top = pair_top();
   uint32_t p[LSG_PL];
 #pragma unroll
   for (int j = 0; j < LSG_PL; j++) p[j] = pair_pick(LSG_P, j);
-  int64_t t[LSG_PL];
+  int64_t t[N][LSG_PL];
 #pragma unroll
-  for (int j = 0; j < LSG_PL; j++) t[j] = 0;
+  for (int n = 0; n < N; n++)
+#pragma unroll
+    for (int j = 0; j < LSG_PL; j++) t[n][j] = 0;
 #pragma unroll
   for (int i = 0; i < 14; i++) {
-    const uint32_t bs = b.l[i % LSG_PL];
-    const int32_t bi = (int32_t)(i / LSG_PL == 0 ? pbcast<0>(bs) : pbcast<LSG_GROUP - 1>(bs));
 #pragma unroll
-    for (int j = 0; j < LSG_PL; j++) t[j] += (int64_t)(int32_t)a.l[j] * bi;
-    const uint32_t m = pbcast<0>(((uint32_t)t[0] * LSG_N0P) & LSG_M29);
+    for (int n = 0; n < N; n++) {
+      const uint32_t bs = b[n].l[i % LSG_PL];
+      const int32_t bi = (int32_t)(i / LSG_PL == 0 ? pbcast<0>(bs) : pbcast<LSG_GROUP - 1>(bs));
 #pragma unroll
-    for (int j = 0; j < LSG_PL; j++) t[j] += (int64_t)(int32_t)m * (int32_t)p[j];
-    // retire limb 0 (its low 29 bits are zero on lane 0): the high part carries into the
-    // next accumulator of the same lane, lane 1's low 29 bits move down to lane 0's top
-    const int64_t c = t[0] >> 29;
-    const uint32_t mv = pdown((uint32_t)t[0] & LSG_M29);
+      for (int j = 0; j < LSG_PL; j++) t[n][j] += (int64_t)(int32_t)a[n].l[j] * bi;
+    }
 #pragma unroll
-    for (int j = 0; j < LSG_PL - 1; j++) t[j] = t[j + 1];
-    t[0] += c;
-    t[LSG_PL - 1] = (int64_t)mv;
+    for (int n = 0; n < N; n++) {
+      const uint32_t m = pbcast<0>(((uint32_t)t[n][0] * LSG_N0P) & LSG_M29);
+#pragma unroll
+      for (int j = 0; j < LSG_PL; j++) t[n][j] += (int64_t)(int32_t)m * (int32_t)p[j];
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      // retire limb 0 (its low 29 bits are zero on lane 0): the high part carries into the
+      // next accumulator of the same lane, lane 1's low 29 bits move down to lane 0's top
+      const int64_t c = t[n][0] >> 29;
+      const uint32_t mv = pdown((uint32_t)t[n][0] & LSG_M29);
+#pragma unroll
+      for (int j = 0; j < LSG_PL - 1; j++) t[n][j] = t[n][j + 1];
+      t[n][0] += c;
+      t[n][LSG_PL - 1] = (int64_t)mv;
+    }
   }
 #pragma unroll
-  for (int j = 0; j < LSG_PL - 1; j++) {
-    t[j + 1] += t[j] >> 29;
-    t[j] &= (int64_t)LSG_M29;
+  for (int n = 0; n < N; n++) {
+#pragma unroll
+    for (int j = 0; j < LSG_PL - 1; j++) {
+      t[n][j + 1] += t[n][j] >> 29;
+      t[n][j] &= (int64_t)LSG_M29;
+    }
   }
 #if LSG_PAIR_G == 2
-  const int64_t ct = t[LSG_PL - 1] >> 29;
-  const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
-  if (!top) t[LSG_PL - 1] &= (int64_t)LSG_M29;
-  t[0] += (int64_t)(((uint64_t)chi << 32) | clo);
 #pragma unroll
-  for (int j = 0; j < LSG_PL - 1; j++) {
-    t[j + 1] += t[j] >> 29;
-    t[j] &= (int64_t)LSG_M29;
+  for (int n = 0; n < N; n++) {
+    const int64_t ct = t[n][LSG_PL - 1] >> 29;
+    const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
+    if (!top) t[n][LSG_PL - 1] &= (int64_t)LSG_M29;
+    t[n][0] += (int64_t)(((uint64_t)chi << 32) | clo);
+#pragma unroll
+    for (int j = 0; j < LSG_PL - 1; j++) {
+      t[n][j + 1] += t[n][j] >> 29;
+      t[n][j] &= (int64_t)LSG_M29;
+    }
   }
 #else
   (void)top;
 #endif
-  fp_t r;
 #pragma unroll
-  for (int j = 0; j < LSG_PL; j++) r.l[j] = (uint32_t)t[j];
+  for (int n = 0; n < N; n++)
+#pragma unroll
+    for (int j = 0; j < LSG_PL; j++) r[n].l[j] = (uint32_t)t[n][j];
+}
+LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
+  LSG_COUNT_MUL();
+  fp_t r;
+  pair_mont_mul_n<1>(&r, &a, &b);
   return r;
 }
+// two products in one call (28 argument VGPRs: the call ABI passes 32 in registers)
+struct fp_duo {
+  fp_t x, y;
+};
+LSG_PLEAF fp_duo pair_mont_mul2(fp_t a0, fp_t b0, fp_t a1, fp_t b1) {
+  LSG_COUNT_MUL();
+  LSG_COUNT_MUL();
+  const fp_t a[2] = {a0, a1}, b[2] = {b0, b1};
+  fp_t r[2];
+  pair_mont_mul_n<2>(r, a, b);
+  return fp_duo{r[0], r[1]};
+}
+// Karatsuba Fp2 product (a0 + a1 u)(b0 + b1 u), u^2 = -1: its three Fp products in one call
+LSG_PLEAF fp_duo pair_fp2_mul(fp_t a0, fp_t a1, fp_t b0, fp_t b1);
+// Fp2 square (a0 + a1)(a0 - a1), 2 a0 a1: its two Fp products in one call
+LSG_PLEAF fp_duo pair_fp2_sqr(fp_t a0, fp_t a1);
+#ifndef LSG_NO_FP2_LEAF  // (A/B builds: -DLSG_NO_FP2_LEAF issues Fp2 products as three separate calls)
+#define LSG_FP2_LEAF 1  // lsg_tower.hpp's fp2_mul / fp2_sqr call the two leaves above
+#endif
 
 // ------------------------------------------------------------------ Fp API
 LSG_PFN fp_t fp_zero() {
@@ -226,21 +271,39 @@ LSG_PFN fp_t fp_sub(const fp_t& a, const fp_t& b) {
 LSG_PFN fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
 LSG_PFN fp_t fp_mul(const fp_t& a, const fp_t& b) { return pair_mont_mul(a, b); }
 LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
-  fp_t t = pair_mont_mul(a0, b0);
-  r1 = pair_mont_mul(a1, b1);
-  r0 = t;
+  const fp_duo d = pair_mont_mul2(a0, b0, a1, b1);
+  r0 = d.x;
+  r1 = d.y;
 }
 LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
                      const fp_t& a2, const fp_t& b2) {
-  fp_t t0 = pair_mont_mul(a0, b0);
-  fp_t t1 = pair_mont_mul(a1, b1);
+  const fp_duo d = pair_mont_mul2(a0, b0, a1, b1);
   r2 = pair_mont_mul(a2, b2);
-  r0 = t0;
-  r1 = t1;
+  r0 = d.x;
+  r1 = d.y;
 }
 LSG_PFN void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
 #pragma unroll
   for (int g = 0; g < 9; g += 3) fp_mul3(r[g], r[g + 1], r[g + 2], a[g], b[g], a[g + 1], b[g + 1], a[g + 2], b[g + 2]);
+}
+
+// the Fp2 leaves declared above (they need fp_add / fp_sub)
+LSG_PLEAF fp_duo pair_fp2_mul(fp_t a0, fp_t a1, fp_t b0, fp_t b1) {
+  LSG_COUNT_MUL();
+  LSG_COUNT_MUL();
+  LSG_COUNT_MUL();
+  const fp_t a[3] = {a0, a1, fp_add(a0, a1)}, b[3] = {b0, b1, fp_add(b0, b1)};
+  fp_t t[3];
+  pair_mont_mul_n<3>(t, a, b);
+  return fp_duo{fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
+}
+LSG_PLEAF fp_duo pair_fp2_sqr(fp_t a0, fp_t a1) {
+  LSG_COUNT_MUL();
+  LSG_COUNT_MUL();
+  const fp_t a[2] = {fp_add(a0, a1), a0}, b[2] = {fp_sub(a0, a1), a1};
+  fp_t t[2];
+  pair_mont_mul_n<2>(t, a, b);
+  return fp_duo{t[0], fp_add(t[1], t[1])};
 }
 
 // ---- canonical values

@@ -101,16 +101,26 @@ LSG_INL fp2_t fp2_conj(const fp2_t& a) { return fp2_t(a.c0, fp_neg(a.c1)); }
 
 // Karatsuba: 3 Fp multiplications
 LSG_INL fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+#ifdef LSG_FP2_LEAF
+  const fp_duo d = pair_fp2_mul(a.c0, a.c1, b.c0, b.c1);
+  return fp2_t(d.x, d.y);
+#else
   fp_t t0, t1, t2;
   fp_mul3(t0, t1, t2, a.c0, b.c0, a.c1, b.c1, fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return fp2_t(fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1));
+#endif
 }
 
 // (a0 + a1)(a0 - a1), 2 a0 a1
 LSG_INL fp2_t fp2_sqr(const fp2_t& a) {
+#ifdef LSG_FP2_LEAF
+  const fp_duo d = pair_fp2_sqr(a.c0, a.c1);
+  return fp2_t(d.x, d.y);
+#else
   fp_t t0, t1;
   fp_mul2(t0, t1, fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1), a.c0, a.c1);
   return fp2_t(t0, fp_dbl(t1));
+#endif
 }
 
 LSG_INL fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& k) {
