@@ -223,23 +223,94 @@ LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
   pair_mont_mul_n<1>(&r, &a, &b);
   return r;
 }
-// two products in one call (28 argument VGPRs: the call ABI passes 32 in registers)
+// Multi-product leaves.  Operands cross the call as 8-word vectors: the gfx950 call ABI
+// passes vector arguments in VGPRs (up to 32), but only the first two 7-word structs; the
+// rest went byval through scratch at every call site.
+// LSG_LEAF_MODE (A/B builds): 0 = one product per call everywhere, 1 = the multi-product
+// leaves below with their products one after another (default), 2 = interleaved
+#ifndef LSG_LEAF_MODE
+#define LSG_LEAF_MODE 1
+#endif
+#if LSG_PAIR_G == 2 && LSG_LEAF_MODE == 1
+#define LSG_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define LSG_SCHED_FENCE() ((void)0)
+#endif
+#if LSG_PAIR_G == 2
+// (the call ABI keeps v31 for the work-item ids, so a fourth 8-word operand would put one
+// word on the stack: the last operand of a four-operand leaf travels as 4 + 3 words)
+typedef uint32_t fp_arg4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t fp_arg3_t __attribute__((ext_vector_type(3)));
+struct fp_tail {
+  fp_arg4_t lo;
+  fp_arg3_t hi;
+};
+LSG_PFN fp_arg4_t fp_pack_lo(const fp_t& a) { return fp_arg4_t{a.l[0], a.l[1], a.l[2], a.l[3]}; }
+LSG_PFN fp_arg3_t fp_pack_hi(const fp_t& a) { return fp_arg3_t{a.l[4], a.l[5], a.l[6]}; }
+LSG_PFN fp_t fp_unpack2(const fp_arg4_t& lo, const fp_arg3_t& hi) {
+  fp_t r;
+  r.l[0] = lo[0];
+  r.l[1] = lo[1];
+  r.l[2] = lo[2];
+  r.l[3] = lo[3];
+  r.l[4] = hi[0];
+  r.l[5] = hi[1];
+  r.l[6] = hi[2];
+  return r;
+}
+#define LSG_TAIL_PARAMS(x) fp_arg4_t x##_lo, fp_arg3_t x##_hi
+#define LSG_TAIL_ARGS(v) fp_pack_lo(v), fp_pack_hi(v)
+#define LSG_TAIL_UNPACK(x) fp_unpack2(x##_lo, x##_hi)
+typedef uint32_t fp_arg_t __attribute__((ext_vector_type(8)));
+LSG_PFN fp_arg_t fp_pack(const fp_t& a) {
+  fp_arg_t v;  // word 7 is never read
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) v[k] = a.l[k];
+  return v;
+}
+LSG_PFN fp_t fp_unpack(const fp_arg_t& v) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = v[k];
+  return r;
+}
+#else
+#define LSG_TAIL_PARAMS(x) fp_t x
+#define LSG_TAIL_ARGS(v) (v)
+#define LSG_TAIL_UNPACK(x) (x)
+typedef fp_t fp_arg_t;
+LSG_PFN fp_arg_t fp_pack(const fp_t& a) { return a; }
+LSG_PFN fp_t fp_unpack(const fp_arg_t& v) { return v; }
+#endif
 struct fp_duo {
   fp_t x, y;
 };
-LSG_PLEAF fp_duo pair_mont_mul2(fp_t a0, fp_t b0, fp_t a1, fp_t b1) {
+LSG_PLEAF fp_duo pair_mont_mul2_v(fp_arg_t a0, fp_arg_t b0, fp_arg_t a1, LSG_TAIL_PARAMS(b1)) {
   LSG_COUNT_MUL();
   LSG_COUNT_MUL();
-  const fp_t a[2] = {a0, a1}, b[2] = {b0, b1};
+  const fp_t x[2] = {fp_unpack(a0), fp_unpack(a1)}, y[2] = {fp_unpack(b0), LSG_TAIL_UNPACK(b1)};
   fp_t r[2];
-  pair_mont_mul_n<2>(r, a, b);
+#if LSG_LEAF_MODE == 2
+  pair_mont_mul_n<2>(r, x, y);
+#else
+  pair_mont_mul_n<1>(&r[0], &x[0], &y[0]);
+  LSG_SCHED_FENCE();
+  pair_mont_mul_n<1>(&r[1], &x[1], &y[1]);
+#endif
   return fp_duo{r[0], r[1]};
 }
+LSG_PFN fp_duo pair_mont_mul2(const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+  return pair_mont_mul2_v(fp_pack(a0), fp_pack(b0), fp_pack(a1), LSG_TAIL_ARGS(b1));
+}
 // Karatsuba Fp2 product (a0 + a1 u)(b0 + b1 u), u^2 = -1: its three Fp products in one call
-LSG_PLEAF fp_duo pair_fp2_mul(fp_t a0, fp_t a1, fp_t b0, fp_t b1);
+LSG_PLEAF fp_duo pair_fp2_mul_v(fp_arg_t a0, fp_arg_t a1, fp_arg_t b0, LSG_TAIL_PARAMS(b1));
 // Fp2 square (a0 + a1)(a0 - a1), 2 a0 a1: its two Fp products in one call
-LSG_PLEAF fp_duo pair_fp2_sqr(fp_t a0, fp_t a1);
-#ifndef LSG_NO_FP2_LEAF  // (A/B builds: -DLSG_NO_FP2_LEAF issues Fp2 products as three separate calls)
+LSG_PLEAF fp_duo pair_fp2_sqr_v(fp_arg_t a0, fp_arg_t a1);
+LSG_PFN fp_duo pair_fp2_mul(const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
+  return pair_fp2_mul_v(fp_pack(a0), fp_pack(a1), fp_pack(b0), LSG_TAIL_ARGS(b1));
+}
+LSG_PFN fp_duo pair_fp2_sqr(const fp_t& a0, const fp_t& a1) { return pair_fp2_sqr_v(fp_pack(a0), fp_pack(a1)); }
+#if LSG_LEAF_MODE != 0
 #define LSG_FP2_LEAF 1  // lsg_tower.hpp's fp2_mul / fp2_sqr call the two leaves above
 #endif
 
@@ -270,6 +341,21 @@ LSG_PFN fp_t fp_sub(const fp_t& a, const fp_t& b) {
 }
 LSG_PFN fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
 LSG_PFN fp_t fp_mul(const fp_t& a, const fp_t& b) { return pair_mont_mul(a, b); }
+#if LSG_LEAF_MODE == 0
+LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
+  fp_t t = pair_mont_mul(a0, b0);
+  r1 = pair_mont_mul(a1, b1);
+  r0 = t;
+}
+LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
+                     const fp_t& a2, const fp_t& b2) {
+  fp_t t0 = pair_mont_mul(a0, b0);
+  fp_t t1 = pair_mont_mul(a1, b1);
+  r2 = pair_mont_mul(a2, b2);
+  r0 = t0;
+  r1 = t1;
+}
+#else
 LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
   const fp_duo d = pair_mont_mul2(a0, b0, a1, b1);
   r0 = d.x;
@@ -282,27 +368,48 @@ LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b
   r0 = d.x;
   r1 = d.y;
 }
+#endif
 LSG_PFN void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
 #pragma unroll
   for (int g = 0; g < 9; g += 3) fp_mul3(r[g], r[g + 1], r[g + 2], a[g], b[g], a[g + 1], b[g + 1], a[g + 2], b[g + 2]);
 }
 
 // the Fp2 leaves declared above (they need fp_add / fp_sub)
-LSG_PLEAF fp_duo pair_fp2_mul(fp_t a0, fp_t a1, fp_t b0, fp_t b1) {
+LSG_PLEAF fp_duo pair_fp2_mul_v(fp_arg_t va0, fp_arg_t va1, fp_arg_t vb0, LSG_TAIL_PARAMS(vb1)) {
   LSG_COUNT_MUL();
   LSG_COUNT_MUL();
   LSG_COUNT_MUL();
-  const fp_t a[3] = {a0, a1, fp_add(a0, a1)}, b[3] = {b0, b1, fp_add(b0, b1)};
+  const fp_t a0 = fp_unpack(va0), a1 = fp_unpack(va1), b0 = fp_unpack(vb0), b1 = LSG_TAIL_UNPACK(vb1);
+  // the three products run one after another (sched_barrier): interleaved, the leaf needed
+  // ~180 VGPRs, and every caller had to spill around it what the call clobbers
   fp_t t[3];
+#if LSG_LEAF_MODE == 2
+  const fp_t a[3] = {a0, a1, fp_add(a0, a1)}, b[3] = {b0, b1, fp_add(b0, b1)};
   pair_mont_mul_n<3>(t, a, b);
+#else
+  pair_mont_mul_n<1>(&t[0], &a0, &b0);
+  LSG_SCHED_FENCE();
+  pair_mont_mul_n<1>(&t[1], &a1, &b1);
+  LSG_SCHED_FENCE();
+  const fp_t s0 = fp_add(a0, a1), s1 = fp_add(b0, b1);
+  pair_mont_mul_n<1>(&t[2], &s0, &s1);
+#endif
   return fp_duo{fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
 }
-LSG_PLEAF fp_duo pair_fp2_sqr(fp_t a0, fp_t a1) {
+LSG_PLEAF fp_duo pair_fp2_sqr_v(fp_arg_t va0, fp_arg_t va1) {
   LSG_COUNT_MUL();
   LSG_COUNT_MUL();
-  const fp_t a[2] = {fp_add(a0, a1), a0}, b[2] = {fp_sub(a0, a1), a1};
+  const fp_t a0 = fp_unpack(va0), a1 = fp_unpack(va1);
   fp_t t[2];
+#if LSG_LEAF_MODE == 2
+  const fp_t a[2] = {fp_add(a0, a1), a0}, b[2] = {fp_sub(a0, a1), a1};
   pair_mont_mul_n<2>(t, a, b);
+#else
+  const fp_t s = fp_add(a0, a1), d = fp_sub(a0, a1);
+  pair_mont_mul_n<1>(&t[0], &s, &d);
+  LSG_SCHED_FENCE();
+  pair_mont_mul_n<1>(&t[1], &a0, &a1);
+#endif
   return fp_duo{t[0], fp_add(t[1], t[1])};
 }
 

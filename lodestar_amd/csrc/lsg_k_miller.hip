@@ -266,19 +266,23 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
     mf_put2(lds, MF_T + 6 * w + 4, T.Z);
   }
   auto line_phase = [&](bool add) {
+    // w and si re-materialised per phase: hoisted out of the loop, the wave-dependent LDS
+    // slot addresses and point pointers were spilled to scratch and reloaded every step
+    int wl = w, sl = si;
+    asm volatile("" : "+v"(wl), "+v"(sl));
     g2p_t T;  // this wave's own slots: no other wave touches them
-    T.X = mf_get2(lds, MF_T + 6 * w);
-    T.Y = mf_get2(lds, MF_T + 6 * w + 2);
-    T.Z = mf_get2(lds, MF_T + 6 * w + 4);
-    line_t L = add ? ml_add_step_raw(T, lane_load<g2a_t>(H, (size_t)si)) : ml_dbl_step_raw(T);
-    mf_put2(lds, MF_T + 6 * w, T.X);
-    mf_put2(lds, MF_T + 6 * w + 2, T.Y);
-    mf_put2(lds, MF_T + 6 * w + 4, T.Z);
-    const g1a_t Pk = lane_load<g1a_t>(P, (size_t)si);
+    T.X = mf_get2(lds, MF_T + 6 * wl);
+    T.Y = mf_get2(lds, MF_T + 6 * wl + 2);
+    T.Z = mf_get2(lds, MF_T + 6 * wl + 4);
+    line_t L = add ? ml_add_step_raw(T, lane_load<g2a_t>(H, (size_t)sl)) : ml_dbl_step_raw(T);
+    mf_put2(lds, MF_T + 6 * wl, T.X);
+    mf_put2(lds, MF_T + 6 * wl + 2, T.Y);
+    mf_put2(lds, MF_T + 6 * wl + 4, T.Z);
+    const g1a_t Pk = lane_load<g1a_t>(P, (size_t)sl);
     L = line_eval(L, Pk.x, Pk.y);
-    mf_put2(lds, MF_LC(w, 0), fp2_select(use, L.l00, fp2_one()));
-    mf_put2(lds, MF_LC(w, 1), fp2_select(use, L.l01, fp2_zero()));
-    mf_put2(lds, MF_LC(w, 2), fp2_select(use, L.l11, fp2_zero()));
+    mf_put2(lds, MF_LC(wl, 0), fp2_select(use, L.l00, fp2_one()));
+    mf_put2(lds, MF_LC(wl, 1), fp2_select(use, L.l01, fp2_zero()));
+    mf_put2(lds, MF_LC(wl, 2), fp2_select(use, L.l11, fp2_zero()));
     __syncthreads();
   };
   // f = 1 (each wave writes a third of the coefficients' limbs: c0.c0 = 1, the rest 0)
