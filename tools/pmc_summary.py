@@ -51,6 +51,24 @@ def counters(d):
     return {k: {c: v[0] / v[1] for c, v in cs.items()} for k, cs in acc.items()}
 
 
+def serial_durations(d):
+    """per-kernel average dispatch duration in a --pmc pass: counter collection serialises the
+    dispatches, so these are each kernel alone on the GPU (the kernel trace of the depth-1 run
+    still overlaps the package's two streams)"""
+    acc = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        seen = set()
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Dispatch_Id"] in seen:
+                    continue
+                seen.add(row["Dispatch_Id"])
+                a = acc.setdefault(kname(row["Kernel_Name"]), [0.0, 0])
+                a[0] += int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                a[1] += 1
+    return {k: v[0] / v[1] for k, v in acc.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -59,6 +77,7 @@ def main():
     ap.add_argument("--tag", default="r02")
     a = ap.parse_args()
     dur = durations(os.path.join(a.dir, "iso_trace", "run_results.db"))
+    ser = serial_durations(os.path.join(a.dir, "iso_sq"))
     cnt = {}
     for sub in ("iso_sq", "iso_sq2", "iso_fetch", "iso_write"):
         for k, cs in counters(os.path.join(a.dir, sub)).items():
@@ -76,6 +95,11 @@ def main():
             r["valu_instr"] = c["SQ_INSTS_VALU"]
             r["int64_share"] = round(c.get("SQ_INSTS_VALU_INT64", 0) / max(c["SQ_INSTS_VALU"], 1), 3)
             r["valu_issue_share"] = round(c.get("SQ_ACTIVE_INST_VALU", 0) / max(c.get("SQ_WAVE_CYCLES", 1), 1), 3)
+            # wave cycles (SQ_WAVE_CYCLES is in quad-cycles) per VALU instruction: ~4-6 means
+            # the wave issues back to back (instruction-bound), much more means it waits
+            r["wave_cycles_per_valu"] = round(4 * c.get("SQ_WAVE_CYCLES", 0) / max(c["SQ_INSTS_VALU"], 1), 2)
+        if k in ser:
+            r["serial_us"] = round(ser[k] / 1e3, 2)
         if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
             b = 1024.0 * (2 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0))
             r["hbm_bytes"] = round(b)
@@ -85,19 +109,24 @@ def main():
             mads = sum(opc["stage_fp_muls"][x] for x in stage[k]) * a.sets * opc["mads_per_fp_mul"]
             r["achieved_tmad_s"] = round(mads / (d["avg_ns"] * 1e-9) / 1e12, 3)
             r["frac_of_peak"] = round(mads / (d["avg_ns"] * 1e-9) / a.peak, 4)
+            if k in ser:
+                r["frac_of_peak_serial"] = round(mads / (ser[k] * 1e-9) / a.peak, 4)
         rows[k] = r
     out = {"sets_per_launch": a.sets, "peak_mad_per_s": a.peak, "kernels": rows,
-           "source": "tools/gpu_pmc.sh (depth-1 bench, one package at a time) -> tools/pmc_summary.py"}
+           "source": "tools/gpu_pmc.sh (depth-1 bench, one package at a time) -> tools/pmc_summary.py",
+           "columns": "avg_us: kernel trace of the depth-1 run (the package's two streams overlap); serial_us: the "
+                      "same dispatches under --pmc, which serialises them (each kernel alone on the GPU); "
+                      "frac_of_peak / frac_of_peak_serial: algorithmic mads over those durations / peak"}
     with open(os.path.join(ROOT, "profiles", f"{a.tag}_pmc_isolation.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(ROOT, "profiles", f"{a.tag}_pmc_traffic.json"), "w") as f:
         json.dump({"sets_per_launch": a.sets, "kernels": traffic,
                    "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM section)"}, f, indent=1)
-    print(f"{'kernel':28s} {'calls':>5s} {'avg_us':>9s} {'VALU/disp':>10s} {'i64':>5s} {'issue':>6s} {'B/set':>8s} {'Tmad/s':>7s} {'frac':>6s}")
+    print(f"{'kernel':28s} {'calls':>5s} {'avg_us':>9s} {'alone_us':>9s} {'VALU/disp':>10s} {'i64':>5s} {'cyc/VALU':>8s} {'B/set':>8s} {'frac':>6s} {'alone':>6s}")
     for k, r in rows.items():
-        print(f"{k[:28]:28s} {r.get('calls') or 0:5d} {r['avg_us']:9.1f} {r.get('valu_instr', 0):10.3g} "
-              f"{r.get('int64_share', 0):5.2f} {r.get('valu_issue_share', 0):6.3f} {r.get('hbm_bytes_per_set', 0):8.1f} "
-              f"{r.get('achieved_tmad_s', 0):7.2f} {r.get('frac_of_peak', 0):6.3f}")
+        print(f"{k[:28]:28s} {r.get('calls') or 0:5d} {r['avg_us']:9.1f} {r.get('serial_us', 0):9.1f} {r.get('valu_instr', 0):10.3g} "
+              f"{r.get('int64_share', 0):5.2f} {r.get('wave_cycles_per_valu', 0):8.2f} {r.get('hbm_bytes_per_set', 0):8.1f} "
+              f"{r.get('frac_of_peak', 0):6.3f} {r.get('frac_of_peak_serial', 0):6.3f}")
 
 
 if __name__ == "__main__":
