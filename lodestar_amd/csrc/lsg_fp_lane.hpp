@@ -178,6 +178,91 @@ LSG_DEVNOINL lsg_u32x16 lane_mont_mul9(lsg_u32x16 a, lsg_u32x16 b) {
   return o;
 }
 
+// ---- one item per wave: the four rows of a wave hold the same item, and a batch of N
+// independent products (fp_mul_list, lsg_tower.hpp) is split over them: row q computes
+// products q, q + 4, ... (M = ceil(N/4) per row, in one interleaved call where possible),
+// then every row collects all N results with ds_bpermute.  Everything outside the batches
+// runs replicated in the four rows, so every row keeps the whole item state.  The serial
+// per-group stages (final exponentiation, signature-side Miller loop) have one item per
+// group: a row per item left three quarters of their one wave idle.
+#ifndef LSG_ROWS_PER_ITEM
+#define LSG_ROWS_PER_ITEM 4
+#endif
+#if LSG_ROWS_PER_ITEM == 4
+#define LSG_ROW_SPLIT 1
+LSG_DEVI uint32_t row_q() { return (__lane_id() >> 4) & 3u; }
+// M independent products of lane values, in as few interleaved leaf calls as possible
+template <int M>
+LSG_DEVI void lane_mul_chunks(uint32_t* o, const uint32_t* a, const uint32_t* b) {
+  int k = 0;
+#pragma unroll
+  for (; k + 9 <= M; k += 9) {
+    lsg_u32x16 x, y;
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      x[t] = t < 9 ? a[k + t] : 0u;
+      y[t] = t < 9 ? b[k + t] : 0u;
+    }
+    lsg_u32x16 z = lane_mont_mul9(x, y);
+#pragma unroll
+    for (int t = 0; t < 9; t++) o[k + t] = z[t];
+  }
+#pragma unroll
+  for (; k + 3 <= M; k += 3) {
+    lsg_u32x4 x, y;
+    x.x = a[k];
+    x.y = a[k + 1];
+    x.z = a[k + 2];
+    x.w = 0;
+    y.x = b[k];
+    y.y = b[k + 1];
+    y.z = b[k + 2];
+    y.w = 0;
+    lsg_u32x4 z = lane_mont_mul3(x, y);
+    o[k] = z.x;
+    o[k + 1] = z.y;
+    o[k + 2] = z.z;
+  }
+  if (M - k == 2) {
+    lsg_u32x2 x, y;
+    x.x = a[k];
+    x.y = a[k + 1];
+    y.x = b[k];
+    y.y = b[k + 1];
+    lsg_u32x2 z = lane_mont_mul2(x, y);
+    o[k] = z.x;
+    o[k + 1] = z.y;
+  } else if (M - k == 1) {
+    o[k] = lane_mont_mul(a[k], b[k]);
+  }
+}
+template <int N>
+LSG_DEVI void lane_mul_rows(uint32_t* r, const uint32_t* x, const uint32_t* y) {
+  constexpr int M = (N + 3) / 4;
+  const uint32_t q = row_q();
+  uint32_t a[M], b[M], o[M];
+#pragma unroll
+  for (int j = 0; j < M; j++) {
+    // row q's operands of product 4j + q (a row past the end repeats product 4j)
+    uint32_t av = x[4 * j], bv = y[4 * j];
+#pragma unroll
+    for (int t = 1; t < 4; t++) {
+      if (4 * j + t < N) {
+        av = q == (uint32_t)t ? x[4 * j + t] : av;
+        bv = q == (uint32_t)t ? y[4 * j + t] : bv;
+      }
+    }
+    a[j] = av;
+    b[j] = bv;
+  }
+  lane_mul_chunks<M>(o, a, b);
+  const int l16 = (int)lane16();
+#pragma unroll
+  for (int k = 0; k < N; k++)
+    r[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((l16 + 16 * (k & 3)) << 2, (int)o[k >> 2]);
+}
+#endif
+
 LSG_DEVI uint32_t lane_add(uint32_t a, uint32_t b) {
   uint64_t s = (uint64_t)a + b;
   uint32_t z = (uint32_t)s;
@@ -245,6 +330,21 @@ LSG_DEVI void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& 
   r1 = fp_t(r.y);
   r2 = fp_t(r.z);
 }
+
+#ifdef LSG_ROW_SPLIT
+template <int N>
+LSG_DEVI void fp_mul_list_rows(fp_t* r, const fp_t* x, const fp_t* y) {
+  uint32_t xv[N], yv[N], rv[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    xv[k] = x[k].v;
+    yv[k] = y[k].v;
+  }
+  lane_mul_rows<N>(rv, xv, yv);
+#pragma unroll
+  for (int k = 0; k < N; k++) r[k] = fp_t(rv[k]);
+}
+#endif
 
 // ---- canonical predicates and byte I/O (row-uniform results)
 LSG_DEVI bool fp_canon_gt_half(const fp_t& c) {

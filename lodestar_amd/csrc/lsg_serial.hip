@@ -16,12 +16,13 @@ namespace {
 #include "lsg_io.hpp"
 }  // namespace
 
-#define LSG_ROW_TPB 64  // one wave: four items
+#define LSG_ROW_TPB 64  // one wave: LSG_ROWS_PER_ITEM rows per item, 4 / LSG_ROWS_PER_ITEM items
+#define ROW_ITEM() ((int)((blockIdx.x * blockDim.x + threadIdx.x) / (16 * LSG_ROWS_PER_ITEM)))
 
 __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_final_exp(int ng, const uint8_t* __restrict__ F576,
                                                                int32_t* __restrict__ verdict) {
   lsg_lane_setup();
-  const int item = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 16);
+  const int item = ROW_ITEM();
   if (item >= ng) return;
   bool one = fp12_is_one(final_exp(fp12_from_canon_bytes(F576 + 576 * (size_t)item)));
   if ((threadIdx.x & 15) == 0) verdict[item] = one ? 1 : 0;
@@ -30,7 +31,7 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_final_exp(int ng, const uin
 __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_miller_neg_g1(int ng, const uint8_t* __restrict__ S288,
                                                                    uint8_t* __restrict__ out576) {
   lsg_lane_setup();
-  const int item = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 16);
+  const int item = ROW_ITEM();
   if (item >= ng) return;
   g2p_t s = g2p_from_canon_bytes(S288 + 288 * (size_t)item);
   fp12_t r = fp12_one();
@@ -49,7 +50,7 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_miller_neg_g1(int ng, const
 __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_horner_miller(int ng, const uint8_t* __restrict__ C288,
                                                                    uint8_t* __restrict__ out576) {
   lsg_lane_setup();
-  const int item = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 16);
+  const int item = ROW_ITEM();
   if (item >= ng) return;
   const uint8_t* c = C288 + (size_t)288 * 64 * item;
   g2p_t s = g2p_from_canon_bytes(c + 288 * 63);
@@ -65,7 +66,7 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_horner_miller(int ng, const
   fp12_to_canon_bytes(out576 + 576 * (size_t)item, r);
 }
 
-static int row_blocks(int n) { return (n * 16 + LSG_ROW_TPB - 1) / LSG_ROW_TPB; }
+static int row_blocks(int n) { return (n * 16 * LSG_ROWS_PER_ITEM + LSG_ROW_TPB - 1) / LSG_ROW_TPB; }
 
 hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   if (ng <= 0) return hipSuccess;

@@ -133,6 +133,12 @@ LSG_INL fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& k) {
 // (fp_mul9 is one call with nine dependency chains in flight; the tail uses mul3/mul2/mul)
 template <int N>
 LSG_INL void fp_mul_list(fp_t* r, const fp_t* x, const fp_t* y) {
+#ifdef LSG_ROW_SPLIT
+  if (N >= 4) {  // the rows of a wave share one item: split the batch over them
+    fp_mul_list_rows<N>(r, x, y);
+    return;
+  }
+#endif
 #pragma unroll
   for (int g = 0; g + 9 <= N; g += 9) fp_mul9(r + g, x + g, y + g);
   constexpr int T = N % 9, B = N - T;
