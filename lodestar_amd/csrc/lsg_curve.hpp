@@ -177,9 +177,84 @@ LSG_INL proj_t<F> proj_dbl(const proj_t<F>& p) {
 LSG_BIGFN g1p_t g1_add(g1p_t p, g1p_t q) { return proj_add(p, q); }
 LSG_BIGFN g1p_t g1_add_mixed(g1p_t p, g1a_t q) { return proj_add_mixed(p, q); }
 LSG_BIGFN g1p_t g1_dbl(g1p_t p) { return proj_dbl(p); }
+#ifdef LSG_ROW_SPLIT
+// Row backend with the rows of a wave sharing one item (lsg_fp_lane.hpp): the same RCB
+// formulas with their independent Fp2 products issued as batches (two rounds each), so the
+// four rows split them.  Values are fully reduced there: the results are identical.
+// Karatsuba operands of the Fp2 product a b at x/y[k..k+2], and its combination
+LSG_INL void kar_prep(fp_t* x, fp_t* y, int k, const fp2_t& a, const fp2_t& b) {
+  x[k] = a.c0;
+  y[k] = b.c0;
+  x[k + 1] = a.c1;
+  y[k + 1] = b.c1;
+  x[k + 2] = fp_add(a.c0, a.c1);
+  y[k + 2] = fp_add(b.c0, b.c1);
+}
+LSG_INL fp2_t kar_fin(const fp_t* z, int k) {
+  return fp2_t(fp_sub(z[k], z[k + 1]), fp_sub(fp_sub(z[k + 2], z[k]), z[k + 1]));
+}
+// RCB 2016 algorithm 7 (a = 0): round 1 the six cross products, round 2 the six outputs
+LSG_INL g2p_t g2_add_rows(const g2p_t& p, const g2p_t& q) {
+  fp_t x[18], y[18], z[18];
+  kar_prep(x, y, 0, p.X, q.X);
+  kar_prep(x, y, 3, p.Y, q.Y);
+  kar_prep(x, y, 6, p.Z, q.Z);
+  kar_prep(x, y, 9, fp2_add(p.X, p.Y), fp2_add(q.X, q.Y));
+  kar_prep(x, y, 12, fp2_add(p.Y, p.Z), fp2_add(q.Y, q.Z));
+  kar_prep(x, y, 15, fp2_add(p.X, p.Z), fp2_add(q.X, q.Z));
+  fp_mul_list<18>(z, x, y);
+  fp2_t t0 = kar_fin(z, 0), t1 = kar_fin(z, 3), t2 = kar_fin(z, 6);
+  const fp2_t t3 = fp2_sub(kar_fin(z, 9), fp2_add(t0, t1));
+  const fp2_t t4 = fp2_sub(kar_fin(z, 12), fp2_add(t1, t2));
+  fp2_t Y3 = fp2_sub(kar_fin(z, 15), fp2_add(t0, t2));
+  t0 = fp2_add(fp2_add(t0, t0), t0);
+  t2 = fp2_mul_b3(t2);
+  const fp2_t Z3 = fp2_add(t1, t2);
+  t1 = fp2_sub(t1, t2);
+  Y3 = fp2_mul_b3(Y3);
+  kar_prep(x, y, 0, t4, Y3);
+  kar_prep(x, y, 3, t3, t1);
+  kar_prep(x, y, 6, Y3, t0);
+  kar_prep(x, y, 9, t1, Z3);
+  kar_prep(x, y, 12, t0, t3);
+  kar_prep(x, y, 15, Z3, t4);
+  fp_mul_list<18>(z, x, y);
+  g2p_t r;
+  r.X = fp2_sub(kar_fin(z, 3), kar_fin(z, 0));
+  r.Y = fp2_add(kar_fin(z, 9), kar_fin(z, 6));
+  r.Z = fp2_add(kar_fin(z, 15), kar_fin(z, 12));
+  return r;
+}
+// RCB 2016 algorithm 9 (a = 0): round 1 Y^2, YZ, Z^2, XY; round 2 the four outputs
+LSG_INL g2p_t g2_dbl_rows(const g2p_t& p) {
+  fp_t x[12], y[12], z[12];
+  kar_prep(x, y, 0, p.Y, p.Y);
+  kar_prep(x, y, 3, p.Y, p.Z);
+  kar_prep(x, y, 6, p.Z, p.Z);
+  kar_prep(x, y, 9, p.X, p.Y);
+  fp_mul_list<12>(z, x, y);
+  const fp2_t t0 = kar_fin(z, 0), t1 = kar_fin(z, 3), t2 = fp2_mul_b3(kar_fin(z, 6)), xy = kar_fin(z, 9);
+  const fp2_t z8 = fp2_dbl(fp2_dbl(fp2_dbl(t0)));
+  const fp2_t y3 = fp2_add(t0, t2);
+  const fp2_t s0 = fp2_sub(t0, fp2_add(fp2_add(t2, t2), t2));
+  kar_prep(x, y, 0, t2, z8);
+  kar_prep(x, y, 3, t1, z8);
+  kar_prep(x, y, 6, s0, y3);
+  kar_prep(x, y, 9, s0, xy);
+  fp_mul_list<12>(z, x, y);
+  g2p_t r;
+  r.X = fp2_dbl(kar_fin(z, 9));
+  r.Y = fp2_add(kar_fin(z, 0), kar_fin(z, 6));
+  r.Z = kar_fin(z, 3);
+  return r;
+}
+LSG_BIGFN g2p_t g2_add(g2p_t p, g2p_t q) { return g2_add_rows(p, q); }
+LSG_BIGFN g2p_t g2_dbl(g2p_t p) { return g2_dbl_rows(p); }
+#else
 LSG_BIGFN g2p_t g2_add(g2p_t p, g2p_t q) { return proj_add(p, q); }
-LSG_BIGFN g2p_t g2_add_mixed(g2p_t p, g2a_t q) { return proj_add_mixed(p, q); }
 LSG_BIGFN g2p_t g2_dbl(g2p_t p) { return proj_dbl(p); }
+#endif
+LSG_BIGFN g2p_t g2_add_mixed(g2p_t p, g2a_t q) { return proj_add_mixed(p, q); }
 
 LSG_INL g1p_t gadd(const g1p_t& p, const g1p_t& q) { return g1_add(p, q); }
 LSG_INL g2p_t gadd(const g2p_t& p, const g2p_t& q) { return g2_add(p, q); }

@@ -74,6 +74,92 @@ LSG_INL line_t line_eval(line_t L, const fp_t& xP, const fp_t& yP) {
   return L;
 }
 
+#ifdef LSG_ROW_SPLIT
+// Rows of a wave sharing one item (lsg_fp_lane.hpp): the steps above with their independent
+// products issued as batches for the rows to split (identical values: the row backend keeps
+// every value fully reduced).  Doubling: round 1 Y^2, YZ, Z^2, X^2, XY; round 2 the point's
+// four products and the line evaluation at P.
+LSG_INL line_t ml_dbl_step_rows(g2p_t& T, const fp_t& xP, const fp_t& yP) {
+  fp_t x[16], y[16], z[16];
+  kar_prep(x, y, 0, T.Y, T.Y);
+  kar_prep(x, y, 3, T.Y, T.Z);
+  kar_prep(x, y, 6, T.Z, T.Z);
+  kar_prep(x, y, 9, T.X, T.X);
+  kar_prep(x, y, 12, T.X, T.Y);
+  fp_mul_list<15>(z, x, y);
+  const fp2_t t0 = kar_fin(z, 0), t1 = kar_fin(z, 3), t2 = fp2_mul_b3(kar_fin(z, 6)), XX = kar_fin(z, 9),
+              v1 = kar_fin(z, 12);
+  line_t L;
+  L.l00 = fp2_sub(t2, t0);
+  const fp2_t l01 = fp2_add(fp2_add(XX, XX), XX), l11 = fp2_neg(fp2_add(t1, t1));
+  const fp2_t z8 = fp2_dbl(fp2_dbl(fp2_dbl(t0)));
+  const fp2_t y3 = fp2_add(t0, t2);
+  const fp2_t s0 = fp2_sub(t0, fp2_add(fp2_add(t2, t2), t2));
+  kar_prep(x, y, 0, t2, z8);
+  kar_prep(x, y, 3, t1, z8);
+  kar_prep(x, y, 6, s0, y3);
+  kar_prep(x, y, 9, s0, v1);
+  x[12] = l01.c0;
+  y[12] = xP;
+  x[13] = l01.c1;
+  y[13] = xP;
+  x[14] = l11.c0;
+  y[14] = yP;
+  x[15] = l11.c1;
+  y[15] = yP;
+  fp_mul_list<16>(z, x, y);
+  const fp2_t X3 = kar_fin(z, 0);
+  T.X = fp2_dbl(kar_fin(z, 9));
+  T.Y = fp2_add(X3, kar_fin(z, 6));
+  T.Z = kar_fin(z, 3);
+  L.l01 = fp2_t(z[12], z[13]);
+  L.l11 = fp2_t(z[14], z[15]);
+  return L;
+}
+// Addition: four rounds (Q Z; the line and C, D; E, F, G and the evaluation; the outputs)
+LSG_INL line_t ml_add_step_rows(g2p_t& T, const g2a_t& Q, const fp_t& xP, const fp_t& yP) {
+  fp_t x[13], y[13], z[13];
+  kar_prep(x, y, 0, Q.y, T.Z);
+  kar_prep(x, y, 3, Q.x, T.Z);
+  fp_mul_list<6>(z, x, y);
+  const fp2_t theta = fp2_sub(T.Y, kar_fin(z, 0)), delta = fp2_sub(T.X, kar_fin(z, 3));
+  kar_prep(x, y, 0, delta, Q.y);
+  kar_prep(x, y, 3, theta, Q.x);
+  kar_prep(x, y, 6, theta, theta);
+  kar_prep(x, y, 9, delta, delta);
+  fp_mul_list<12>(z, x, y);
+  line_t L;
+  L.l00 = fp2_sub(kar_fin(z, 0), kar_fin(z, 3));
+  const fp2_t C = kar_fin(z, 6), D = kar_fin(z, 9), l11 = fp2_neg(delta);
+  kar_prep(x, y, 0, D, delta);
+  kar_prep(x, y, 3, T.Z, C);
+  kar_prep(x, y, 6, T.X, D);
+  x[9] = theta.c0;
+  y[9] = xP;
+  x[10] = theta.c1;
+  y[10] = xP;
+  x[11] = l11.c0;
+  y[11] = yP;
+  x[12] = l11.c1;
+  y[12] = yP;
+  fp_mul_list<13>(z, x, y);
+  const fp2_t E = kar_fin(z, 0), F = kar_fin(z, 3), G = kar_fin(z, 6);
+  L.l01 = fp2_t(z[9], z[10]);
+  L.l11 = fp2_t(z[11], z[12]);
+  const fp2_t H = fp2_sub(fp2_add(E, F), fp2_add(G, G));
+  kar_prep(x, y, 0, delta, H);
+  kar_prep(x, y, 3, theta, fp2_sub(G, H));
+  kar_prep(x, y, 6, E, T.Y);
+  kar_prep(x, y, 9, E, T.Z);
+  fp_mul_list<12>(z, x, y);
+  T.X = kar_fin(z, 0);
+  T.Y = fp2_sub(kar_fin(z, 3), kar_fin(z, 6));
+  T.Z = kar_fin(z, 9);
+  return L;
+}
+LSG_INL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) { return ml_dbl_step_rows(T, xP, yP); }
+LSG_INL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) { return ml_add_step_rows(T, Q, xP, yP); }
+#else
 // T <- 2T; line = (3b'Z^2 - Y^2, 3X^2 xP, -2YZ yP)
 LSG_INL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) { return line_eval(ml_dbl_step_raw(T), xP, yP); }
 
@@ -81,6 +167,7 @@ LSG_INL line_t ml_dbl_step(g2p_t& T, fp_t xP, fp_t yP) { return line_eval(ml_dbl
 LSG_INL line_t ml_add_step(g2p_t& T, g2a_t Q, fp_t xP, fp_t yP) {
   return line_eval(ml_add_step_raw(T, Q), xP, yP);
 }
+#endif
 
 // f_{|x|,Q}(P) conjugated (x < 0).  P affine G1, Q affine G2, both finite.
 LSG_BIGFN fp12_t miller_loop(g1a_t P, g2a_t Q) {
