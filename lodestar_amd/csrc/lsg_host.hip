@@ -134,13 +134,17 @@ struct SegPlan {
   size_t tmp_items = 0;  // per tmp buffer
 };
 constexpr int SEG_FOLD = 16;  // at most this many serial folds per lane pair within one pass
+// Fp12 products (op 2) cost ~50 us each on one lane pair: their passes fold at most 4 terms
+// per pair before the butterfly (an 8193-term package product: 17 serial products in two
+// passes instead of 28)
+constexpr int SEG_FOLD_FP12 = 4;
 
 // lane pairs per chunk (log2): enough that the longest segment fits one chunk of SEG_FOLD
 // folds per pair (one pass), and at least a quarter of the mean length (latency: folds are
 // serial, the butterfly is log2(ips) steps); at most a wave's 32 pairs
-int ips_for(double avg, int32_t max_len) {
+int ips_for(double avg, int32_t max_len, int fold) {
   int l = 0;
-  while (l < 5 && ((int32_t)(SEG_FOLD << l) < max_len || (double)(2 << l) * 4.0 <= avg)) l++;
+  while (l < 5 && ((int32_t)(fold << l) < max_len || (double)(2 << l) * 4.0 <= avg)) l++;
   return l;
 }
 
@@ -168,10 +172,11 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
     SegPass pass;
     int32_t max_len = 0;
     for (const Pend& p : cur) max_len = std::max(max_len, p.len);
-    pass.ips_log2 = ips_for(avg, max_len);
+    const int fold = op == 2 ? SEG_FOLD_FP12 : SEG_FOLD;
+    pass.ips_log2 = ips_for(avg, max_len, fold);
     pass.src = src;
     pass.tmp_out = tmp_out;
-    const int32_t cap = (int32_t)((1 << pass.ips_log2) * SEG_FOLD);
+    const int32_t cap = (int32_t)((1 << pass.ips_log2) * fold);
     pass.chunk_off = A.size();
     std::vector<Pend> nxt;
     int32_t t = 0;
