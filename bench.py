@@ -256,7 +256,7 @@ def main():
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     args = ap.parse_args()
     if args.depth is None:
-        args.depth = {"jobs": 4, "adversarial": 4, "block": 4, "sync": 6, "gossip": 8}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 6, "gossip": 8}[args.workload]
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
         args.packages = 2 if args.workload == "block" else args.depth + 1
 
