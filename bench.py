@@ -428,7 +428,7 @@ def main():
     accum_key = f"miller_accum{mk}_per_set" if f"miller_accum{mk}_per_set" in opc["stage_fp_muls"] \
         else "miller_accum2_per_set"
     stage_of = {"k_miller_accum": [accum_key], "k_miller_lines": ["miller_lines"],
-                "k_miller_fused": ["miller_lines", "miller_accum4_per_set"], "k_sig_subgroup": ["sig_subgroup"],
+                "k_miller_fused": ["miller_fused_per_set"], "k_sig_subgroup": ["sig_subgroup"],
                 "k_sig_decode": ["sig_decode"], "k_pk_scale": ["pk_scale"], "k_h2c_map": ["hash_map"]}
     per_set = {k: v for k, v in agg.items() if k in stage_of and k != "k_h2c_map"}
     dom = max(per_set, key=per_set.get)
@@ -450,7 +450,10 @@ def main():
         per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / group
     else:
         per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / group
-    per_set_muls += opc["stage_fp_muls"][accum_key] - opc["stage_fp_muls"]["miller_accum2_per_set"]
+    fused = os.environ.get("LSG_MILLER_FUSED", "1") != "0"
+    sf = opc["stage_fp_muls"]
+    per_set_muls += (sf["miller_fused_per_set"] if fused else sf["miller_lines"] + sf[accum_key]) \
+        - sf["miller_multi2_per_set"]
     per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:

@@ -71,24 +71,28 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
 // staged in LDS"), the Fp12 accumulator of each item shared by four waves.
 //
 // A workgroup is 4 waves and owns 32 items of <= 4 sets (MF_ITEMS).  Lane pair q of every
-// wave works on item q; wave w is "pair w" of its item:
-//   L phase   wave w advances its set's G2 point T (doubling or addition step), evaluates the
-//             line at its P and writes it to LDS (the identity line (1, 0, 0) for a set that
-//             does not contribute) -- the four lines of an item come out in parallel;
+// wave works on item q; wave w is "pair w" of its item and keeps that pair's G2 point T in
+// registers:
+//   L phase   wave w advances T (doubling or addition step), evaluates the line at its P and
+//             writes it to LDS (the identity line (1, 0, 0) for a set that does not
+//             contribute) -- the four lines of an item come out in parallel;
+//   P phase   the lines are multiplied in pairs, M01 = l0 l1 and M23 = l2 l3 (sparse x sparse:
+//             6 Fp2 products each, three per wave), into the slots of the lines;
 //   S phase   f <- f^2: the 12 Fp2 products of (a + b w)^2 = (u - t - v t) + 2t w,
 //             t = a b, u = (a + b)(a + v b), three per wave, then the six output
 //             coefficients combined by the waves in parallel;
-//   M phase   f <- f * line_k for k = 0..3: the 13 Fp2 products of fp12_mul_line split 4/3/3/3
-//             over the waves, then the six output coefficients.
-// f, the lines, the products and the G2 points live in LDS only (154 KB per workgroup), so a set's HBM
-// traffic is its inputs (Q, P, flags) and 1/4 of its item's f: no line round trip.  The
-// operation order differs from miller_accum_multi (every product is issued as an Fp2
-// product of the same Karatsuba form), the field element is the same: the host-checked
-// split loop and the GPU parity tests pin it.
+//   M phase   f <- f * M for M = M01, M23: 17 Fp2 products (Karatsuba over Fp6 with the
+//             second half of M sparse) split 5/4/4/4, then the six output coefficients.
+// Per doubling that is 12 + 12 + 34 Fp2 products in phases of 3, 3, 5 and 5 per wave, where
+// four line multiplications (13 products each, split 4/3/3/3) were 12 + 52 in phases of 3 and
+// 4 x 4.  f, the lines and the products live in LDS only (125 KB per workgroup), so a set's
+// HBM traffic is its inputs (Q, P, flags) and 1/4 of its item's f: no line round trip.  The
+// operation order differs from miller_accum_multi, the field element is the same: the
+// host-checked split loop and the GPU parity tests pin it.
 constexpr int MF_ITEMS = 32;
-// LDS components (one Fp of 32 items each): f, the four lines, the products, the four G2 points T
-constexpr int MF_F = 0, MF_L = 12, MF_V = 36, MF_T = 62, MF_COMPS = 86;
-constexpr size_t MF_LDS_BYTES = (size_t)MF_COMPS * 7 * 64 * 4;  // 154,112 B: one workgroup per CU
+// LDS components (one Fp of 32 items each): f, the four lines (then M01, M23), the products
+constexpr int MF_F = 0, MF_L = 12, MF_V = 36, MF_COMPS = 70;
+constexpr size_t MF_LDS_BYTES = (size_t)MF_COMPS * 7 * 64 * 4;  // 125,440 B: one workgroup per CU
 
 LSG_DEVI uint32_t* mf_slot(uint32_t* lds, int c) { return lds + (size_t)c * 7 * 64 + (threadIdx.x & 63); }
 LSG_DEVI void mf_put(uint32_t* lds, int c, const fp_t& v) {
@@ -173,65 +177,125 @@ LSG_DEVI void mf_sqr(uint32_t* lds, int w) {
   __syncthreads();
 }
 
-// f <- f * line_k (M phase): fp12_mul_line's 13 Fp2 products (lsg_tower.hpp), with a = f.c0,
-// b = f.c1, s = a + b, m = l01 + l11:
-//   P0 a0 l00  P1 a1 l01  P2 a2 l01  P3 (a0+a1)(l00+l01)  P4 a2 l00          (t0 = a (l00, l01))
-//   P5 s0 l00  P6 s1 m    P7 s2 m    P8 (s0+s1)(l00+m)    P9 s2 l00          (u = s (l00, m))
-//   P10 b2 l11 P11 b0 l11 P12 b1 l11                                         (t1 = b (l11 v))
-// new f: c0 = t0 + v t1, c1 = u - t0 - t1, i.e.
-//   c0.c0 = P0 + xi (P2 + P12)        c1.c0 = P5 - P0 + xi (P7 - P2 - P10)
-//   c0.c1 = P3 - P0 - P1 + xi P10     c1.1  = P8 - P5 - P6 - P3 + P0 + P1 - P11
-//   c0.c2 = P4 + P1 + P11             c1.2  = P9 + P6 - P4 - P1 - P12
-LSG_DEVI void mf_mul_line(uint32_t* lds, int w, int k) {
+// P phase: M01 = l0 l1 into the slots of lines 0 and 1, M23 = l2 l3 into those of 2 and 3.
+// For lines l = (l00 + l01 v) + (l11 v) w:  l l' = (m0 + m1 v + m2 v^2) + (m4 v + m5 v^2) w,
+//   m0 = P0 + xi P1, m1 = P3 - P0 - P2, m2 = P2, m4 = P4 - P0 - P1, m5 = P5 - P2 - P1, with
+//   P0 = l00 l00', P1 = l11 l11', P2 = l01 l01', P3 = (l00 + l01)(l00' + l01'),
+//   P4 = (l00 + l11)(l00' + l11'), P5 = (l01 + l11)(l01' + l11').
+// Waves 2pi and 2pi + 1 work on pair pi: three products each, then m0..m2 / m4, m5.
+LSG_DEVI void mf_pair_lines(uint32_t* lds, int w) {
+  const int pi = w >> 1, h = w & 1;
   {
-    const fp2_t l00 = mf_get2(lds, MF_LC(k, 0)), l01 = mf_get2(lds, MF_LC(k, 1)), l11 = mf_get2(lds, MF_LC(k, 2));
+    const fp2_t a0 = mf_get2(lds, MF_LC(2 * pi, 0)), a1 = mf_get2(lds, MF_LC(2 * pi, 1)),
+                a2 = mf_get2(lds, MF_LC(2 * pi, 2));
+    const fp2_t b0 = mf_get2(lds, MF_LC(2 * pi + 1, 0)), b1 = mf_get2(lds, MF_LC(2 * pi + 1, 1)),
+                b2 = mf_get2(lds, MF_LC(2 * pi + 1, 2));
+    if (h == 0) {
+      mf_put2(lds, MF_VC(6 * pi), fp2_mul(a0, b0));
+      mf_put2(lds, MF_VC(6 * pi + 1), fp2_mul(a2, b2));
+      mf_put2(lds, MF_VC(6 * pi + 2), fp2_mul(a1, b1));
+    } else {
+      mf_put2(lds, MF_VC(6 * pi + 3), fp2_mul(fp2_add(a0, a1), fp2_add(b0, b1)));
+      mf_put2(lds, MF_VC(6 * pi + 4), fp2_mul(fp2_add(a0, a2), fp2_add(b0, b2)));
+      mf_put2(lds, MF_VC(6 * pi + 5), fp2_mul(fp2_add(a1, a2), fp2_add(b1, b2)));
+    }
+  }
+  __syncthreads();
+  // the lines of pair pi were read before the barrier: their slots take M
+  const fp2_t P0 = mf_get2(lds, MF_VC(6 * pi)), P1 = mf_get2(lds, MF_VC(6 * pi + 1)), P2 = mf_get2(lds, MF_VC(6 * pi + 2));
+  if (h == 0) {
+    mf_put2(lds, MF_LC(2 * pi, 0), fp2_add(P0, fp2_mul_xi(P1)));
+    mf_put2(lds, MF_LC(2 * pi, 1), fp2_sub(fp2_sub(mf_get2(lds, MF_VC(6 * pi + 3)), P0), P2));
+    mf_put2(lds, MF_LC(2 * pi, 2), P2);
+  } else {
+    mf_put2(lds, MF_LC(2 * pi + 1, 0), fp2_sub(fp2_sub(mf_get2(lds, MF_VC(6 * pi + 4)), P0), P1));
+    mf_put2(lds, MF_LC(2 * pi + 1, 1), fp2_sub(fp2_sub(mf_get2(lds, MF_VC(6 * pi + 5)), P2), P1));
+  }
+  __syncthreads();
+}
+
+// M phase: f <- f * M for M = (m0, m1, m2) + (0, m4, m5) w in the slots of lines 2k, 2k + 1.
+// f = a + b w:  t0 = a M0 (6 products), t1 = b M1 = v n with n = b (m4 + m5 v) (5),
+// t2 = (a + b)(M0 + M1) (6);  f' = (t0 + v t1) + (t2 - t0 - t1) w.
+//   V0 a0 m0   V1 a1 m1   V2 a2 m2   V3 (a0+a1)(m0+m1)   V4 (a1+a2)(m1+m2)   V5 (a0+a2)(m0+m2)
+//   V6 b0 m4   V7 b1 m5   V8 (b0+b1)(m4+m5)   V9 b2 m4   V10 b2 m5
+//   V11 s0 q0  V12 s1 q1  V13 s2 q2  V14 (s0+s1)(q0+q1)  V15 (s1+s2)(q1+q2)  V16 (s0+s2)(q0+q2)
+//   with s = a + b, q = (m0, m1 + m4, m2 + m5); split 5/4/4/4 over the waves.
+LSG_DEVI void mf_mul_pair(uint32_t* lds, int w, int k) {
+  {
+    const fp2_t m0 = mf_get2(lds, MF_LC(2 * k, 0)), m1 = mf_get2(lds, MF_LC(2 * k, 1)), m2 = mf_get2(lds, MF_LC(2 * k, 2));
     if (w == 0) {
       const fp2_t a0 = mf_get2(lds, MF_FC(0)), a1 = mf_get2(lds, MF_FC(1)), a2 = mf_get2(lds, MF_FC(2));
-      mf_put2(lds, MF_VC(0), fp2_mul(a0, l00));
-      mf_put2(lds, MF_VC(1), fp2_mul(a1, l01));
-      mf_put2(lds, MF_VC(2), fp2_mul(a2, l01));
-      mf_put2(lds, MF_VC(3), fp2_mul(fp2_add(a0, a1), fp2_add(l00, l01)));
+      mf_put2(lds, MF_VC(0), fp2_mul(a0, m0));
+      mf_put2(lds, MF_VC(1), fp2_mul(a1, m1));
+      mf_put2(lds, MF_VC(2), fp2_mul(a2, m2));
+      mf_put2(lds, MF_VC(3), fp2_mul(fp2_add(a0, a1), fp2_add(m0, m1)));
+      mf_put2(lds, MF_VC(4), fp2_mul(fp2_add(a1, a2), fp2_add(m1, m2)));
     } else if (w == 1) {
-      const fp2_t a2 = mf_get2(lds, MF_FC(2));
+      const fp2_t m4 = mf_get2(lds, MF_LC(2 * k + 1, 0)), m5 = mf_get2(lds, MF_LC(2 * k + 1, 1));
+      const fp2_t b0 = mf_get2(lds, MF_FC(3)), b1 = mf_get2(lds, MF_FC(4));
+      mf_put2(lds, MF_VC(5), fp2_mul(fp2_add(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(2))), fp2_add(m0, m2)));
+      mf_put2(lds, MF_VC(6), fp2_mul(b0, m4));
+      mf_put2(lds, MF_VC(7), fp2_mul(b1, m5));
+      mf_put2(lds, MF_VC(8), fp2_mul(fp2_add(b0, b1), fp2_add(m4, m5)));
+    } else if (w == 2) {
+      const fp2_t m4 = mf_get2(lds, MF_LC(2 * k + 1, 0)), m5 = mf_get2(lds, MF_LC(2 * k + 1, 1));
+      const fp2_t b2 = mf_get2(lds, MF_FC(5));
+      mf_put2(lds, MF_VC(9), fp2_mul(b2, m4));
+      mf_put2(lds, MF_VC(10), fp2_mul(b2, m5));
       const fp2_t s0 = fp2_add(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(3)));
       const fp2_t s1 = fp2_add(mf_get2(lds, MF_FC(1)), mf_get2(lds, MF_FC(4)));
-      mf_put2(lds, MF_VC(4), fp2_mul(a2, l00));
-      mf_put2(lds, MF_VC(5), fp2_mul(s0, l00));
-      mf_put2(lds, MF_VC(6), fp2_mul(s1, fp2_add(l01, l11)));
-    } else if (w == 2) {
+      mf_put2(lds, MF_VC(11), fp2_mul(s0, m0));
+      mf_put2(lds, MF_VC(12), fp2_mul(s1, fp2_add(m1, m4)));
+    } else {
+      const fp2_t m4 = mf_get2(lds, MF_LC(2 * k + 1, 0)), m5 = mf_get2(lds, MF_LC(2 * k + 1, 1));
       const fp2_t s0 = fp2_add(mf_get2(lds, MF_FC(0)), mf_get2(lds, MF_FC(3)));
       const fp2_t s1 = fp2_add(mf_get2(lds, MF_FC(1)), mf_get2(lds, MF_FC(4)));
       const fp2_t s2 = fp2_add(mf_get2(lds, MF_FC(2)), mf_get2(lds, MF_FC(5)));
-      const fp2_t m = fp2_add(l01, l11);
-      mf_put2(lds, MF_VC(7), fp2_mul(s2, m));
-      mf_put2(lds, MF_VC(8), fp2_mul(fp2_add(s0, s1), fp2_add(l00, m)));
-      mf_put2(lds, MF_VC(9), fp2_mul(s2, l00));
-    } else {
-      mf_put2(lds, MF_VC(10), fp2_mul(mf_get2(lds, MF_FC(5)), l11));
-      mf_put2(lds, MF_VC(11), fp2_mul(mf_get2(lds, MF_FC(3)), l11));
-      mf_put2(lds, MF_VC(12), fp2_mul(mf_get2(lds, MF_FC(4)), l11));
+      const fp2_t q1 = fp2_add(m1, m4), q2 = fp2_add(m2, m5);
+      mf_put2(lds, MF_VC(13), fp2_mul(s2, q2));
+      mf_put2(lds, MF_VC(14), fp2_mul(fp2_add(s0, s1), fp2_add(m0, q1)));
+      mf_put2(lds, MF_VC(15), fp2_mul(fp2_add(s1, s2), fp2_add(q1, q2)));
+      mf_put2(lds, MF_VC(16), fp2_mul(fp2_add(s0, s2), fp2_add(m0, q2)));
     }
   }
   __syncthreads();
   auto V = [&](int p) { return mf_get2(lds, MF_VC(p)); };
+  // t0 = a M0, n = b (m4 + m5 v), t2 = s q (Karatsuba over Fp6, as in mf_sqr)
+  auto t0c = [&](int j) {
+    if (j == 0) return fp2_add(V(0), fp2_mul_xi(fp2_sub(fp2_sub(V(4), V(1)), V(2))));
+    if (j == 1) return fp2_add(fp2_sub(fp2_sub(V(3), V(0)), V(1)), fp2_mul_xi(V(2)));
+    return fp2_add(fp2_sub(fp2_sub(V(5), V(0)), V(2)), V(1));
+  };
+  auto t2c = [&](int j) {
+    if (j == 0) return fp2_add(V(11), fp2_mul_xi(fp2_sub(fp2_sub(V(15), V(12)), V(13))));
+    if (j == 1) return fp2_add(fp2_sub(fp2_sub(V(14), V(11)), V(12)), fp2_mul_xi(V(13)));
+    return fp2_add(fp2_sub(fp2_sub(V(16), V(11)), V(13)), V(12));
+  };
+  auto nc = [&](int j) {
+    if (j == 0) return fp2_add(V(6), fp2_mul_xi(V(10)));
+    if (j == 1) return fp2_sub(fp2_sub(V(8), V(6)), V(7));
+    return fp2_add(V(7), V(9));
+  };
+  // f'.c0 = t0 + v t1 = t0 + (xi n1, xi n2, n0);  f'.c1 = t2 - t0 - t1 = t2 - t0 - (xi n2, n0, n1)
   fp2_t o0, o1;
   int j0, j1 = -1;
-  if (w == 0) {  // c0.c0, c0.c2
-    o0 = fp2_add(V(0), fp2_mul_xi(fp2_add(V(2), V(12))));
-    o1 = fp2_add(fp2_add(V(4), V(1)), V(11));
+  if (w == 0) {  // c0.0, c0.1
+    o0 = fp2_add(t0c(0), fp2_mul_xi(nc(1)));
+    o1 = fp2_add(t0c(1), fp2_mul_xi(nc(2)));
     j0 = 0;
-    j1 = 2;
-  } else if (w == 1) {  // c0.c1
-    o0 = fp2_add(fp2_sub(fp2_sub(V(3), V(0)), V(1)), fp2_mul_xi(V(10)));
-    j0 = 1;
-  } else if (w == 2) {  // c1.c0, c1.c2
-    o0 = fp2_add(fp2_sub(V(5), V(0)), fp2_mul_xi(fp2_sub(fp2_sub(V(7), V(2)), V(10))));
-    o1 = fp2_sub(fp2_sub(fp2_sub(fp2_add(V(9), V(6)), V(4)), V(1)), V(12));
-    j0 = 3;
-    j1 = 5;
-  } else {  // c1.c1
-    o0 = fp2_sub(fp2_add(fp2_add(fp2_sub(fp2_sub(fp2_sub(V(8), V(5)), V(6)), V(3)), V(0)), V(1)), V(11));
+    j1 = 1;
+  } else if (w == 1) {  // c0.2, c1.0
+    o0 = fp2_add(t0c(2), nc(0));
+    o1 = fp2_sub(fp2_sub(t2c(0), t0c(0)), fp2_mul_xi(nc(2)));
+    j0 = 2;
+    j1 = 3;
+  } else if (w == 2) {  // c1.1
+    o0 = fp2_sub(fp2_sub(t2c(1), t0c(1)), nc(0));
     j0 = 4;
+  } else {  // c1.2
+    o0 = fp2_sub(fp2_sub(t2c(2), t0c(2)), nc(1));
+    j0 = 5;
   }
   // f's coefficients are not read in this half: write them at once
   mf_put2(lds, MF_FC(j0), o0);
@@ -257,33 +321,24 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
   const int first = item_first[itc], cnt = item_cnt[itc];
   const int si = first + (w < cnt ? w : cnt - 1);
   const bool use = live && w < cnt && err[si] == 0 && !pinf[si] && !hinf[si];
-  // nothing stays in registers across the loop: T lives in LDS, Q (addition steps) and P are
-  // re-read from global memory (L2 hits)
-  {
-    const g2p_t T = proj_from_aff(lane_load<g2a_t>(H, (size_t)si));
-    mf_put2(lds, MF_T + 6 * w, T.X);
-    mf_put2(lds, MF_T + 6 * w + 2, T.Y);
-    mf_put2(lds, MF_T + 6 * w + 4, T.Z);
-  }
+  // T (this wave's pair) stays in registers; Q (addition steps) and P are re-read from global
+  // memory (L2 hits)
+  g2p_t T = proj_from_aff(lane_load<g2a_t>(H, (size_t)si));
   auto line_phase = [&](bool add) {
     // w and si re-materialised per phase: hoisted out of the loop, the wave-dependent LDS
     // slot addresses and point pointers were spilled to scratch and reloaded every step
     int wl = w, sl = si;
     asm volatile("" : "+v"(wl), "+v"(sl));
-    g2p_t T;  // this wave's own slots: no other wave touches them
-    T.X = mf_get2(lds, MF_T + 6 * wl);
-    T.Y = mf_get2(lds, MF_T + 6 * wl + 2);
-    T.Z = mf_get2(lds, MF_T + 6 * wl + 4);
     line_t L = add ? ml_add_step_raw(T, lane_load<g2a_t>(H, (size_t)sl)) : ml_dbl_step_raw(T);
-    mf_put2(lds, MF_T + 6 * wl, T.X);
-    mf_put2(lds, MF_T + 6 * wl + 2, T.Y);
-    mf_put2(lds, MF_T + 6 * wl + 4, T.Z);
     const g1a_t Pk = lane_load<g1a_t>(P, (size_t)sl);
     L = line_eval(L, Pk.x, Pk.y);
     mf_put2(lds, MF_LC(wl, 0), fp2_select(use, L.l00, fp2_one()));
     mf_put2(lds, MF_LC(wl, 1), fp2_select(use, L.l01, fp2_zero()));
     mf_put2(lds, MF_LC(wl, 2), fp2_select(use, L.l11, fp2_zero()));
     __syncthreads();
+    mf_pair_lines(lds, wl);
+#pragma unroll 1
+    for (int k = 0; k < 2; k++) mf_mul_pair(lds, wl, k);
   };
   // f = 1 (each wave writes a third of the coefficients' limbs: c0.c0 = 1, the rest 0)
   if (w < 2) {
@@ -293,22 +348,12 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
   }
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
   line_phase(false);  // the first doubling
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
-  line_phase(true);  // bit 62 of |x|
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
+  line_phase(true);   // bit 62 of |x|
 #pragma unroll 1
   for (int b = 61; b >= 0; b--) {
     mf_sqr(lds, w);
     line_phase(false);
-#pragma unroll 1
-    for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
-    if ((xa >> b) & 1u) {
-      line_phase(true);
-#pragma unroll 1
-      for (int k = 0; k < 4; k++) mf_mul_line(lds, w, k);
-    }
+    if ((xa >> b) & 1u) line_phase(true);
   }
   // f_item = conj(f): wave w stores Fp components 3w..3w+2 (components 6..11 negated)
   if (live) {

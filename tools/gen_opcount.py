@@ -24,8 +24,18 @@ def main():
     counts = (ctypes.c_ulonglong * len(NAMES))()
     lib.hc_opcount(sig, pks[0], m, 0xF00DCAFE12345678, counts)
     c = {n: int(counts[i]) for i, n in enumerate(NAMES)}
+    # k_miller_fused (lsg_k_miller.hip): items of four pairs; per item the first doubling and
+    # bit 62 (P and M phases: 12 + 34 Fp2 products each), 62 further doublings (S, P, M: 12 +
+    # 12 + 34) and the additions for the other set bits of |x| (46 each); per set its 68 line
+    # steps (miller_lines) and their evaluations at P (two Fp2 x Fp products, 4 Fp products)
+    xabs = 0xD201000000010000
+    adds = bin(xabs & ((1 << 62) - 1)).count("1")
+    fp2_products_per_item = 2 * 46 + 62 * 58 + adds * 46
+    c["miller_fused_per_set"] = c["miller_lines"] + 68 * 4 + 3 * fp2_products_per_item // 4
     # device path: multi-Miller items of K = 2 pairs (shared squarings), so per set the Miller
     # stage costs miller_multi2_per_set; one Fp12 product per item in the product tree
+    # (the default Miller kernel is k_miller_fused: bench.py swaps miller_multi2_per_set for
+    # miller_fused_per_set)
     per_set = (c["sig_decode"] + c["sig_subgroup"] + c["pk_decode"] + c["pk_scale"] + c["hash_map"] + c["sig_scale"]
                + c["miller_multi2_per_set"] + c["g2_add"] + c["fp12_mul"] // 2)
     per_batch = c["miller"] + c["fp12_mul"] + c["final_exp"]  # group sig term + product + FE

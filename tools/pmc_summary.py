@@ -85,7 +85,7 @@ def main():
     opc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))
     mk = os.environ.get("LSG_MILLER_K", "4")
     stage = {"k_miller_accum<4>": [f"miller_accum{mk}_per_set"], "k_miller_lines": ["miller_lines"],
-             "k_miller_fused": ["miller_lines", "miller_accum4_per_set"],
+             "k_miller_fused": ["miller_fused_per_set"],
              "k_sig_subgroup": ["sig_subgroup"], "k_sig_decode": ["sig_decode"], "k_pk_scale": ["pk_scale"]}
     rows, traffic = {}, {}
     for k in sorted(set(dur) | set(cnt), key=lambda x: -dur.get(x, {}).get("avg_ns", 0)):
