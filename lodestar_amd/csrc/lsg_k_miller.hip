@@ -72,7 +72,7 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
 //
 // A workgroup is 4 waves and owns 32 items of <= 4 sets (MF_ITEMS).  Lane pair q of every
 // wave works on item q; wave w is "pair w" of its item and keeps that pair's G2 point T in
-// registers:
+// LDS:
 //   L phase   wave w advances T (doubling or addition step), evaluates the line at its P and
 //             writes it to LDS (the identity line (1, 0, 0) for a set that does not
 //             contribute) -- the four lines of an item come out in parallel;
@@ -85,14 +85,16 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
 //             second half of M sparse) split 5/4/4/4, then the six output coefficients.
 // Per doubling that is 12 + 12 + 34 Fp2 products in phases of 3, 3, 5 and 5 per wave, where
 // four line multiplications (13 products each, split 4/3/3/3) were 12 + 52 in phases of 3 and
-// 4 x 4.  f, the lines and the products live in LDS only (125 KB per workgroup), so a set's
+// 4 x 4.  f, the lines, the products and the points live in LDS only (158 KB per workgroup), so a set's
 // HBM traffic is its inputs (Q, P, flags) and 1/4 of its item's f: no line round trip.  The
 // operation order differs from miller_accum_multi, the field element is the same: the
 // host-checked split loop and the GPU parity tests pin it.
 constexpr int MF_ITEMS = 32;
-// LDS components (one Fp of 32 items each): f, the four lines (then M01, M23), the products
-constexpr int MF_F = 0, MF_L = 12, MF_V = 36, MF_COMPS = 70;
-constexpr size_t MF_LDS_BYTES = (size_t)MF_COMPS * 7 * 64 * 4;  // 125,440 B: one workgroup per CU
+// LDS components (one Fp of 32 items each): f, the four lines (then M01, M23), the products,
+// the four G2 points T.  Products V15 and V16 of the M phase use the third coefficient slots of
+// lines 1 and 3, which M01 and M23 leave free, so that everything fits 160 KB.
+constexpr int MF_F = 0, MF_L = 12, MF_V = 36, MF_T = 66, MF_COMPS = 90;
+constexpr size_t MF_LDS_BYTES = (size_t)MF_COMPS * 7 * 64 * 4;  // 161,280 B: one workgroup per CU
 
 LSG_DEVI uint32_t* mf_slot(uint32_t* lds, int c) { return lds + (size_t)c * 7 * 64 + (threadIdx.x & 63); }
 LSG_DEVI void mf_put(uint32_t* lds, int c, const fp_t& v) {
@@ -114,8 +116,8 @@ LSG_DEVI void mf_put2(uint32_t* lds, int c, const fp2_t& v) {
 LSG_DEVI fp2_t mf_get2(uint32_t* lds, int c) { return fp2_t(mf_get(lds, c), mf_get(lds, c + 1)); }
 // Fp2 coefficient j (0..5: c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2) of f, product p, line k
 #define MF_FC(j) (MF_F + 2 * (j))
-#define MF_VC(p) (MF_V + 2 * (p))
 #define MF_LC(k, j) (MF_L + 6 * (k) + 2 * (j))
+#define MF_VC(p) ((p) < 15 ? MF_V + 2 * (p) : ((p) == 15 ? MF_LC(1, 2) : MF_LC(3, 2)))
 
 // f <- f^2 (S phase).  V0..5: t = a b (v0, v1, v2, m0, m1, m2 of the Karatsuba Fp6 product),
 // V6..11: u = (a + b)(a + v b).
@@ -321,15 +323,27 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
   const int first = item_first[itc], cnt = item_cnt[itc];
   const int si = first + (w < cnt ? w : cnt - 1);
   const bool use = live && w < cnt && err[si] == 0 && !pinf[si] && !hinf[si];
-  // T (this wave's pair) stays in registers; Q (addition steps) and P are re-read from global
-  // memory (L2 hits)
-  g2p_t T = proj_from_aff(lane_load<g2a_t>(H, (size_t)si));
+  // nothing stays in registers across the loop: T lives in LDS, Q (addition steps) and P are
+  // re-read from global memory (L2 hits)
+  {
+    const g2p_t T = proj_from_aff(lane_load<g2a_t>(H, (size_t)si));
+    mf_put2(lds, MF_T + 6 * w, T.X);
+    mf_put2(lds, MF_T + 6 * w + 2, T.Y);
+    mf_put2(lds, MF_T + 6 * w + 4, T.Z);
+  }
   auto line_phase = [&](bool add) {
     // w and si re-materialised per phase: hoisted out of the loop, the wave-dependent LDS
     // slot addresses and point pointers were spilled to scratch and reloaded every step
     int wl = w, sl = si;
     asm volatile("" : "+v"(wl), "+v"(sl));
+    g2p_t T;  // this wave's own slots: no other wave touches them
+    T.X = mf_get2(lds, MF_T + 6 * wl);
+    T.Y = mf_get2(lds, MF_T + 6 * wl + 2);
+    T.Z = mf_get2(lds, MF_T + 6 * wl + 4);
     line_t L = add ? ml_add_step_raw(T, lane_load<g2a_t>(H, (size_t)sl)) : ml_dbl_step_raw(T);
+    mf_put2(lds, MF_T + 6 * wl, T.X);
+    mf_put2(lds, MF_T + 6 * wl + 2, T.Y);
+    mf_put2(lds, MF_T + 6 * wl + 4, T.Z);
     const g1a_t Pk = lane_load<g1a_t>(P, (size_t)sl);
     L = line_eval(L, Pk.x, Pk.y);
     mf_put2(lds, MF_LC(wl, 0), fp2_select(use, L.l00, fp2_one()));

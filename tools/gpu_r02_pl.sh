@@ -20,3 +20,9 @@ for v in new old; do
   LSG_LIB=$lib timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES --kernel-trace --output-format csv -d gpurun_out/pl_pmc_$v -o run -- python3 bench.py --steps 4 --warmup 2 --depth 1 --no-cpu-baseline > gpurun_out/pl_pmc_$v.log 2>&1 || exit 1
   echo PMC_$v
 done
+for v in new old; do
+  lib=lodestar_amd/liblodestar_bls.so; [ $v = old ] && lib=lodestar_amd/liblodestar_bls_old.so
+  LSG_LIB=$lib timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/plt_f_$v -o run -- python3 bench.py --steps 4 --warmup 2 --depth 1 --no-cpu-baseline > gpurun_out/plt_f_$v.log 2>&1 || exit 1
+  LSG_LIB=$lib timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/plt_w_$v -o run -- python3 bench.py --steps 4 --warmup 2 --depth 1 --no-cpu-baseline > gpurun_out/plt_w_$v.log 2>&1 || exit 1
+  echo TRAFFIC_$v
+done
