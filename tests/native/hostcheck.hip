@@ -168,6 +168,85 @@ void hc_miller_split4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t
   wr12(out576, miller_accum_multi<4>(P, use, [&](int k, int st) { return lines[k][st]; }));
 }
 
+// The fused kernel's schedule (lsg_k_miller.hip k_miller_fused) restated on the host with
+// the same formulas: per step the four lines, multiplied in pairs (P phase), then f^2 on
+// doublings after the first two steps (S phase) and f * M01 * M23 (M phase).
+struct pair_m_t {
+  fp2_t m0, m1, m2, m4, m5;  // (m0 + m1 v + m2 v^2) + (m4 v + m5 v^2) w
+};
+static pair_m_t hc_pair_lines(const line_t& a, const line_t& b) {
+  const fp2_t P0 = fp2_mul(a.l00, b.l00), P1 = fp2_mul(a.l11, b.l11), P2 = fp2_mul(a.l01, b.l01);
+  const fp2_t P3 = fp2_mul(fp2_add(a.l00, a.l01), fp2_add(b.l00, b.l01));
+  const fp2_t P4 = fp2_mul(fp2_add(a.l00, a.l11), fp2_add(b.l00, b.l11));
+  const fp2_t P5 = fp2_mul(fp2_add(a.l01, a.l11), fp2_add(b.l01, b.l11));
+  pair_m_t m;
+  m.m0 = fp2_add(P0, fp2_mul_xi(P1));
+  m.m1 = fp2_sub(fp2_sub(P3, P0), P2);
+  m.m2 = P2;
+  m.m4 = fp2_sub(fp2_sub(P4, P0), P1);
+  m.m5 = fp2_sub(fp2_sub(P5, P2), P1);
+  return m;
+}
+static fp12_t hc_mul_pair(const fp12_t& f, const pair_m_t& M) {
+  const fp6_t& a = f.c0;
+  const fp6_t& b = f.c1;
+  const fp2_t V0 = fp2_mul(a.c0, M.m0), V1 = fp2_mul(a.c1, M.m1), V2 = fp2_mul(a.c2, M.m2);
+  const fp2_t V3 = fp2_mul(fp2_add(a.c0, a.c1), fp2_add(M.m0, M.m1));
+  const fp2_t V4 = fp2_mul(fp2_add(a.c1, a.c2), fp2_add(M.m1, M.m2));
+  const fp2_t V5 = fp2_mul(fp2_add(a.c0, a.c2), fp2_add(M.m0, M.m2));
+  const fp2_t V6 = fp2_mul(b.c0, M.m4), V7 = fp2_mul(b.c1, M.m5), V8 = fp2_mul(fp2_add(b.c0, b.c1), fp2_add(M.m4, M.m5));
+  const fp2_t V9 = fp2_mul(b.c2, M.m4), V10 = fp2_mul(b.c2, M.m5);
+  const fp6_t sv = fp6_add(a, b);
+  const fp2_t q0 = M.m0, q1 = fp2_add(M.m1, M.m4), q2 = fp2_add(M.m2, M.m5);
+  const fp2_t V11 = fp2_mul(sv.c0, q0), V12 = fp2_mul(sv.c1, q1), V13 = fp2_mul(sv.c2, q2);
+  const fp2_t V14 = fp2_mul(fp2_add(sv.c0, sv.c1), fp2_add(q0, q1));
+  const fp2_t V15 = fp2_mul(fp2_add(sv.c1, sv.c2), fp2_add(q1, q2));
+  const fp2_t V16 = fp2_mul(fp2_add(sv.c0, sv.c2), fp2_add(q0, q2));
+  const fp2_t t0[3] = {fp2_add(V0, fp2_mul_xi(fp2_sub(fp2_sub(V4, V1), V2))),
+                       fp2_add(fp2_sub(fp2_sub(V3, V0), V1), fp2_mul_xi(V2)), fp2_add(fp2_sub(fp2_sub(V5, V0), V2), V1)};
+  const fp2_t t2[3] = {fp2_add(V11, fp2_mul_xi(fp2_sub(fp2_sub(V15, V12), V13))),
+                       fp2_add(fp2_sub(fp2_sub(V14, V11), V12), fp2_mul_xi(V13)),
+                       fp2_add(fp2_sub(fp2_sub(V16, V11), V13), V12)};
+  const fp2_t n[3] = {fp2_add(V6, fp2_mul_xi(V10)), fp2_sub(fp2_sub(V8, V6), V7), fp2_add(V7, V9)};
+  fp12_t r;
+  r.c0 = fp6_make(fp2_add(t0[0], fp2_mul_xi(n[1])), fp2_add(t0[1], fp2_mul_xi(n[2])), fp2_add(t0[2], n[0]));
+  r.c1 = fp6_make(fp2_sub(fp2_sub(t2[0], t0[0]), fp2_mul_xi(n[2])), fp2_sub(fp2_sub(t2[1], t0[1]), n[0]),
+                  fp2_sub(fp2_sub(t2[2], t0[2]), n[1]));
+  return r;
+}
+void hc_miller_paired4(const uint8_t* p96x4, const uint8_t* q192x4, const int32_t* use4, uint8_t* out576) {
+  g1a_t P[4];
+  g2a_t Q[4];
+  g2p_t T[4];
+  bool use[4];
+  for (int k = 0; k < 4; k++) {
+    bool inf;
+    g1_deserialize(P[k], inf, p96x4 + 96 * k, 96);
+    g2_deserialize_uncompressed(Q[k], inf, q192x4 + 192 * k);
+    use[k] = use4[k] != 0;
+    T[k] = proj_from_aff(Q[k]);
+  }
+  fp12_t f = fp12_one();
+  auto step = [&](bool add, bool sqr) {
+    line_t L[4];
+    for (int k = 0; k < 4; k++) {
+      line_t l = line_eval(add ? ml_add_step_raw(T[k], Q[k]) : ml_dbl_step_raw(T[k]), P[k].x, P[k].y);
+      L[k] = use[k] ? l : line_t{fp2_one(), fp2_zero(), fp2_zero()};
+    }
+    const pair_m_t M01 = hc_pair_lines(L[0], L[1]), M23 = hc_pair_lines(L[2], L[3]);
+    if (sqr) f = fp12_sqr(f);
+    f = hc_mul_pair(hc_mul_pair(f, M01), M23);
+  };
+  const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
+  step(false, false);
+  step(true, false);
+  for (int b = 61; b >= 0; b--) {
+    step(false, true);
+    if ((xa >> b) & 1u) step(true, false);
+  }
+  wr12(out576, fp12_conj(f));
+}
+
 // KeyValidate's subgroup test (lsg_curve.hpp:g1_in_group) on a 96-byte uncompressed point
 int hc_g1_in_group(const uint8_t* p96) {
   g1a_t a;

@@ -269,6 +269,26 @@ def test_split_miller_loop_equals_multi_loop(hc):
         assert ub12(o.raw) == exp, use
 
 
+def test_paired_line_miller_schedule(hc):
+    """The fused kernel's schedule (lsg_k_miller.hip k_miller_fused: lines multiplied in pairs,
+    then f * (l0 l1) * (l2 l3) with the kernel's product formulas), restated on the host,
+    gives the product of single Miller loops (oracle/pairing.py:miller_loop_fast); dropped
+    pairs contribute 1."""
+    from oracle.fields import f12_mul, F12_ONE
+    pairs = [(E1.mul(G1_GEN, 7 + 5 * k), E2.mul(G2_GEN, 13 + 9 * k)) for k in range(4)]
+    pb = b"".join(g1_serialize(p) for p, _ in pairs)
+    qb = b"".join(g2_serialize(q) for _, q in pairs)
+    singles = [miller_loop_fast(p, q) for p, q in pairs]
+    for use in ([1, 1, 1, 1], [0, 1, 1, 1], [1, 0, 0, 1], [1, 1, 0, 0], [0, 0, 0, 0]):
+        o = buf(576)
+        hc.hc_miller_paired4(pb, qb, (ctypes.c_int32 * 4)(*use), o)
+        exp = F12_ONE
+        for u, f in zip(use, singles):
+            if u:
+                exp = f12_mul(exp, f)
+        assert ub12(o.raw) == exp, use
+
+
 def test_g1_subgroup_check(hc):
     """lsg_curve.hpp:g1_in_group ([r]P == O, KeyValidate) against oracle/curves.py:in_g1 on
     subgroup points, the identity and on-curve points outside the subgroup."""
