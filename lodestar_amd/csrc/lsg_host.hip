@@ -267,6 +267,7 @@ struct Slot {
   std::vector<uint32_t> pk_cnt, pk_first;
   std::vector<uint64_t> rnd;
   bool single_keys = false;  // every set has exactly one key (key i is set i's)
+  uint32_t pk_stride = 96;   // bytes per key slot in d_pk: 4 when every key is a table index
   // per-set state
   DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_rs2, d_fall,
       d_fall2;
@@ -749,10 +750,15 @@ int launch_hash(Slot* s, int n) {
 // randomizers drawn here (seed == 0: OS CSPRNG; else deterministic, for tests)
 int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
   size_t npk = 0, msg_total = 0;
+  bool all_index = true;  // every key names a table row: 4-byte key slots (a block body's
+                          // ~3.7M signers cross PCIe as 15 MB instead of 355 MB)
   for (size_t i = 0; i < n; i++) {
     npk += sets[i]->n_pks;
     msg_total += sets[i]->msg_len;
+    if (sets[i]->n_pks && sets[i]->pk_len != LSG_PK_INDEX) all_index = false;
   }
+  const size_t ks = all_index ? 4 : 96;
+  s->pk_stride = (uint32_t)ks;
   s->n_sets = n;
   s->n_pks = npk;
   LSG_RC(size_inputs(s, n, npk, msg_total));
@@ -760,7 +766,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
   const size_t o_sig = 0, o_siglen = al(o_sig + 192 * nn), o_msgoff = al(o_siglen + 4 * nn),
                o_msglen = al(o_msgoff + 4 * nn), o_pklen = al(o_msglen + 4 * nn), o_rnd = al(o_pklen + 4 * np),
-               o_pk = al(o_rnd + 8 * nn), o_msg = al(o_pk + 96 * np);
+               o_pk = al(o_rnd + 8 * nn), o_msg = al(o_pk + ks * np);
   uint8_t* A = H_<uint8_t>(s->h_arena);
   uint32_t* siglen = (uint32_t*)(A + o_siglen);
   uint32_t* msgoff = (uint32_t*)(A + o_msgoff);
@@ -789,6 +795,15 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
     s->pk_cnt[i] = q->n_pks;
     s->pk_first[i] = (uint32_t)po;
     if (q->n_pks != 1) single = false;
+    if (all_index) {  // the set's indices are contiguous in the caller's buffer
+      std::fill(pklen + po, pklen + po + q->n_pks, (uint32_t)LSG_PK_INDEX);
+      if (q->pks)
+        memcpy(A + o_pk + 4 * po, q->pks, 4 * (size_t)q->n_pks);
+      else
+        memset(A + o_pk + 4 * po, 0, 4 * (size_t)q->n_pks);
+      po += q->n_pks;
+      continue;
+    }
     for (uint32_t k = 0; k < q->n_pks; k++) {
       pklen[po] = q->pk_len;
       uint8_t* pd = A + o_pk + 96 * po;
@@ -830,7 +845,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
     DevBuf* d;
     size_t off, len;
   } cp[] = {{&s->d_sig, o_sig, 192 * nn},      {&s->d_siglen, o_siglen, 4 * nn}, {&s->d_msg, o_msg, std::max(msg_total, (size_t)1)},
-            {&s->d_msgoff, o_msgoff, 4 * nn}, {&s->d_msglen, o_msglen, 4 * nn}, {&s->d_pk, o_pk, 96 * np},
+            {&s->d_msgoff, o_msgoff, 4 * nn}, {&s->d_msglen, o_msglen, 4 * nn}, {&s->d_pk, o_pk, ks * np},
             {&s->d_pklen, o_pklen, 4 * np},   {&s->d_rnd, o_rnd, 8 * nn}};
   for (auto& x : cp) LSG_HIP(s, hipMemcpyAsync(x.d->p, A + x.off, x.len, hipMemcpyHostToDevice, S));
   return LSG_OK;
@@ -1027,7 +1042,7 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item
   if (np > 0) {
     // single-key sets decode straight into their aggregate slot
     uint32_t* dst = s->single_keys ? P_<uint32_t>(s->d_agg) : P_<uint32_t>(s->d_pkp);
-    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen), dst,
+    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen), dst,
                                          P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok),
                                          (uint32_t)d->pktab_n));
   }
@@ -1825,7 +1840,7 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
   }
   LSG_RC(util_stage_keys(s, pks, pk_len, n));
   // decode straight into the table rows first .. first + n - 1
-  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)n, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen),
+  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)n, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
                                        P_<uint32_t>(d->d_pktab) + W_G1P * first, P_<int32_t>(s->d_pkerr), nullptr,
                                        nullptr, 0u));
   pkerr.assign(n, 0);
@@ -2174,7 +2189,7 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
   SegPlan P = plan_seg(s->plan, 0, off, len, false, 0, 0);
   LSG_RC(upload_plan(s));
   const int np = (int)n;
-  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), P_<uint32_t>(s->d_pklen),
+  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
                                        P_<uint32_t>(s->d_pkp), P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab),
                                        P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
   LSG_RC(run_seg(s, 0, "g1_aggregate", P, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));

@@ -7,7 +7,8 @@
 // pubkey -> projective G1 (infinity and undecodable keys become (0:1:0)).  A key given by
 // index (len == LSG_PK_INDEX: the slot's first 4 bytes) is gathered from the resident table
 // (tab, tab_ok: decoded keys of lsg_pubkey_table_set; tab_n indices).
-__global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ pk, const uint32_t* __restrict__ pk_len,
+__global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ pk, uint32_t stride,
+                                            const uint32_t* __restrict__ pk_len,
                                             uint32_t* __restrict__ pkp, int32_t* __restrict__ err,
                                             const uint32_t* __restrict__ tab, const uint8_t* __restrict__ tab_ok,
                                             uint32_t tab_n) {
@@ -16,7 +17,7 @@ __global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ p
   g1p_t p = proj_inf<fp_t>();
   int e;
   if (len == LSG_PK_INDEX) {
-    const uint8_t* b = pk + 96 * item;
+    const uint8_t* b = pk + (size_t)stride * item;
     const uint32_t idx = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
     const bool ok = idx < tab_n && tab_ok[idx];
     e = ok ? 0 : LSG_ERR_BAD_INDEX;
@@ -26,7 +27,7 @@ __global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ p
     a.x = fp_zero();
     a.y = fp_zero();
     bool is_inf = false;
-    e = (len == 48 || len == 96) ? g1_deserialize(a, is_inf, pk + 96 * item, (int)len) : LSG_BLST_INVALID_SIZE;
+    e = (len == 48 || len == 96) ? g1_deserialize(a, is_inf, pk + (size_t)stride * item, (int)len) : LSG_BLST_INVALID_SIZE;
     if (e == 0 && !is_inf) p = proj_from_aff(a);
   }
   lane_store(pkp, item, p);
@@ -125,9 +126,9 @@ __global__ void LSG_KERNEL_ATTR k_sk_to_pk(int n, const uint8_t* __restrict__ sk
 }
 
 namespace lsgk {
-hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, const uint32_t* pk_len, uint32_t* pts, int32_t* err,
-                     const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n) {
-  LSG_LAUNCH_ITEMS(k_pk_decode, n, st, n, pk, pk_len, pts, err, tab, tab_ok, tab_n);
+hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
+                     int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n) {
+  LSG_LAUNCH_ITEMS(k_pk_decode, n, st, n, pk, stride, pk_len, pts, err, tab, tab_ok, tab_n);
 }
 hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err) {
   LSG_LAUNCH_ITEMS(k_pk_validate, n, st, n, pk, len, pts, err);

@@ -39,7 +39,8 @@ hipError_t g2p_to_canon(hipStream_t st, int n, const uint32_t* pts, uint8_t* out
 hipError_t sign(hipStream_t st, int n, const uint8_t* sks, const uint32_t* H, uint8_t* out96);
 
 // ---- public keys (lsg_k_pk.hip)                                       SURVEY 8a H8, M1, M4
-hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, const uint32_t* pk_len, uint32_t* pts,
+// pk: key slots of `stride` bytes (96, or 4 when every key is a table index)
+hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
                      int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
 hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err);
 hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* rnd, uint32_t* Pp, uint32_t* zP,
