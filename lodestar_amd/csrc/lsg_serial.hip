@@ -11,6 +11,19 @@
 
 #include "lsg_serial.h"
 
+// Built twice: lsg_serial.hip (LSG_ROWS_PER_ITEM 4, the rows of a wave share one item: latency
+// for the few groups of a clean package) and lsg_serial_wide.hip (1: four items per wave, no
+// replicated work, for the thousands of per-job groups of a fallback phase); lsg_serial.h
+// picks by the number of groups.
+#ifndef LSG_ROWS_PER_ITEM
+#define LSG_ROWS_PER_ITEM 4
+#endif
+#if LSG_ROWS_PER_ITEM == 4
+#define LSG_ROW_FN(x) x##_r4
+#else
+#define LSG_ROW_FN(x) x##_r1
+#endif
+
 namespace {
 #include "lsg_fp_lane.hpp"
 #include "lsg_io.hpp"
@@ -19,7 +32,7 @@ namespace {
 #define LSG_ROW_TPB 64  // one wave: LSG_ROWS_PER_ITEM rows per item, 4 / LSG_ROWS_PER_ITEM items
 #define ROW_ITEM() ((int)((blockIdx.x * blockDim.x + threadIdx.x) / (16 * LSG_ROWS_PER_ITEM)))
 
-__global__ void __launch_bounds__(LSG_ROW_TPB) k_row_final_exp(int ng, const uint8_t* __restrict__ F576,
+__global__ void __launch_bounds__(LSG_ROW_TPB) LSG_ROW_FN(k_row_final_exp)(int ng, const uint8_t* __restrict__ F576,
                                                                int32_t* __restrict__ verdict) {
   lsg_lane_setup();
   const int item = ROW_ITEM();
@@ -28,7 +41,7 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_final_exp(int ng, const uin
   if ((threadIdx.x & 15) == 0) verdict[item] = one ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(LSG_ROW_TPB) k_row_miller_neg_g1(int ng, const uint8_t* __restrict__ S288,
+__global__ void __launch_bounds__(LSG_ROW_TPB) LSG_ROW_FN(k_row_miller_neg_g1)(int ng, const uint8_t* __restrict__ S288,
                                                                    uint8_t* __restrict__ out576) {
   lsg_lane_setup();
   const int item = ROW_ITEM();
@@ -47,7 +60,7 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_miller_neg_g1(int ng, const
 // The bucket MSM's last step fused with the signature Miller loop: S_g = sum_k 2^k C_{g,k}
 // by Horner over the group's 64 per-bit sums (63 doublings + 63 additions, complete
 // formulas), then ML(-G1, S_g).  Both are single dependency chains, so they run on rows.
-__global__ void __launch_bounds__(LSG_ROW_TPB) k_row_horner_miller(int ng, const uint8_t* __restrict__ C288,
+__global__ void __launch_bounds__(LSG_ROW_TPB) LSG_ROW_FN(k_row_horner_miller)(int ng, const uint8_t* __restrict__ C288,
                                                                    uint8_t* __restrict__ out576) {
   lsg_lane_setup();
   const int item = ROW_ITEM();
@@ -68,20 +81,20 @@ __global__ void __launch_bounds__(LSG_ROW_TPB) k_row_horner_miller(int ng, const
 
 static int row_blocks(int n) { return (n * 16 * LSG_ROWS_PER_ITEM + LSG_ROW_TPB - 1) / LSG_ROW_TPB; }
 
-hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
+hipError_t LSG_ROW_FN(lsg_row_final_exp)(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   if (ng <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_row_final_exp, dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, F576, verdict);
+  hipLaunchKernelGGL(LSG_ROW_FN(k_row_final_exp), dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, F576, verdict);
   return hipGetLastError();
 }
 
-hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
+hipError_t LSG_ROW_FN(lsg_row_miller_neg_g1)(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
   if (ng <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_row_miller_neg_g1, dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, S288, out576);
+  hipLaunchKernelGGL(LSG_ROW_FN(k_row_miller_neg_g1), dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, S288, out576);
   return hipGetLastError();
 }
 
-hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
+hipError_t LSG_ROW_FN(lsg_row_horner_miller)(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
   if (ng <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_row_horner_miller, dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, C288, out576);
+  hipLaunchKernelGGL(LSG_ROW_FN(k_row_horner_miller), dim3(row_blocks(ng)), dim3(LSG_ROW_TPB), 0, st, ng, C288, out576);
   return hipGetLastError();
 }
