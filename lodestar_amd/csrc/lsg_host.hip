@@ -138,6 +138,10 @@ constexpr int SEG_FOLD = 16;  // at most this many serial folds per lane pair wi
 // per pair before the butterfly (an 8193-term package product: 17 serial products in two
 // passes instead of 28)
 constexpr int SEG_FOLD_FP12 = 4;
+// work-bound passes (>= SEG_WIDE_PAIRS lane pairs at a wave's 32 pairs per segment): up to 64
+// folds per pair
+constexpr int SEG_FOLD_WIDE = 64;
+constexpr size_t SEG_WIDE_PAIRS = 131072;
 
 // lane pairs per chunk (log2): enough that the longest segment fits one chunk of SEG_FOLD
 // folds per pair (one pass), and at least a quarter of the mean length (latency: folds are
@@ -172,8 +176,17 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
     SegPass pass;
     int32_t max_len = 0;
     for (const Pend& p : cur) max_len = std::max(max_len, p.len);
-    const int fold = op == 2 ? SEG_FOLD_FP12 : SEG_FOLD;
+    int fold = op == 2 ? SEG_FOLD_FP12 : SEG_FOLD;
     pass.ips_log2 = ips_for(avg, max_len, fold);
+    // many segments (a block body's ~8k aggregations of ~450 keys): the launch is work-bound,
+    // and every butterfly level costs each lane pair one operation, so use as few pairs per
+    // chunk as keep the chip full, folding up to SEG_FOLD_WIDE terms each
+    if (op != 2 && (cur.size() << 5) >= SEG_WIDE_PAIRS) {
+      int l = 0;
+      while (l < pass.ips_log2 && (int32_t)(SEG_FOLD_WIDE << l) < max_len) l++;
+      pass.ips_log2 = l;
+      fold = SEG_FOLD_WIDE;
+    }
     pass.src = src;
     pass.tmp_out = tmp_out;
     const int32_t cap = (int32_t)((1 << pass.ips_log2) * fold);

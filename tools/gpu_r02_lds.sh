@@ -1,5 +1,5 @@
 #!/bin/bash
-# segmented G1/G2 reductions with chunks of up to a workgroup (LDS tree across its waves):
+# segmented reductions (throughput-mode chunking for work-bound passes):
 # parity suite, then the block, sync and jobs workloads
 set -o pipefail
 cd $GRAFT_REPO_ROOT
