@@ -242,6 +242,23 @@ def pmc_traffic(kernel, sets_per_launch):
     return k["hbm_bytes_per_dispatch"]
 
 
+def pmc_alone(kernel, sets_per_launch):
+    """The kernel alone on the GPU, from the committed isolation profile (tools/gpu_pmc.sh ->
+    tools/pmc_summary.py -> profiles/rNN_pmc_isolation.json: rocprofv3 --pmc serialises the
+    dispatches): its average duration and fraction of the mad peak.  The live `achieved`
+    above shares the SIMDs with the other packages in flight."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_isolation.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = d["kernels"].get(kernel)
+    if k is None or d.get("sets_per_launch") != sets_per_launch or "serial_us" not in k:
+        return None
+    return {"kernel_us": k["serial_us"], "frac": k.get("frac_of_peak_serial"),
+            "wave_cycles_per_valu": k.get("wave_cycles_per_valu"), "source": os.path.relpath(files[-1], ROOT)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -438,7 +455,7 @@ def main():
     peak = peak_mad / 1e12
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
             "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
-            "traffic": pmc_traffic(dom, n_sets),
+            "traffic": pmc_traffic(dom, n_sets), "alone": pmc_alone(dom, n_sets),
             "kernel_ms": round(agg[dom] / max(calls[dom], 1), 3), "work_per_launch_fp_muls": muls}
     total_sets = n_sets * world * args.steps
     value = total_sets / elapsed
