@@ -413,6 +413,51 @@ LSG_PLEAF fp_duo pair_fp2_sqr_v(fp_arg_t va0, fp_arg_t va1) {
   return fp_duo{t[0], fp_add(t[1], t[1])};
 }
 
+// a^e for a fixed public exponent e (12 little-endian words) in one call: the same sliding
+// window of width 4 as lsg_tower.hpp's generic fp_pow_fixed, with its ~455 products inline
+// (one call, one load of p, no per-product argument moves) -- the square roots of signature
+// decompression and SSWU and the batched inversions' roots are chains of these
+LSG_PLEAF fp_t pair_pow_fixed(fp_t a, const uint32_t* __restrict__ e) {
+  auto mul = [](const fp_t& x, const fp_t& y) {
+    LSG_COUNT_MUL();
+    fp_t r;
+    pair_mont_mul_n<1>(&r, &x, &y);
+    return r;
+  };
+  fp_t T[8];  // T[k] = a^(2k+1)
+  T[0] = a;
+  const fp_t a2 = mul(a, a);
+#pragma unroll
+  for (int k = 1; k < 8; k++) T[k] = mul(T[k - 1], a2);
+  int i = 383;
+  while (i >= 0 && !((e[i >> 5] >> (i & 31)) & 1u)) i--;
+  fp_t r = T[0];
+  bool started = false;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = mul(r, r);
+      i--;
+      continue;
+    }
+    int j = i - 3 < 0 ? 0 : i - 3;
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) j++;
+    uint32_t v = 0;
+    for (int t = i; t >= j; t--) v = (v << 1) | ((e[t >> 5] >> (t & 31)) & 1u);
+    if (started)
+      for (int t = i; t >= j; t--) r = mul(r, r);
+    fp_t tv = T[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) tv = fp_select(v == (uint32_t)(2 * k + 1), T[k], tv);
+    r = started ? mul(r, tv) : tv;
+    started = true;
+    i = j - 1;
+  }
+  return r;
+}
+#if LSG_LEAF_MODE != 0 && !defined(LSG_NO_POW_LEAF)  // (A/B builds: -DLSG_NO_POW_LEAF)
+#define LSG_POW_LEAF 1  // lsg_tower.hpp's fp_pow_fixed calls pair_pow_fixed
+#endif
+
 // ---- canonical values
 // v in (-p, 2p) -> the representative in [0, p), fully normalised
 LSG_PFN fp_t pair_canon_small(const fp_t& v0) {

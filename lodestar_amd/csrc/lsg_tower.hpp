@@ -31,6 +31,9 @@ LSG_INL fp_t fp_from_be48(const uint8_t* b) { return fp_from_be_bytes(b, 12); }
 // wave takes the same branches; the table entry is picked with selects (no indexed
 // register access).
 LSG_BIGFN fp_t fp_pow_fixed(fp_t a, const uint32_t* e) {
+#ifdef LSG_POW_LEAF
+  return pair_pow_fixed(a, e);
+#else
   fp_t T[8];  // T[k] = a^(2k+1)
   T[0] = a;
   const fp_t a2 = fp_sqr(a);
@@ -60,6 +63,7 @@ LSG_BIGFN fp_t fp_pow_fixed(fp_t a, const uint32_t* e) {
     i = j - 1;
   }
   return r;
+#endif
 }
 
 LSG_INL fp_t fp_inv(const fp_t& a) { return fp_pow_fixed(a, LSG_EXP_P_MINUS_2); }  // inv(0) = 0
