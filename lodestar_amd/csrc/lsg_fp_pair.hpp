@@ -424,11 +424,18 @@ LSG_PLEAF fp_t pair_pow_fixed(fp_t a, const uint32_t* __restrict__ e) {
     pair_mont_mul_n<1>(&r, &x, &y);
     return r;
   };
-  fp_t T[8];  // T[k] = a^(2k+1)
-  T[0] = a;
+  // T[k] = a^(2k+1), written out: a table loop the compiler declines to unroll would put T
+  // in scratch with indexed access
+  fp_t T[8];
   const fp_t a2 = mul(a, a);
-#pragma unroll
-  for (int k = 1; k < 8; k++) T[k] = mul(T[k - 1], a2);
+  T[0] = a;
+  T[1] = mul(T[0], a2);
+  T[2] = mul(T[1], a2);
+  T[3] = mul(T[2], a2);
+  T[4] = mul(T[3], a2);
+  T[5] = mul(T[4], a2);
+  T[6] = mul(T[5], a2);
+  T[7] = mul(T[6], a2);
   int i = 383;
   while (i >= 0 && !((e[i >> 5] >> (i & 31)) & 1u)) i--;
   fp_t r = T[0];

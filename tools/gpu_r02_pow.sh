@@ -1,5 +1,5 @@
 #!/bin/bash
-# one-call fixed exponentiation (pair_pow_fixed, default) vs the generic loop of leaf calls
+# one-call fixed exponentiation with its table written out (default) vs the previous build
 # (-DLSG_NO_POW_LEAF): parity suite, then jobs benches interleaved
 set -o pipefail
 cd $GRAFT_REPO_ROOT
