@@ -259,19 +259,71 @@ def pmc_alone(kernel, sets_per_launch):
             "wave_cycles_per_valu": k.get("wave_cycles_per_valu"), "source": os.path.relpath(files[-1], ROOT)}
 
 
+def run_node_workload(args):
+    """The drop-in path itself: node bench/bench_node.js drives BlsGpuVerifier.verifySignatureSets
+    ([set], {batchable: true}) at the config D shape (one 32,768-set slot per step), intake gated
+    on canAcceptWork() as the gossip processor gates it; the JS host packs the arena, the addon's
+    package threads submit and wait, the verdicts settle every call's promise.  One GPU: the
+    verifier of a multi-GPU node opens one context over all of them (lsg_init_devices), which
+    `--devices` in the jobs workload measures."""
+    import subprocess
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        raise SystemExit("--workload node runs one Node process per node (use --gpus 1)")
+    cmd = ["node", os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--sets-per-step", str(args.sets_per_step), "--max-sigs-per-package",
+           str(args.node_max_sigs), "--device", str(local)]
+    w0 = time.monotonic_ns()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    w1 = time.monotonic_ns()
+    if r.returncode != 0:
+        raise SystemExit("bench_node.js failed:\n" + r.stdout[-2000:] + r.stderr[-4000:])
+    nb = json.loads(r.stdout.strip().splitlines()[-1])
+    cpu = None
+    if not args.no_cpu_baseline:
+        from lodestar_amd._native import Context
+        ctx = Context(local)
+        wl = Workload(ctx, "jobs", 0, 4096, 1)
+        ctx.close()
+        cpu = cpu_baseline_oracle([s for job, _ in wl.packages[0][0] for s in job])
+    line = {
+        "metric": METRIC, "value": round(nb["sets_per_s"], 1), "unit": "sets/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(nb["ms_per_step"], 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (interop keys, GPU-signed; fresh OS-CSPRNG randomizers per package)",
+        "config": {"workload": "drop-in Node host (SURVEY 8d config D shape): BlsGpuVerifier.verifySignatureSets"
+                               "([set], {batchable: true}) per single-pubkey gossip set, intake gated on canAcceptWork, "
+                               "through the N-API addon's package threads",
+                   "sets_per_step_per_gpu": args.sets_per_step, "global_batch": args.sets_per_step,
+                   "max_sigs_per_package": nb["max_sigs_per_package"], "parallelism": "shard1", "node": nb["node"]},
+        "p50_batch_latency_ms": round(nb["p50_call_latency_ms"], 3),
+        "p99_call_latency_ms": round(nb["p99_call_latency_ms"], 3),
+        "p50_unloaded_latency_ms": round(nb["p50_lone_call_latency_ms"], 3),
+        "packages": nb["packages"], "mean_package_sets": round(nb["mean_package_sets"], 1),
+        "timed_window_monotonic_ns": [w0, w1], "roofline": None,
+        "roofline_note": "kernel-level roofline: the jobs workload (same kernels, ctypes host)",
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30, help="timed packages per GPU")
     ap.add_argument("--warmup", type=int, default=5, help="untimed packages per GPU (at least --depth are run)")
-    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial"], default="jobs")
+    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node"], default="jobs")
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
+    ap.add_argument("--node-max-sigs", type=int, default=32768, help="node workload: maxSigsPerPackage")
     args = ap.parse_args()
+    if args.workload == "node":
+        return run_node_workload(args)
     if args.depth is None:
         args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 6, "gossip": 8}[args.workload]
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)

@@ -117,6 +117,8 @@ typedef struct {
   uint64_t end_ns;        /* CLOCK_MONOTONIC ns: verdicts resolved */
   uint32_t n_final_exps;  /* final exponentiations run (package, chunk and job groups; node check) */
   uint32_t submit_us;     /* host time inside lsg_submit_jobs (staging, randomizers, plans, launches) */
+  int32_t key_error;      /* deserializeSet failure that rejected the whole package (BLST_*), 0: none */
+  uint32_t key_error_job; /* caller index of the job holding that first bad key */
 } lsg_stats;
 
 /* A context over one or more devices.  Per device it owns 16 pipeline slots (each: a main
@@ -153,7 +155,13 @@ int lsg_allocation_count(lsg_ctx* ctx, uint64_t* n);
  * and then the jobs of failing chunks checked (on the resident per-set values), so verdicts
  * and the batch_retries / batch_sigs_success counters are those of worker.ts.  wait blocks on
  * the ticket and applies those rules.  seed != 0 makes the randomizers deterministic (tests);
- * seed == 0 draws them from getrandom (LSG_ERR_ENTROPY if that fails). */
+ * seed == 0 draws them from getrandom (LSG_ERR_ENTROPY if that fails).
+ * A key that does not deserialize anywhere in the package (any device of the context) rejects
+ * every job with the code of the first bad key in caller job order (worker.ts:41-43).
+ * On a multi-device context the 16-job chunks are formed per device, so batch_retries /
+ * batch_sigs_success can differ from a single device's; per-job verdicts never do.
+ * A wait that fails before resolving (a device error while blocking) leaves the ticket
+ * outstanding: it may be waited on again. */
 int lsg_submit_jobs(lsg_ctx* ctx, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket);
 int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n_jobs] */, lsg_stats* stats);
 /* One process per GPU (SURVEY.md 8e over torch.distributed / any host collective), on a
@@ -161,7 +169,10 @@ int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n
  * ready and writes it (576 bytes, canonical; the identity when the package has no batchable
  * set; *has_batch says which).  The caller all-gathers the partials, checks their product with
  * lsg_final_*, and resolves the ticket with that node verdict (1 passed, 0 failed: this GPU's
- * own package check then localises).  lsg_wait_jobs == lsg_wait_jobs_node(..., -1, ...). */
+ * own package check then localises).  lsg_wait_jobs == lsg_wait_jobs_node(..., -1, ...).
+ * The node verdict is advisory: this GPU's own check of its share is computed in any case and
+ * decides, so a caller whose exchange went wrong (node_valid 1 but this share invalid) gets
+ * the localised per-job verdicts, never a wrongly accepted package. */
 int lsg_jobs_partial(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* has_batch);
 int lsg_wait_jobs_node(lsg_ctx* ctx, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results,
                        lsg_stats* stats);

@@ -82,6 +82,7 @@ class LsgStats(ctypes.Structure):
         ("batch_retries", ctypes.c_uint32), ("batch_sigs_success", ctypes.c_uint32),
         ("start_ns", ctypes.c_uint64), ("end_ns", ctypes.c_uint64),
         ("n_final_exps", ctypes.c_uint32), ("submit_us", ctypes.c_uint32),
+        ("key_error", ctypes.c_int32), ("key_error_job", ctypes.c_uint32),
     ]
 
 

@@ -112,9 +112,9 @@ def build_napi(verbose=True):
     deps = [NAPI_SRC, OUT, os.path.join(ROOT, "include", "lodestar_bls.h")]
     if os.path.exists(NAPI_OUT) and max(os.path.getmtime(d) for d in deps) <= os.path.getmtime(NAPI_OUT):
         return NAPI_OUT
-    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-DNODE_GYP_MODULE_NAME=lsg_napi",
+    cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-shared", "-fPIC", "-DNODE_GYP_MODULE_NAME=lsg_napi",
            "-I", NODE_INCLUDE, "-I", os.path.join(ROOT, "include"), NAPI_SRC, "-o", NAPI_OUT + ".tmp",
-           "-L", HERE, "-llodestar_bls", "-Wl,-rpath,$ORIGIN/.."]
+           "-L", HERE, "-llodestar_bls", "-lpthread", "-Wl,-rpath,$ORIGIN/.."]
     if verbose:
         print("[lodestar_amd.build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -648,8 +648,9 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, int pkg = 
     if (!miller_fused()) LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
     LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg + nn / 16 + 1)));
   }
-  if (pkg) {  // fallback signature sums and Miller items
-    LSG_RC(ensure(s, s->d_fall2, 4 * W_F12 * (nn + gg)));
+  if (pkg) {  // fallback signature sums and Miller items: a phase C of single-set jobs needs
+              // one item and one term slot per retried set
+    LSG_RC(ensure(s, s->d_fall2, 4 * W_F12 * (nn + std::max(gg, nn))));
     LSG_RC(ensure(s, s->d_rs2, 4 * W_G2P * nn));
   }
   LSG_RC(ensure_host(s, s->h_err, 4 * nn));
@@ -1357,6 +1358,10 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
                        const std::vector<std::pair<int32_t, int32_t>>* given, std::vector<int32_t>& v) {
   v.assign(groups.size(), 0);
   if (groups.empty()) return LSG_OK;
+  // size this phase's buffers BEFORE any pointer into them is taken or any launch queued:
+  // a phase with more groups than phase A had grows d_fall2 (and the group buffers), and a
+  // pointer saved earlier would name the freed allocation
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, groups.size(), 0, 2));
   timer_reset(s);
   s->plan.clear();
   PhasePlan Ph;
@@ -1398,16 +1403,31 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
 // The reference's verdict rules for this device's share of the package (worker.ts:30-106),
 // after ev_done.  node_valid: 1 = the node-wide check of all devices' partials passed, 0 = it
 // failed (this device's own package check localises), -1 = no node check (single device).
-int pkg_resolve(Slot* s, CtxLock* lk, int node_valid) {
+// worker.ts:41-43: deserializeSet runs over the package's jobs in caller order before any
+// verification; the first bad pubkey throws out of verifyManySignatureSets.  Returns that
+// key's code for this device's share (0: none) and the caller index of its job.
+int32_t first_pk_error(Slot* s, size_t* job_id) {
+  const int32_t* pkerr = H_<int32_t>(s->h_pkerr);
+  for (size_t k = 0; k < s->jobs.size(); k++) {  // jobs[k] are in caller order (job_ids ascending)
+    const JobRec& J = s->jobs[k];
+    for (size_t i = J.first; i < J.first + J.count; i++)
+      for (uint32_t q = 0; q < s->pk_cnt[i]; q++)
+        if (const int32_t e = pkerr[s->pk_first[i] + q]) {
+          *job_id = s->job_ids[k];
+          return e;
+        }
+  }
+  return 0;
+}
+
+// pkfail: the package-wide deserializeSet failure (first_pk_error over every device of the
+// ticket, in caller order) -- a bad key on any device rejects every job of the package
+int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
   const SetStatus ss = read_status(s);
   const PhasePlan& A = s->phA;
   std::vector<int32_t> vA(H_<int32_t>(s->h_verdict), H_<int32_t>(s->h_verdict) + A.groups.size());
   s->stats.n_final_exps += (uint32_t)A.groups.size();
   const size_t nj = s->jobs.size();
-  // worker.ts:108-114: deserializeSet runs first; a bad pubkey throws out of
-  // verifyManySignatureSets and rejects every job of the package
-  int32_t pkfail = 0;
-  for (size_t k = 0; k < s->n_pks && !pkfail; k++) pkfail = ss.pkerr[k];
   if (pkfail) {
     for (size_t j = 0; j < nj; j++) s->results[j] = {LSG_ERROR, pkfail};
     return LSG_OK;
@@ -1421,7 +1441,12 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid) {
   }
   if (s->batch_order.empty()) return LSG_OK;
   // batchable jobs: chunks of >= 16 jobs (worker.ts:51-86)
-  const bool big_ok = s->big_g < 0 || node_valid == 1 || (node_valid != 1 && vA[(size_t)s->big_g] != 0);
+  // The device's own check of its share (computed in phase A in any case) decides.  The
+  // node-wide verdict is advisory: a passing node check with a failing own check (a caller
+  // whose all-gather missed a rank) localises like a failing one instead of
+  // accepting the package.
+  (void)node_valid;
+  const bool big_ok = s->big_g < 0 || vA[(size_t)s->big_g] != 0;
   auto chunks = chunkify(s->batch_order.size(), 16);
   std::vector<size_t> retry;  // jobs verified individually (phase C)
   std::vector<Grp> chk;       // chunks checked on their own (phase B)
@@ -1669,10 +1694,20 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
   memset(&total, 0, sizeof(total));
   total.start_ns = s0->stats.start_ns;
   total.submit_us = s0->stats.submit_us;
+  int32_t pkfail = 0;  // package-wide: the first bad key in caller job order over all devices
+  size_t pkfail_job = SIZE_MAX;
+  for (int d = 0; d < n && !rc; d++) {
+    size_t j = SIZE_MAX;
+    const int32_t e = first_pk_error(&c->dev[d]->slots[p], &j);
+    if (e && j < pkfail_job) {
+      pkfail = e;
+      pkfail_job = j;
+    }
+  }
   for (int d = 0; d < n && !rc; d++) {
     Slot* s = &c->dev[d]->slots[p];
     (void)hipSetDevice(c->dev[d]->device);
-    rc = pkg_resolve(s, lk, node_valid);
+    rc = pkg_resolve(s, lk, node_valid, pkfail);
     if (rc) break;
     for (size_t k = 0; k < s->jobs.size(); k++) results[s->job_ids[k]] = s->results[k];
     total.batch_retries += s->stats.batch_retries;
@@ -1680,6 +1715,8 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
     total.n_final_exps += s->stats.n_final_exps;
   }
   if (s0->has_node) total.n_final_exps += 1;
+  total.key_error = pkfail;
+  total.key_error_job = pkfail ? (uint32_t)pkfail_job : 0;
   total.end_ns = now_ns();
   if (stats) *stats = total;
   for (int d = 0; d < n; d++) {
@@ -2096,11 +2133,16 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
     int rc = submit_pkg(c, &job, 1, seed, &t);
     if (rc) return rc;
   }
-  if (int prc = presync_pkg(c, t, false)) return prc;
+  const int prc = presync_pkg(c, t, false);
   LSG_ENTER(c);
   const int p = ticket_pkg(c, t);
   if (p < 0) return LSG_ERR_INVALID_ARG;
   Slot* s = &c->dev[0]->slots[p];
+  if (prc) {  // the internal ticket cannot be waited on again: give its slot back
+    sync_slot(s);
+    s->kind = SLOT_FREE;
+    return prc;
+  }
   const SetStatus ss = read_status(s);
   *any_error = 0;
   for (size_t i = 0; i < n_sets; i++) {

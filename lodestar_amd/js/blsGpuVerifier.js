@@ -8,22 +8,23 @@
  * method restates):
  *   verifySignatureSets   index.ts:151-191  verifyOnMainThread shortcut, chunks of <= 128
  *                         sets, AND over the chunks, empty chunk list -> throw
- *   canAcceptWork         index.ts:143-149  back-pressure: packages in flight < pipeline
- *                         slots (the reference's workersBusy < poolSize) and jobs < 512
+ *   canAcceptWork         index.ts:143-149  back-pressure, on sets for a GPU: queued +
+ *                         buffered + in-flight sets < maxPendingSigs
  *   close                 index.ts:193-217  pending jobs reject with QueueError
  *                         QUEUE_ERROR_QUEUE_ABORTED
  *   _queueBlsWork         index.ts:255-302  batchable jobs buffered until > 32 sigs or
  *                         100 ms; others queued and run on the next macrotask
- *   _runJob/_prepareWork  index.ts:307-420  one package of <= 128 sigs per free slot;
+ *   _runJob/_prepareWork  index.ts:307-420  packages sized for the GPU (class comment);
  *                         per-job resolve/reject; metrics
  *   _runBufferedJobs      index.ts:425-431
  *   chunkifyMaximizeChunkSize  multithread/utils.ts:4-19
  * What replaces the worker threads and @chainsafe/blst: the N-API addon
  * (lodestar_amd/napi/lsg_napi.c) over the C ABI (include/lodestar_bls.h).  A package is
- * submitted with addon.submitJobs (inputs copied to pinned memory before it returns) and
- * awaited with addon.waitJobs (blocking part on a libuv pool thread).  The GPU applies the
- * worker's batch + per-job retry rules (worker.ts:30-106) itself, so one package costs one
- * round trip.  Aggregate sets send all their pubkeys; the GPU sums them (utils.ts:11).
+ * packed into one byte arena (packJobs) and handed to addon.verifyPacked, whose native
+ * package thread submits and waits (neither the JS thread nor libuv's pool blocks); the
+ * promise settles with per-job verdict arrays.  The GPU applies the worker's batch + per-job
+ * retry rules (worker.ts:30-106) itself, so one package costs one round trip.  Aggregate sets
+ * send all their pubkeys; the GPU sums them (utils.ts:11).
  *
  * Node-wide: chain.ts:195-198 builds ONE verifier per node, its pool spanning every core
  * (multithread/poolSize.ts:7).  options.devices = [0, 1, ...] opens one context over all the
@@ -35,7 +36,8 @@
  * createBlsVerifier picks between the two as chain.ts:196-198 does (blsVerifyAllMainThread).
  *
  * Metrics: the reference's names and observation points (metrics/metrics/lodestar.ts:350-430,
- * multithread/index.ts:319-381): jobWaitTime, totalJobsGroupsStarted, totalJobsStarted,
+ * multithread/index.ts:135-140,319-381): queueLength, workersBusy (collected at scrape time),
+ * jobWaitTime, totalJobsGroupsStarted, totalJobsStarted,
  * totalSigSetsStarted, timePerSigSet, jobsWorkerTime{workerId}, latencyToWorker,
  * latencyFromWorker, successJobsSignatureSetsCount, errorJobsSignatureSetsCount,
  * batchRetries, batchSigsSuccess, mainThreadDurationInThreadPool, bls.aggregatedPubkeys.
@@ -160,38 +162,301 @@ function loadAddon() {
   return require("../napi/lsg_napi.node");
 }
 
+/** Reference set shape check done at call time, as serializeSet throws there (index.ts:177). */
+function checkSet(set) {
+  if (set.pubkeyIndices === undefined && set.type !== SignatureSetType.single && set.type !== SignatureSetType.aggregate) {
+    throw Error("Unknown signature set type");
+  }
+}
+
+/** FIFO with O(1) shift (Array.prototype.shift is O(n) on long queues). */
+class Fifo {
+  constructor() {
+    this.items = [];
+    this.head = 0;
+  }
+  get length() {
+    return this.items.length - this.head;
+  }
+  push(x) {
+    this.items.push(x);
+  }
+  shift() {
+    if (this.head >= this.items.length) return undefined;
+    const x = this.items[this.head];
+    this.items[this.head++] = undefined;
+    if (this.head > 1024 && this.head * 2 > this.items.length) {
+      this.items = this.items.slice(this.head);
+      this.head = 0;
+    }
+    return x;
+  }
+  drain() {
+    const out = this.items.slice(this.head);
+    this.items = [];
+    this.head = 0;
+    return out;
+  }
+}
+
+/**
+ * Jobs travel in blocks.  A block is the group of jobs queued together -- one buffered batch
+ * of batchable jobs (index.ts:255-302 flushes it to the queue as a whole), or one
+ * non-batchable job -- kept as parallel arrays (no object per job), and a job's promise is
+ * `block.promise.then(PICK[idx])` with PICK[idx] a shared function reading verdict idx: one
+ * promise per call, no executor, no per-call closure.  In node 12 `new Promise(executor)`
+ * costs ~0.75 us against ~0.2 us for a `then` on a shared promise, which decides whether the
+ * JS thread can feed the GPU at all (it has to issue >1M calls/s).  The block resolves when
+ * its last job is answered.
+ */
+const JOB_PENDING = -1;
+const JOB_FAILED = 3; // settled with a JS Error (queue aborted, serialisation)
+const MAX_JOBS_PER_BLOCK = 4096;
+
+class VerdictBlock {
+  constructor(withTimes) {
+    this.sets = []; // per job: its sets
+    this.flags = []; // per job: JOB_BATCHABLE | JOB_PRIORITY
+    this.added = withTimes ? [] : null; // per job: Date.now() at queueing (jobWaitTime metric)
+    this.status = [];
+    this.codes = [];
+    this.errors = null;
+    this.nSigs = 0;
+    this.remaining = 0;
+    this.sealed = false;
+    this.order = null;
+    this.promise = new Promise((resolve) => {
+      this._resolve = resolve;
+    });
+  }
+  /** appends a job; priority jobs of a buffer go to its head (index.ts:296 unshift).
+   * Returns the job's verdict index; `order` maps queue positions to verdict indices once
+   * a job has been put in front. */
+  add(sets, flags, front) {
+    const idx = this.status.length;
+    this.status.push(JOB_PENDING);
+    this.codes.push(0);
+    if (front) {
+      if (!this.order) {
+        this.order = [];
+        for (let k = 0; k < idx; k++) this.order.push(k);
+      }
+      this.order.unshift(idx);
+      this.sets.unshift(sets);
+      this.flags.unshift(flags);
+      if (this.added) this.added.unshift(Date.now());
+    } else {
+      if (this.order) this.order.push(idx);
+      this.sets.push(sets);
+      this.flags.push(flags);
+      if (this.added) this.added.push(Date.now());
+    }
+    this.nSigs += sets.length;
+    this.remaining++;
+    return idx;
+  }
+  /** verdict index of the job at queue position k */
+  at(k) {
+    return this.order ? this.order[k] : k;
+  }
+  seal() {
+    this.sealed = true;
+    if (this.remaining === 0) this._resolve(this);
+  }
+  settle(idx, status, code, error) {
+    if (this.status[idx] !== JOB_PENDING) return;
+    this.status[idx] = status;
+    this.codes[idx] = code;
+    if (status === JOB_FAILED) {
+      if (!this.errors) this.errors = [];
+      this.errors[idx] = error;
+    }
+    if (--this.remaining === 0 && this.sealed) this._resolve(this);
+  }
+  failAll(error) {
+    for (let k = 0; k < this.status.length; k++) this.settle(k, JOB_FAILED, 0, error);
+  }
+  verdict(idx) {
+    const st = this.status[idx];
+    if (st === LSG_ERROR) throw Error(errorMessage(this.codes[idx]));
+    if (st === JOB_FAILED) throw this.errors[idx];
+    return st === LSG_VALID;
+  }
+}
+
+const PICK = [];
+for (let i = 0; i < MAX_JOBS_PER_BLOCK; i++) PICK.push((b) => b.verdict(i));
+
+const SET_DESC_WORDS = 7; // pkOff, pkLen, nPks, msgOff, msgLen, sigOff, sigLen (lsg_napi.c verifyPacked)
+
+/**
+ * A package of blocks in the addon's packed form: one byte arena with every key, message and
+ * signature, 7 descriptor words per set and 2 per job -- the role of the structured clone of
+ * BlsWorkReq[] in multithread/index.ts:335 (and of getAggregatedPubkey + toBytes,
+ * index.ts:177, except that aggregate keys are summed on the GPU).  A job whose sets cannot
+ * be serialized fails on its own and is left out.  `into` (optional) is a previous package's
+ * buffers, reused when large enough (fresh multi-MB typed arrays per package cost GC time).
+ */
+function packBlocks(blocks, nSigs, into) {
+  let cap = nSigs * 224 + 256;
+  let arena = into && into.arenaBuf.length >= cap ? into.arenaBuf : new Uint8Array(cap);
+  cap = arena.length;
+  let off = 0;
+  const put = (bytes) => {
+    const n = bytes.length;
+    if (off + n > cap) {
+      while (off + n > cap) cap *= 2;
+      const grown = new Uint8Array(cap);
+      grown.set(arena.subarray(0, off));
+      arena = grown;
+    }
+    const o = off;
+    arena.set(bytes, o);
+    off += n;
+    return o;
+  };
+  const setDescBuf = into && into.setDescBuf.length >= SET_DESC_WORDS * nSigs ? into.setDescBuf : new Uint32Array(SET_DESC_WORDS * nSigs);
+  let nJobs = 0;
+  for (const b of blocks) nJobs += b.sets.length;
+  const jobDescBuf = into && into.jobDescBuf.length >= 2 * nJobs ? into.jobDescBuf : new Uint32Array(2 * nJobs);
+  const jobBlock = [];
+  const jobIdx = [];
+  const sd = setDescBuf;
+  let k = 0;
+  let j = 0;
+  for (const block of blocks) {
+    for (let q = 0; q < block.sets.length; q++) {
+      const sets = block.sets[q];
+      const off0 = off;
+      const k0 = k;
+      try {
+        for (const set of sets) {
+          const d = SET_DESC_WORDS * k;
+          if (set.pubkeyIndices !== undefined) {
+            const ix = set.pubkeyIndices instanceof Uint32Array ? set.pubkeyIndices : Uint32Array.from(set.pubkeyIndices);
+            sd[d] = put(new Uint8Array(ix.buffer, ix.byteOffset, 4 * ix.length));
+            sd[d + 1] = 4; // LSG_PK_INDEX
+            sd[d + 2] = ix.length;
+          } else if (set.type === SignatureSetType.single) {
+            const pk = pubkeyBytes(set.pubkey);
+            sd[d] = put(pk);
+            sd[d + 1] = pk.length;
+            sd[d + 2] = 1;
+          } else if (set.type === SignatureSetType.aggregate) {
+            const pks = set.pubkeys;
+            const len = pks.length ? pubkeyBytes(pks[0]).length : 96;
+            sd[d] = off;
+            for (const pk of pks) {
+              const b = pubkeyBytes(pk);
+              if (b.length !== len) throw Error("every pubkey of an aggregate set must have the same encoding");
+              put(b);
+            }
+            sd[d + 1] = len;
+            sd[d + 2] = pks.length;
+          } else {
+            throw Error("Unknown signature set type");
+          }
+          sd[d + 3] = put(set.signingRoot);
+          sd[d + 4] = set.signingRoot.length;
+          sd[d + 5] = put(set.signature);
+          sd[d + 6] = set.signature.length;
+          k++;
+        }
+      } catch (e) {
+        off = off0;
+        k = k0;
+        block.settle(block.at(q), JOB_FAILED, 0, e);
+        continue;
+      }
+      jobDescBuf[2 * j] = sets.length;
+      jobDescBuf[2 * j + 1] = block.flags[q];
+      jobBlock.push(block);
+      jobIdx.push(block.at(q));
+      j++;
+    }
+  }
+  return {
+    jobBlock,
+    jobIdx,
+    arena: arena.subarray(0, off),
+    setDesc: sd.subarray(0, SET_DESC_WORDS * k),
+    jobDesc: jobDescBuf.subarray(0, 2 * j),
+    arenaBuf: arena,
+    setDescBuf,
+    jobDescBuf,
+    nSigs: k,
+  };
+}
+
+/** GPU package policy defaults (see the class comment) */
+const DEFAULT_MAX_SIGS_PER_PACKAGE = 32768;
+const DEFAULT_EAGER_PACKAGES = 2;
+
 class BlsGpuVerifier {
   /**
    * @param {{blsVerifyAllMultiThread?: boolean, device?: number, devices?: number[], seed?: number,
-   *          maxSigsPerPackage?: number, reserveSets?: number, reservePubkeys?: number}} options
+   *          maxSigsPerPackage?: number, eagerPackages?: number, minSigsWhenBusy?: number,
+   *          maxPendingSigs?: number, bufferWaitMs?: number, reserveSets?: number,
+   *          reservePubkeys?: number}} options
    * @param {{logger?: object, metrics?: object|null, addon?: object}} modules  addon is
    *        injectable (tests drive the queue logic with a mock of the addon's surface)
+   *
+   * Package policy (replaces the CPU pool's "<= 128 sigs per idle worker", index.ts:400-418,
+   * whose 16 busy workers would hold the GPU to ~128-set packages and ~40k sets/s):
+   *   - up to `eagerPackages` (2) packages go out as soon as jobs are queued, whatever their
+   *     size: an idle GPU answers a lone job at once;
+   *   - beyond that a package goes out only when the queue holds `minSigsWhenBusy` sigs
+   *     (maxSigsPerPackage / 4), or when an in-flight package completes: while the GPU is
+   *     busy the queue grows, so under load packages approach `maxSigsPerPackage` (32,768,
+   *     one launch filling all 256 CUs) and light load keeps the latency of small packages;
+   *   - at most one package per pipeline slot / package thread (addon.slots) is in flight.
+   * Back-pressure (canAcceptWork, index.ts:143-149) is on SETS: queued + buffered + in flight
+   * < `maxPendingSigs` (4 x maxSigsPerPackage).  Per-job verdicts do not depend on any of it:
+   * the GPU applies worker.ts's batch + retry rules to whatever package it gets.
+   * The reference's policy is {maxSigsPerPackage: 128, eagerPackages: slots}.
    */
   constructor(options = {}, modules = {}) {
     this.logger = modules.logger || null;
     this.metrics = modules.metrics || null;
     this.blsVerifyAllMultiThread = options.blsVerifyAllMultiThread === true;
     this.seed = options.seed || 0; // 0: randomizers from the OS CSPRNG (production)
-    // sigs of queued jobs drained into one GPU package (prepareWork, index.ts:400-418).  The
-    // reference's 128 suits a CPU worker; one GPU launch wants thousands of sets, so a
-    // production node sets e.g. 4096.  Per-job verdicts do not depend on it.
-    this.maxSigsPerPackage = options.maxSigsPerPackage || MAX_SIGNATURE_SETS_PER_JOB;
     this.addon = modules.addon || loadAddon();
     // throws loudly without a gfx950 device
     this.ctx = this.addon.open(Array.isArray(options.devices) ? options.devices : options.device || 0);
     this.poolSize = this.addon.slots(this.ctx);
+    this.maxSigsPerPackage = options.maxSigsPerPackage || DEFAULT_MAX_SIGS_PER_PACKAGE;
+    this.eagerPackages = options.eagerPackages === undefined ? DEFAULT_EAGER_PACKAGES : options.eagerPackages;
+    this.minSigsWhenBusy = options.minSigsWhenBusy || Math.max(1, Math.floor(this.maxSigsPerPackage / 4));
+    this.maxPendingSigs = options.maxPendingSigs || 4 * this.maxSigsPerPackage;
+    this.bufferWaitMs = options.bufferWaitMs === undefined ? MAX_BUFFER_WAIT_MS : options.bufferWaitMs;
     if (options.reserveSets && this.addon.reserve) {
       // preallocate every pipeline slot for packages of up to reserveSets sets (lsg_reserve)
       const pks = options.reservePubkeys || options.reserveSets;
       this.addon.reserve(this.ctx, options.reserveSets, pks, 32 * options.reserveSets, 0);
     }
-    this.jobs = [];
+    this.jobs = new Fifo(); // queued blocks (index.ts `jobs`, a block at a time)
+    this.priorityJobs = []; // blocks of non-batchable priority jobs: a stack, drained first
+    this.queuedJobs = 0;
+    this.queuedSigs = 0;
     this.bufferedJobs = null;
     this.closed = false;
     this.workersBusy = 0; // packages in flight (the reference's busy workers)
+    this.sigsInFlight = 0;
     this.inflight = new Set();
+    this.spare = []; // packed buffers of completed packages, reused
+    this.stats = {packages: 0, packageSigs: 0}; // packages submitted and their sets (bench, tests)
+    this.scheduled = false;
+    this.kick = false; // a package completed: the next dispatch goes out whatever its size
     this._runJob = this._runJob.bind(this);
     this._runBufferedJobs = this._runBufferedJobs.bind(this);
+    const m = this.metrics && this.metrics.blsThreadPool;
+    if (m && m.queueLength && m.workersBusy && typeof m.queueLength.addCollect === "function") {
+      // index.ts:135-140: sampled at scrape time
+      m.queueLength.addCollect(() => {
+        m.queueLength.set(this.queuedJobs);
+        m.workersBusy.set(this.workersBusy);
+      });
+    }
   }
 
   /** Mirror index2pubkey[firstIndex ..] into the device pubkey table (SURVEY 8f(1); call next
@@ -210,36 +475,48 @@ class BlsGpuVerifier {
     return this.addon.aggregateSignatures(this.ctx, groups);
   }
 
-  canAcceptWork() {
-    return this.workersBusy < this.poolSize && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
+  /** Sets not yet answered: queued, buffered and on the GPU. */
+  pendingSigs() {
+    return this.queuedSigs + (this.bufferedJobs ? this.bufferedJobs.sigCount : 0) + this.sigsInFlight;
   }
 
-  async verifySignatureSets(sets, opts = {}) {
-    if (this.metrics && this.metrics.bls) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
+  canAcceptWork() {
+    return this.pendingSigs() < this.maxPendingSigs;
+  }
 
-    if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
-      // verifySignatureSetsMaybeBatch on the calling thread: no retry, errors propagate
-      const m = this.metrics && this.metrics.blsThreadPool;
-      const timer = m ? m.mainThreadDurationInThreadPool.startTimer() : null;
-      try {
-        const r = this.addon.verifySets(this.ctx, sets.map(serializeSet), this.seed);
-        if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
-        return r.status === LSG_VALID;
-      } finally {
-        if (timer) timer();
+  verifySignatureSets(sets, opts = {}) {
+    try {
+      if (this.metrics && this.metrics.bls) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
+
+      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
+        // verifySignatureSetsMaybeBatch on the calling thread: no retry, errors propagate
+        const m = this.metrics && this.metrics.blsThreadPool;
+        const timer = m ? m.mainThreadDurationInThreadPool.startTimer() : null;
+        try {
+          const r = this.addon.verifySets(this.ctx, sets.map(serializeSet), this.seed);
+          if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
+          return Promise.resolve(r.status === LSG_VALID);
+        } finally {
+          if (timer) timer();
+        }
       }
-    }
 
-    const results = await Promise.all(
-      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((setsWorker) =>
-        this._queueBlsWork({opts, sets: setsWorker.map(serializeSet)})
-      )
-    );
-    // .every on an empty array returns true
-    if (results.length === 0) {
-      throw Error("Empty results array");
+      for (let i = 0; i < sets.length; i++) checkSet(sets[i]);
+      // one chunk (the common case: a gossip call carries one set): the AND over one job's
+      // boolean verdict is that verdict, so the job's own promise is the answer
+      if (sets.length <= MAX_SIGNATURE_SETS_PER_JOB) return this._queueBlsWork(opts, sets);
+      return Promise.all(
+        chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((setsWorker) => this._queueBlsWork(opts, setsWorker))
+      ).then((results) => {
+        // .every on an empty array returns true
+        if (results.length === 0) {
+          throw Error("Empty results array");
+        }
+        return results.every((isValid) => isValid === true);
+      });
+    } catch (e) {
+      return Promise.reject(e);
     }
-    return results.every((isValid) => isValid === true);
   }
 
   /**
@@ -248,112 +525,130 @@ class BlsGpuVerifier {
    * and, if that fails, re-verifies each set on its own (worker.ts:74-96).  A set whose
    * signature does not decode is reported false.
    */
-  async verifySignatureSetsSameMessage(sets, message, opts = {}) {
-    const jobs = sets.map((s) => ({
-      opts: {batchable: true, priority: opts.priority},
-      sets: [{pubkeys: [pubkeyBytes(s.publicKey)], message, signature: s.signature}],
-    }));
-    const verdicts = await Promise.all(
-      jobs.map((workReq) => this._queueBlsWork(workReq).catch(() => false))
+  verifySignatureSetsSameMessage(sets, message, opts = {}) {
+    const o = {batchable: true, priority: opts.priority};
+    return Promise.all(
+      sets.map((s) =>
+        this._queueBlsWork(o, [{type: SignatureSetType.single, pubkey: s.publicKey, signingRoot: message, signature: s.signature}]).catch(
+          () => false
+        )
+      )
     );
-    return verdicts;
   }
 
   async close() {
+    const aborted = new QueueError({code: QueueErrorCode.QUEUE_ABORTED});
     if (this.bufferedJobs) {
       clearTimeout(this.bufferedJobs.timeout);
-      for (const job of this.bufferedJobs.jobs) job.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
+      this.bufferedJobs.block.failAll(aborted);
+      this.bufferedJobs.block.seal();
       this.bufferedJobs = null;
     }
-    for (const job of this.jobs) {
-      job.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
-    }
-    this.jobs.splice(0, this.jobs.length);
+    for (const b of this.priorityJobs) b.failAll(aborted);
+    for (const b of this.jobs.drain()) b.failAll(aborted);
+    this.priorityJobs = [];
+    this.queuedJobs = 0;
+    this.queuedSigs = 0;
     this.closed = true;
     // let packages already on the GPU finish, then release the device context
-    await Promise.all(Array.from(this.inflight).map((p) => p.catch(() => undefined)));
+    await Promise.all(Array.from(this.inflight));
     if (this.ctx) {
       this.addon.close(this.ctx);
       this.ctx = null;
     }
   }
 
-  _queueBlsWork(workReq) {
+  _queueBlsWork(opts, sets) {
     if (this.closed) {
       return Promise.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
     }
-    return new Promise((resolve, reject) => {
-      const job = {resolve, reject, addedTimeMs: Date.now(), workReq};
-      if (workReq.opts.batchable) {
-        if (!this.bufferedJobs) {
-          this.bufferedJobs = {
-            jobs: [],
-            sigCount: 0,
-            firstPush: Date.now(),
-            timeout: setTimeout(this._runBufferedJobs, MAX_BUFFER_WAIT_MS),
-          };
-        }
-        if (workReq.opts.priority) this.bufferedJobs.jobs.unshift(job);
-        else this.bufferedJobs.jobs.push(job);
-        this.bufferedJobs.sigCount += job.workReq.sets.length;
-        if (this.bufferedJobs.sigCount > MAX_BUFFERED_SIGS) {
-          clearTimeout(this.bufferedJobs.timeout);
-          this._runBufferedJobs();
-        }
-      } else {
-        if (workReq.opts.priority) this.jobs.unshift(job);
-        else this.jobs.push(job);
-        setTimeout(this._runJob, 0);
+    const priority = opts.priority === true;
+    if (opts.batchable === true) {
+      let buf = this.bufferedJobs;
+      if (!buf) {
+        buf = this.bufferedJobs = {
+          sigCount: 0,
+          firstPush: Date.now(),
+          timeout: setTimeout(this._runBufferedJobs, this.bufferWaitMs),
+          block: new VerdictBlock(this.metrics !== null),
+        };
       }
-    });
+      const idx = buf.block.add(sets, JOB_BATCHABLE | (priority ? JOB_PRIORITY : 0), priority);
+      const p = buf.block.promise.then(PICK[idx]);
+      buf.sigCount += sets.length;
+      if (buf.sigCount > MAX_BUFFERED_SIGS || buf.block.sets.length >= MAX_JOBS_PER_BLOCK) {
+        clearTimeout(buf.timeout);
+        this._runBufferedJobs();
+      }
+      return p;
+    }
+    const block = new VerdictBlock(this.metrics !== null);
+    block.add(sets, priority ? JOB_PRIORITY : 0, false);
+    block.seal();
+    if (priority) this.priorityJobs.push(block);
+    else this.jobs.push(block);
+    this.queuedJobs++;
+    this.queuedSigs += sets.length;
+    this._schedule();
+    return block.promise.then(PICK[0]);
   }
 
-  async _runJob() {
-    if (this.closed) return;
-    if (this.workersBusy >= this.poolSize) return;
-    const jobs = this._prepareWork();
-    if (jobs.length === 0) return;
+  _schedule() {
+    // setImmediate, not the reference's setTimeout(0) (a >= 1 ms timer in node)
+    if (!this.scheduled) {
+      this.scheduled = true;
+      setImmediate(this._runJob);
+    }
+  }
 
+  _runJob() {
+    this.scheduled = false;
+    if (this.closed) return;
+    while (this.workersBusy < this.poolSize && this.queuedJobs > 0) {
+      // while the GPU is busy let the queue grow into a large package, unless a package has
+      // just completed (class comment)
+      if (this.workersBusy >= this.eagerPackages && this.queuedSigs < this.minSigsWhenBusy && !this.kick) break;
+      this.kick = false;
+      const blocks = this._prepareWork();
+      if (blocks.length === 0) break;
+      this._runPackage(blocks);
+    }
+  }
+
+  _runPackage(blocks) {
     const m = this.metrics && this.metrics.blsThreadPool;
     let startedSigSets = 0;
-    for (const job of jobs) {
-      if (m) m.jobWaitTime.observe((Date.now() - job.addedTimeMs) / 1000);
-      startedSigSets += job.workReq.sets.length;
+    let startedJobs = 0;
+    const now = m ? Date.now() : 0;
+    for (const b of blocks) {
+      startedSigSets += b.nSigs;
+      startedJobs += b.sets.length;
+      if (m) for (const t of b.added) m.jobWaitTime.observe((now - t) / 1000);
     }
     if (m) {
       m.totalJobsGroupsStarted.inc(1);
-      m.totalJobsStarted.inc(jobs.length);
+      m.totalJobsStarted.inc(startedJobs);
       m.totalSigSetsStarted.inc(startedSigSets);
     }
-
     this.workersBusy++;
+    this.sigsInFlight += startedSigSets;
+    this.stats.packages++;
+    this.stats.packageSigs += startedSigSets;
     const run = (async () => {
+      let pkg = null;
       try {
-        const pkg = jobs.map((job) => ({
-          sets: job.workReq.sets,
-          flags: (job.workReq.opts.batchable ? JOB_BATCHABLE : 0) | (job.workReq.opts.priority ? JOB_PRIORITY : 0),
-        }));
+        pkg = packBlocks(blocks, startedSigSets, this.spare.pop());
+        const n = pkg.jobBlock.length;
+        if (n === 0) return;
         const jobStartNs = process.hrtime.bigint();
-        const ticket = this.addon.submitJobs(this.ctx, pkg, this.seed);
-        if (ticket === null) throw Error("BlsGpuVerifier: every pipeline slot is busy");
-        const workResult = await this.addon.waitJobs(this.ctx, ticket);
+        const workResult = await this.addon.verifyPacked(this.ctx, pkg.arena, pkg.setDesc, pkg.jobDesc, this.seed);
         const jobEndNs = process.hrtime.bigint();
-        let successCount = 0;
+        const status = workResult.status;
+        const codes = workResult.errCode;
         let errorCount = 0;
-        for (let i = 0; i < jobs.length; i++) {
-          const job = jobs[i];
-          const r = workResult.results[i];
-          const n = job.workReq.sets.length;
-          if (!r) {
-            job.reject(Error(`No jobResult for index ${i}`));
-            errorCount += n;
-          } else if (r.status === LSG_ERROR) {
-            job.reject(Error(errorMessage(r.errCode)));
-            errorCount += n;
-          } else {
-            job.resolve(r.status === LSG_VALID);
-            successCount += n;
-          }
+        for (let i = 0; i < n; i++) {
+          if (status[i] === LSG_ERROR) errorCount += pkg.jobBlock[i].sets.length;
+          pkg.jobBlock[i].settle(pkg.jobIdx[i], status[i], codes[i]);
         }
         if (m) {
           // index.ts:362-381, with the GPU package in the worker's place
@@ -364,40 +659,55 @@ class BlsGpuVerifier {
           m.jobsWorkerTime.inc({workerId: workResult.workerId || 0}, workerJobTimeSec);
           m.latencyToWorker.observe(latencyToWorkerSec);
           m.latencyFromWorker.observe(latencyFromWorkerSec);
-          m.successJobsSignatureSetsCount.inc(successCount);
+          m.successJobsSignatureSetsCount.inc(pkg.nSigs - errorCount);
           m.errorJobsSignatureSetsCount.inc(errorCount);
           m.batchRetries.inc(workResult.batchRetries);
           m.batchSigsSuccess.inc(workResult.batchSigsSuccess);
         }
+        if (this.spare.length < 4) this.spare.push(pkg);
       } catch (e) {
         if (!this.closed && this.logger) this.logger.error("BlsGpuVerifier error", {}, e);
-        for (const job of jobs) job.reject(e);
+        for (const b of blocks) b.failAll(e);
       }
     })();
     this.inflight.add(run);
-    await run;
-    this.inflight.delete(run);
-    this.workersBusy--;
-    setTimeout(this._runJob, 0);
+    run.then(() => {
+      this.inflight.delete(run);
+      this.workersBusy--;
+      this.sigsInFlight -= startedSigSets;
+      this.kick = true;
+      this._schedule();
+    });
   }
 
+  /** blocks for one package: priority blocks first, then FIFO, up to maxSigsPerPackage sigs
+   * (a block is never split; index.ts:400-418 takes whole jobs the same way) */
   _prepareWork() {
-    const jobs = [];
+    const blocks = [];
     let totalSigs = 0;
+    let totalJobs = 0;
     while (totalSigs < this.maxSigsPerPackage) {
-      const job = this.jobs.shift();
-      if (!job) break;
-      jobs.push(job);
-      totalSigs += job.workReq.sets.length;
+      const b = this.priorityJobs.length ? this.priorityJobs.pop() : this.jobs.shift();
+      if (!b) break;
+      blocks.push(b);
+      totalSigs += b.nSigs;
+      totalJobs += b.sets.length;
     }
-    return jobs;
+    this.queuedSigs -= totalSigs;
+    this.queuedJobs -= totalJobs;
+    return blocks;
   }
 
   _runBufferedJobs() {
-    if (this.bufferedJobs) {
-      this.jobs.push(...this.bufferedJobs.jobs);
+    const buf = this.bufferedJobs;
+    if (buf) {
+      // the buffer goes to the tail of the queue as a whole (index.ts:425-431)
       this.bufferedJobs = null;
-      setTimeout(this._runJob, 0);
+      buf.block.seal();
+      this.jobs.push(buf.block);
+      this.queuedJobs += buf.block.sets.length;
+      this.queuedSigs += buf.block.nSigs;
+      this._schedule();
     }
   }
 }
@@ -466,6 +776,8 @@ module.exports = {
   SignatureSetType,
   chunkifyMaximizeChunkSize,
   errorMessage,
+  packBlocks,
+  DEFAULT_MAX_SIGS_PER_PACKAGE,
   MAX_SIGNATURE_SETS_PER_JOB,
   MAX_BUFFERED_SIGS,
   MAX_BUFFER_WAIT_MS,

@@ -6,9 +6,11 @@
  * (/root/reference/packages/beacon-node/src/chain/bls/multithread/index.ts).  Where the
  * reference posts BlsWorkReq[] packages to @chainsafe/threads workers running
  * @chainsafe/blst (multithread/worker.ts:30-106), the verifier hands each package to
- * submitJobs() (inputs copied into pinned staging memory before it returns) and awaits
- * waitJobs(), whose blocking part runs on a libuv pool thread (napi_create_async_work), so
- * the JS main thread never blocks on the GPU.  Nothing here does arithmetic.
+ * verifyPacked(): one of the context's own package threads submits it (lsg_submit_jobs copies
+ * the inputs into pinned staging) and blocks in lsg_wait_jobs; the verdicts return to the JS
+ * thread through a napi_threadsafe_function.  Neither the JS main thread nor libuv's thread
+ * pool (the beacon node's file and DB I/O runs there) ever blocks on the GPU.  Nothing here
+ * does arithmetic.
  *
  * JS surface (all synchronous unless noted):
  *   open(device | devices[]) -> ctx         lsg_init / lsg_init_devices (one context over the
@@ -18,14 +20,13 @@
  *   close(ctx)                              lsg_destroy
  *   slots(ctx) -> n                         lsg_pipeline_slots
  *   deviceName(ctx) -> string               lsg_device_name
- *   submitJobs(ctx, jobs, seed) -> ticket | null (every slot busy)     lsg_submit_jobs
- *       jobs = [{sets: [{pubkeys: Uint8Array[], message: Uint8Array, signature: Uint8Array}],
- *                flags: number}]
- *   waitJobs(ctx, ticket) -> Promise<{results: [{status, errCode}], batchRetries,
- *                                     batchSigsSuccess, startNs, endNs, finalExps,
- *                                     workerId}>   lsg_wait_jobs
- *       startNs / endNs are CLOCK_MONOTONIC nanoseconds (process.hrtime.bigint()'s clock);
- *       workerId is the pipeline slot that ran the package (the reference's workerId label)
+ *   verifyPacked(ctx, arena, setDesc, jobDesc, seed) -> Promise<{status: Uint8Array,
+ *       errCode: Int32Array, batchRetries, batchSigsSuccess, startNs, endNs, finalExps,
+ *       submitUs, keyError, workerId}>     lsg_submit_jobs + lsg_wait_jobs on a package thread
+ *       (layout below, at js_verify_packed).  startNs / endNs are CLOCK_MONOTONIC nanoseconds
+ *       (process.hrtime.bigint()'s clock); workerId is the pipeline slot that ran the package
+ *       (the reference's workerId label)
+ *   sign(ctx, sks, msgs) / skToPk(ctx, sks)  test and bench input generation
  *   verifySets(ctx, sets, seed) -> {status, errCode}                   lsg_verify_sets
  *   aggregatePubkeys(ctx, pubkeys[]) -> {errCode, bytes: Uint8Array(96)} lsg_aggregate_pubkeys
  *   pubkeyTableSet(ctx, firstIndex, pubkeys[]) -> errCodes[]          lsg_pubkey_table_set
@@ -56,13 +57,17 @@ static napi_value throw_lsg(napi_env env, lsg_ctx* ctx, const char* what, int rc
   return NULL;
 }
 
+/* the external of a context is an addon_ctx (defined with the package engine below) whose
+ * first member is the lsg_ctx (NULL once closed) */
 static lsg_ctx* get_ctx(napi_env env, napi_value v) {
   void* p = NULL;
   if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
     napi_throw_type_error(env, NULL, "lsg_napi: expected a context from open()");
     return NULL;
   }
-  return (lsg_ctx*)p;
+  lsg_ctx* c = *(lsg_ctx**)p;
+  if (!c) napi_throw_error(env, NULL, "lsg_napi: the context is closed");
+  return c;
 }
 
 /* Uint8Array (or Buffer) -> pointer + length; returns 0 on success */
@@ -219,57 +224,6 @@ static napi_value make_result(napi_env env, const lsg_job_result* r) {
   return o;
 }
 
-/* ------------------------------------------------------------------ open / close */
-static void finalize_noop(napi_env env, void* data, void* hint) {
-  (void)env;
-  (void)data;
-  (void)hint;
-}
-
-static napi_value js_open(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  lsg_ctx* ctx = NULL;
-  int rc;
-  bool is_arr = false;
-  if (argc >= 1) napi_is_array(env, argv[0], &is_arr);
-  if (is_arr) {
-    uint32_t n = array_len(env, argv[0]);
-    if (n == 0 || n > 64) {
-      napi_throw_range_error(env, NULL, "lsg_napi: open() expects 1..64 device ids");
-      return NULL;
-    }
-    int ids[64];
-    for (uint32_t k = 0; k < n; k++) {
-      napi_value e;
-      napi_get_element(env, argv[0], k, &e);
-      int32_t d = 0;
-      napi_get_value_int32(env, e, &d);
-      ids[k] = d;
-    }
-    rc = lsg_init_devices(ids, (int)n, &ctx);
-  } else {
-    int32_t dev = 0;
-    if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
-    rc = lsg_init(dev, &ctx);
-  }
-  if (rc != LSG_OK) return throw_lsg(env, NULL, "lsg_init (no gfx950 device?)", rc);
-  napi_value ext;
-  NAPI_CALL(env, napi_create_external(env, ctx, finalize_noop, NULL, &ext));
-  return ext;
-}
-
-static napi_value js_close(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  lsg_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
-  lsg_destroy(ctx);
-  return NULL;
-}
-
 static napi_value js_reserve(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
@@ -321,127 +275,327 @@ static napi_value js_device_name(napi_env env, napi_callback_info info) {
   return s;
 }
 
-/* ------------------------------------------------------------------ jobs */
-static napi_value js_submit_jobs(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  lsg_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
-  uint32_t nj = array_len(env, argv[1]);
-  if (nj == UINT32_MAX) {
-    napi_throw_type_error(env, NULL, "lsg_napi: jobs must be an array");
-    return NULL;
-  }
-  double seedd = 0;
-  if (argc >= 3) napi_get_value_double(env, argv[2], &seedd);
-  lsg_job* jobs = (lsg_job*)calloc(nj ? nj : 1, sizeof(lsg_job));
-  set_view* views = (set_view*)calloc(nj ? nj : 1, sizeof(set_view));
-  napi_value ret = NULL;
-  uint32_t built = 0;
-  for (; built < nj; built++) {
-    napi_value j;
-    napi_get_element(env, argv[1], built, &j);
-    napi_value sets = get_prop(env, j, "sets"), flags = get_prop(env, j, "flags");
-    uint32_t f = 0;
-    if (flags) napi_get_value_uint32(env, flags, &f);
-    if (!sets || view_sets(env, sets, &views[built])) goto out;
-    jobs[built].sets = views[built].sets;
-    jobs[built].n_sets = (uint32_t)views[built].n_sets;
-    jobs[built].flags = f;
-  }
-  {
-    lsg_ticket t = 0;
-    int rc = lsg_submit_jobs(ctx, jobs, nj, (uint64_t)seedd, &t);
-    if (rc == LSG_ERR_BUSY) {
-      napi_get_null(env, &ret);
-    } else if (rc != LSG_OK) {
-      throw_lsg(env, ctx, "lsg_submit_jobs", rc);
-    } else {
-      /* tickets are serial << 16 | kind << 8 | slot: exact in a double for 2^37 submissions */
-      napi_value o;
-      napi_create_object(env, &o);
-      set_int(env, o, "ticket", (int64_t)t);
-      set_int(env, o, "nJobs", nj);
-      ret = o;
-    }
-  }
-out:
-  for (uint32_t k = 0; k < built && k < nj; k++) view_free(&views[k]);
-  free(views);
-  free(jobs);
-  return ret;
-}
+/* ------------------------------------------------------------------ packages (async engine)
+ * verifyPacked(ctx, arena, setDesc, jobDesc, seed) -> Promise<result>
+ *   arena    Uint8Array: every byte of the package's sets (keys, messages, signatures)
+ *   setDesc  Uint32Array, 7 words per set: pkOff, pkLen (48|96|4 = index), nPks, msgOff,
+ *            msgLen, sigOff, sigLen (offsets into arena; sets in job order)
+ *   jobDesc  Uint32Array, 2 words per job: nSets, flags (LSG_JOB_*)
+ *   result   {status: Uint8Array(nJobs), errCode: Int32Array(nJobs), batchRetries,
+ *             batchSigsSuccess, startNs, endNs, finalExps, submitUs, keyError, workerId}
+ * The call returns at once.  One of the context's package threads (native, not libuv's pool)
+ * builds the lsg_job list over the arena, calls lsg_submit_jobs (the inputs are copied into
+ * pinned staging there) and blocks in lsg_wait_jobs; the verdicts come back to the JS thread
+ * through a napi_threadsafe_function, which resolves the promise.  The JS buffers are held by
+ * references until then and must not be modified by the caller.  The JS thread never blocks
+ * on the GPU and never stages bytes: it only packs the arena (the role of the structured
+ * clone of multithread/index.ts:335) and resolves per-job promises. */
+#include <pthread.h>
 
-typedef struct {
-  napi_async_work work;
+#define LSG_NAPI_THREADS 16 /* package threads per context: one outstanding package each */
+
+typedef struct pkg_req {
+  struct pkg_req* next;
   napi_deferred deferred;
-  lsg_ctx* ctx;
+  napi_ref refs[3]; /* arena, setDesc, jobDesc: kept alive until the promise settles */
+  const uint8_t* arena;
+  size_t arena_len;
+  const uint32_t* sdesc;
+  const uint32_t* jdesc;
+  uint32_t n_sets, n_jobs;
+  uint64_t seed;
   lsg_ticket ticket;
-  uint32_t n;
   lsg_job_result* results;
   lsg_stats stats;
   int rc;
-  char err[256];
-} wait_req;
+  char err[320];
+} pkg_req;
 
-static void wait_execute(napi_env env, void* data) {
-  (void)env;
-  wait_req* w = (wait_req*)data;
-  w->rc = lsg_wait_jobs(w->ctx, w->ticket, w->results, &w->stats);
-  if (w->rc) snprintf(w->err, sizeof w->err, "lsg_wait_jobs failed (status %d): %s", w->rc, lsg_last_error(w->ctx));
-}
+typedef struct {
+  lsg_ctx* c;
+  /* engine (started by the first verifyPacked) */
+  int started, stop, n_threads;
+  pthread_t th[LSG_NAPI_THREADS];
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  pkg_req *head, *tail;
+  napi_threadsafe_function tsfn;
+  uint32_t pending; /* promises not yet settled (JS thread only) */
+} addon_ctx;
 
-static void wait_complete(napi_env env, napi_status status, void* data) {
-  wait_req* w = (wait_req*)data;
-  if (status != napi_ok || w->rc != LSG_OK) {
-    napi_value msg, err;
-    napi_create_string_utf8(env, w->rc ? w->err : "lsg_napi: async wait cancelled", NAPI_AUTO_LENGTH, &msg);
-    napi_create_error(env, NULL, msg, &err);
-    napi_reject_deferred(env, w->deferred, err);
-  } else {
-    napi_value o, arr;
-    napi_create_object(env, &o);
-    napi_create_array_with_length(env, w->n, &arr);
-    for (uint32_t i = 0; i < w->n; i++) napi_set_element(env, arr, i, make_result(env, &w->results[i]));
-    napi_set_named_property(env, o, "results", arr);
-    set_int(env, o, "batchRetries", w->stats.batch_retries);
-    set_int(env, o, "batchSigsSuccess", w->stats.batch_sigs_success);
-    set_int(env, o, "startNs", (int64_t)w->stats.start_ns);
-    set_int(env, o, "endNs", (int64_t)w->stats.end_ns);
-    set_int(env, o, "finalExps", w->stats.n_final_exps);
-    set_int(env, o, "workerId", (int64_t)(w->ticket & 0xff));
-    napi_resolve_deferred(env, w->deferred, o);
-  }
-  napi_delete_async_work(env, w->work);
-  free(w->results);
-  free(w);
-}
-
-static napi_value js_wait_jobs(napi_env env, napi_callback_info info) {
-  size_t argc = 2;
-  napi_value argv[2];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  lsg_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
-  napi_value tv = get_prop(env, argv[1], "ticket"), nv = get_prop(env, argv[1], "nJobs");
-  double t = 0;
-  uint32_t n = 0;
-  if (!tv || !nv || napi_get_value_double(env, tv, &t) != napi_ok || napi_get_value_uint32(env, nv, &n) != napi_ok) {
-    napi_throw_type_error(env, NULL, "lsg_napi: waitJobs expects the object submitJobs returned");
+static addon_ctx* get_actx(napi_env env, napi_value v) {
+  void* p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "lsg_napi: expected a context from open()");
     return NULL;
   }
-  wait_req* w = (wait_req*)calloc(1, sizeof(wait_req));
-  w->ctx = ctx;
-  w->ticket = (lsg_ticket)t;
-  w->n = n;
-  w->results = (lsg_job_result*)calloc(n ? n : 1, sizeof(lsg_job_result));
-  napi_value promise, name;
-  NAPI_CALL(env, napi_create_promise(env, &w->deferred, &promise));
-  NAPI_CALL(env, napi_create_string_utf8(env, "lsg_wait_jobs", NAPI_AUTO_LENGTH, &name));
-  NAPI_CALL(env, napi_create_async_work(env, NULL, name, wait_execute, wait_complete, w, &w->work));
-  NAPI_CALL(env, napi_queue_async_work(env, w->work));
+  return (addon_ctx*)p;
+}
+
+/* the sets of a package over the arena; returns 0 or an LSG_ERR_* (bounds are checked here:
+ * a descriptor naming bytes outside the arena is an argument error, never a wild read) */
+static int build_jobs(pkg_req* r, lsg_set** sets_out, lsg_job** jobs_out) {
+  lsg_set* sets = (lsg_set*)calloc(r->n_sets ? r->n_sets : 1, sizeof(lsg_set));
+  lsg_job* jobs = (lsg_job*)calloc(r->n_jobs ? r->n_jobs : 1, sizeof(lsg_job));
+  if (!sets || !jobs) {
+    free(sets);
+    free(jobs);
+    return LSG_ERR_NOMEM;
+  }
+  const uint64_t L = r->arena_len;
+  for (uint32_t i = 0; i < r->n_sets; i++) {
+    const uint32_t* d = r->sdesc + 7 * (size_t)i;
+    lsg_set* q = &sets[i];
+    const uint64_t pk_bytes = (uint64_t)d[1] * d[2];
+    if ((uint64_t)d[0] + pk_bytes > L || (uint64_t)d[3] + d[4] > L || (uint64_t)d[5] + d[6] > L) {
+      free(sets);
+      free(jobs);
+      return LSG_ERR_INVALID_ARG;
+    }
+    q->pks = r->arena + d[0];
+    q->pk_len = d[1];
+    q->n_pks = d[2];
+    q->msg = r->arena + d[3];
+    q->msg_len = d[4];
+    q->sig = r->arena + d[5];
+    q->sig_len = d[6];
+  }
+  uint64_t pos = 0;
+  for (uint32_t j = 0; j < r->n_jobs; j++) {
+    jobs[j].n_sets = r->jdesc[2 * (size_t)j];
+    jobs[j].flags = r->jdesc[2 * (size_t)j + 1];
+    jobs[j].sets = sets + pos;
+    pos += jobs[j].n_sets;
+  }
+  if (pos != r->n_sets) {
+    free(sets);
+    free(jobs);
+    return LSG_ERR_INVALID_ARG;
+  }
+  *sets_out = sets;
+  *jobs_out = jobs;
+  return LSG_OK;
+}
+
+static void* engine_main(void* arg) {
+  addon_ctx* a = (addon_ctx*)arg;
+  for (;;) {
+    pthread_mutex_lock(&a->mu);
+    while (!a->head && !a->stop) pthread_cond_wait(&a->cv, &a->mu);
+    pkg_req* r = a->head;
+    if (!r) { /* stopping and drained */
+      pthread_mutex_unlock(&a->mu);
+      break;
+    }
+    a->head = r->next;
+    if (!a->head) a->tail = NULL;
+    pthread_mutex_unlock(&a->mu);
+    lsg_set* sets = NULL;
+    lsg_job* jobs = NULL;
+    r->rc = build_jobs(r, &sets, &jobs);
+    if (r->rc == LSG_OK) {
+      /* at most LSG_NAPI_THREADS <= lsg_pipeline_slots packages are outstanding per context,
+       * so BUSY only means another host thread of this process shares the context: back off */
+      for (int tries = 0;; tries++) {
+        r->rc = lsg_submit_jobs(a->c, jobs, r->n_jobs, r->seed, &r->ticket);
+        if (r->rc != LSG_ERR_BUSY || tries > 100000) break;
+        struct timespec ts = {0, 200000};
+        nanosleep(&ts, NULL);
+      }
+      if (r->rc == LSG_OK) r->rc = lsg_wait_jobs(a->c, r->ticket, r->results, &r->stats);
+    }
+    if (r->rc) snprintf(r->err, sizeof r->err, "lsg_submit_jobs/lsg_wait_jobs failed (status %d): %s", r->rc, lsg_last_error(a->c));
+    free(sets);
+    free(jobs);
+    napi_call_threadsafe_function(a->tsfn, r, napi_tsfn_blocking);
+  }
+  return NULL;
+}
+
+/* JS thread: settle one package's promise */
+static void engine_deliver(napi_env env, napi_value js_cb, void* context, void* data) {
+  (void)js_cb;
+  addon_ctx* a = (addon_ctx*)context;
+  pkg_req* r = (pkg_req*)data;
+  if (env) {
+    if (r->rc != LSG_OK) {
+      napi_value msg, err;
+      napi_create_string_utf8(env, r->err, NAPI_AUTO_LENGTH, &msg);
+      napi_create_error(env, NULL, msg, &err);
+      napi_reject_deferred(env, r->deferred, err);
+    } else {
+      napi_value o, st, ec, ab;
+      void* p;
+      napi_create_object(env, &o);
+      napi_create_arraybuffer(env, r->n_jobs ? r->n_jobs : 1, &p, &ab);
+      for (uint32_t i = 0; i < r->n_jobs; i++) ((uint8_t*)p)[i] = (uint8_t)r->results[i].status;
+      napi_create_typedarray(env, napi_uint8_array, r->n_jobs, ab, 0, &st);
+      napi_create_arraybuffer(env, 4 * (size_t)(r->n_jobs ? r->n_jobs : 1), &p, &ab);
+      for (uint32_t i = 0; i < r->n_jobs; i++) ((int32_t*)p)[i] = r->results[i].err_code;
+      napi_create_typedarray(env, napi_int32_array, r->n_jobs, ab, 0, &ec);
+      napi_set_named_property(env, o, "status", st);
+      napi_set_named_property(env, o, "errCode", ec);
+      set_int(env, o, "batchRetries", r->stats.batch_retries);
+      set_int(env, o, "batchSigsSuccess", r->stats.batch_sigs_success);
+      set_int(env, o, "startNs", (int64_t)r->stats.start_ns);
+      set_int(env, o, "endNs", (int64_t)r->stats.end_ns);
+      set_int(env, o, "finalExps", r->stats.n_final_exps);
+      set_int(env, o, "submitUs", r->stats.submit_us);
+      set_int(env, o, "keyError", r->stats.key_error);
+      set_int(env, o, "workerId", (int64_t)(r->ticket & 0xff));
+      napi_resolve_deferred(env, r->deferred, o);
+    }
+    for (int k = 0; k < 3; k++)
+      if (r->refs[k]) napi_delete_reference(env, r->refs[k]);
+    if (a->pending && --a->pending == 0) napi_unref_threadsafe_function(env, a->tsfn);
+  }
+  free(r->results);
+  free(r);
+}
+
+static int engine_start(napi_env env, addon_ctx* a) {
+  if (a->started) return 0;
+  napi_value name;
+  if (napi_create_string_utf8(env, "lsg_packages", NAPI_AUTO_LENGTH, &name) != napi_ok) return -1;
+  if (napi_create_threadsafe_function(env, NULL, NULL, name, 0, 1, NULL, NULL, a, engine_deliver, &a->tsfn) != napi_ok)
+    return -1;
+  napi_unref_threadsafe_function(env, a->tsfn); /* an idle verifier does not keep node alive */
+  pthread_mutex_init(&a->mu, NULL);
+  pthread_cond_init(&a->cv, NULL);
+  int32_t slots = LSG_NAPI_THREADS;
+  lsg_pipeline_slots(a->c, &slots);
+  a->n_threads = slots < LSG_NAPI_THREADS ? slots : LSG_NAPI_THREADS;
+  a->started = 1;
+  for (int i = 0; i < a->n_threads; i++) pthread_create(&a->th[i], NULL, engine_main, a);
+  return 0;
+}
+
+/* join the package threads (every promise has settled: BlsGpuVerifier.close awaits them) */
+static void engine_stop(addon_ctx* a) {
+  if (!a->started) return;
+  pthread_mutex_lock(&a->mu);
+  a->stop = 1;
+  pthread_cond_broadcast(&a->cv);
+  pthread_mutex_unlock(&a->mu);
+  for (int i = 0; i < a->n_threads; i++) pthread_join(a->th[i], NULL);
+  napi_release_threadsafe_function(a->tsfn, napi_tsfn_release);
+  pthread_mutex_destroy(&a->mu);
+  pthread_cond_destroy(&a->cv);
+  a->started = 0;
+}
+
+static int typed_info(napi_env env, napi_value v, napi_typedarray_type want, void** data, size_t* n) {
+  bool is_ta = false;
+  napi_typedarray_type t;
+  napi_value ab;
+  size_t off;
+  if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return -1;
+  if (napi_get_typedarray_info(env, v, &t, n, data, &ab, &off) != napi_ok || t != want) return -1;
+  return 0;
+}
+
+static napi_value js_verify_packed(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* a = get_actx(env, argv[0]);
+  if (!a) return NULL;
+  void *arena, *sd, *jd;
+  size_t na, ns, nj;
+  if (argc < 4 || typed_info(env, argv[1], napi_uint8_array, &arena, &na) ||
+      typed_info(env, argv[2], napi_uint32_array, &sd, &ns) || typed_info(env, argv[3], napi_uint32_array, &jd, &nj) ||
+      ns % 7 || nj % 2) {
+    napi_throw_type_error(env, NULL, "lsg_napi: verifyPacked(ctx, arena: Uint8Array, setDesc: Uint32Array(7n), jobDesc: Uint32Array(2m), seed)");
+    return NULL;
+  }
+  double seedd = 0;
+  if (argc >= 5) napi_get_value_double(env, argv[4], &seedd);
+  if (engine_start(env, a)) {
+    napi_throw_error(env, NULL, "lsg_napi: could not start the package threads");
+    return NULL;
+  }
+  pkg_req* r = (pkg_req*)calloc(1, sizeof(pkg_req));
+  r->arena = (const uint8_t*)arena;
+  r->arena_len = na;
+  r->sdesc = (const uint32_t*)sd;
+  r->jdesc = (const uint32_t*)jd;
+  r->n_sets = (uint32_t)(ns / 7);
+  r->n_jobs = (uint32_t)(nj / 2);
+  r->seed = (uint64_t)seedd;
+  r->results = (lsg_job_result*)calloc(r->n_jobs ? r->n_jobs : 1, sizeof(lsg_job_result));
+  for (int k = 0; k < 3; k++) napi_create_reference(env, argv[1 + k], 1, &r->refs[k]);
+  napi_value promise;
+  NAPI_CALL(env, napi_create_promise(env, &r->deferred, &promise));
+  if (a->pending++ == 0) napi_ref_threadsafe_function(env, a->tsfn);
+  pthread_mutex_lock(&a->mu);
+  if (a->tail)
+    a->tail->next = r;
+  else
+    a->head = r;
+  a->tail = r;
+  pthread_cond_signal(&a->cv);
+  pthread_mutex_unlock(&a->mu);
   return promise;
+}
+
+/* ------------------------------------------------------------------ open / close */
+static void engine_stop(addon_ctx* a);
+static void finalize_actx(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  addon_ctx* a = (addon_ctx*)data;
+  if (!a->c && !a->started) free(a); /* an unclosed context lives until the process exits */
+}
+
+static napi_value js_open(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = NULL;
+  int rc;
+  bool is_arr = false;
+  /* the package threads sleep on the completion events instead of spinning (the library's
+   * LSG_BLOCKING_WAITS; an explicit setting in the environment wins) */
+  setenv("LSG_BLOCKING_WAITS", "1", 0);
+  if (argc >= 1) napi_is_array(env, argv[0], &is_arr);
+  if (is_arr) {
+    uint32_t n = array_len(env, argv[0]);
+    if (n == 0 || n > 64) {
+      napi_throw_range_error(env, NULL, "lsg_napi: open() expects 1..64 device ids");
+      return NULL;
+    }
+    int ids[64];
+    for (uint32_t k = 0; k < n; k++) {
+      napi_value e;
+      napi_get_element(env, argv[0], k, &e);
+      int32_t d = 0;
+      napi_get_value_int32(env, e, &d);
+      ids[k] = d;
+    }
+    rc = lsg_init_devices(ids, (int)n, &ctx);
+  } else {
+    int32_t dev = 0;
+    if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
+    rc = lsg_init(dev, &ctx);
+  }
+  if (rc != LSG_OK) return throw_lsg(env, NULL, "lsg_init (no gfx950 device?)", rc);
+  addon_ctx* a = (addon_ctx*)calloc(1, sizeof(addon_ctx));
+  a->c = ctx;
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, a, finalize_actx, NULL, &ext));
+  return ext;
+}
+
+static napi_value js_close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* a = get_actx(env, argv[0]);
+  if (!a || !a->c) return NULL;
+  engine_stop(a);
+  lsg_destroy(a->c);
+  a->c = NULL;
+  return NULL;
 }
 
 static napi_value js_verify_sets(napi_env env, napi_callback_info info) {
@@ -679,6 +833,53 @@ static napi_value js_attestation_signing_roots(napi_env env, napi_callback_info 
   return out;
 }
 
+/* sign(ctx, sks: Uint8Array(32n, big-endian), msgs: Uint8Array(32n)) -> Uint8Array(96n) and
+ * skToPk(ctx, sks) -> Uint8Array(96n): test/bench input generation on the GPU (lsg_sign,
+ * lsg_sk_to_pk), not on the verify path */
+static napi_value js_sign(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  const uint8_t *k, *m;
+  size_t kl, ml;
+  if (argc < 3 || get_bytes(env, argv[1], &k, &kl) || get_bytes(env, argv[2], &m, &ml) || kl % 32 || ml != kl) {
+    napi_throw_type_error(env, NULL, "lsg_napi: sign(ctx, sks: 32n bytes, msgs: 32n bytes)");
+    return NULL;
+  }
+  const size_t n = kl / 32;
+  void* outp;
+  napi_value ab, out;
+  NAPI_CALL(env, napi_create_arraybuffer(env, 96 * (n ? n : 1), &outp, &ab));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, 96 * n, ab, 0, &out));
+  int rc = n ? lsg_sign(ctx, k, m, 32, n, (uint8_t*)outp) : LSG_OK;
+  if (rc) return throw_lsg(env, ctx, "lsg_sign", rc);
+  return out;
+}
+
+static napi_value js_sk_to_pk(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  lsg_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  const uint8_t* k;
+  size_t kl;
+  if (argc < 2 || get_bytes(env, argv[1], &k, &kl) || kl % 32) {
+    napi_throw_type_error(env, NULL, "lsg_napi: skToPk(ctx, sks: 32n bytes)");
+    return NULL;
+  }
+  const size_t n = kl / 32;
+  void* outp;
+  napi_value ab, out;
+  NAPI_CALL(env, napi_create_arraybuffer(env, 96 * (n ? n : 1), &outp, &ab));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, 96 * n, ab, 0, &out));
+  int rc = n ? lsg_sk_to_pk(ctx, k, n, (uint8_t*)outp) : LSG_OK;
+  if (rc) return throw_lsg(env, ctx, "lsg_sk_to_pk", rc);
+  return out;
+}
+
 /* ------------------------------------------------------------------ module */
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
@@ -688,8 +889,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"reserve", NULL, js_reserve, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceName", NULL, js_device_name, NULL, NULL, NULL, napi_enumerable, NULL},
-      {"submitJobs", NULL, js_submit_jobs, NULL, NULL, NULL, napi_enumerable, NULL},
-      {"waitJobs", NULL, js_wait_jobs, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"verifyPacked", NULL, js_verify_packed, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"sign", NULL, js_sign, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"skToPk", NULL, js_sk_to_pk, NULL, NULL, NULL, napi_enumerable, NULL},
       {"verifySets", NULL, js_verify_sets, NULL, NULL, NULL, napi_enumerable, NULL},
       {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, napi_enumerable, NULL},
       {"hashToG2", NULL, js_hash_to_g2, NULL, NULL, NULL, napi_enumerable, NULL},

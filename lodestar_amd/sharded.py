@@ -17,7 +17,9 @@ packages/beacon-node/src/chain/bls/multithread/types.ts:14-17) every rank:
 5. resolves its jobs with that node verdict (``backend.resolve``): when the node check fails,
    the rank's own package check (already computed on its GPU) localises, and only a failing
    rank runs the reference's chunk / per-job fallback (worker.ts:51-96).  Per-job verdicts
-   are all-gathered.
+   are all-gathered.  A key that does not deserialize on ANY rank rejects every job of the
+   package with the code of the first bad key in caller order (worker.ts:41-43), as on one
+   device.  The node verdict is advisory: a rank's own check of its share decides its jobs.
 
 Randomizers: seed 0 means the OS CSPRNG on every rank (production); a nonzero seed (tests)
 is offset per rank.
@@ -53,6 +55,7 @@ class ShardOutcome:
     results: list          # per job: (status, err_code)
     combined_ok: bool      # the one-final-exponentiation node check passed
     retried_ranks: list    # ranks that ran the reference's batch-retry fallback
+    rank_stats: list = None  # per rank: its BlsWorkResult counters for its own share
 
 
 class ShardedVerifier:
@@ -81,12 +84,23 @@ class ShardedVerifier:
         node_ok = self.backend.final_verify(parts)
         res, stats = self.backend.resolve(h, 1 if node_ok else 0)
         local = {j: tuple(r) for j, r in zip(mine, res)}
-        merged, retried = {}, []
-        for r, (loc, retries) in enumerate(self._all_gather((local, stats.get("batch_retries", 0)))):
-            if retries:
+        # a key that does not deserialize rejects the WHOLE package (worker.ts:41-43): the
+        # first bad key in caller job order over all ranks decides the code
+        kerr = stats.get("key_error", 0)
+        key = (mine[stats.get("key_error_job", 0)], kerr) if kerr else None
+        merged, retried, stats_all, key_errs = {}, [], [], []
+        for r, (loc, st, ke) in enumerate(self._all_gather((local, stats, key))):
+            if st.get("batch_retries", 0):
                 retried.append(r)
             merged.update(loc)
-        return ShardOutcome([merged[j] for j in range(len(jobs))], node_ok, retried)
+            stats_all.append(st)
+            if ke is not None:
+                key_errs.append(ke)
+        results = [merged[j] for j in range(len(jobs))]
+        if key_errs:
+            code = min(key_errs)[1]
+            results = [(ERROR, code)] * len(jobs)
+        return ShardOutcome(results, node_ok, retried, stats_all)
 
 
 class GpuBackend:

@@ -73,8 +73,34 @@ const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
   const sr = cases.signing_roots;
   const roots = pool.addon.attestationSigningRoots(pool.ctx, hex(sr.data), hex(sr.domain));
   assert.strictEqual(Buffer.from(roots).toString("hex"), sr.roots);
+  // the package engine at volume: 4096 single-set batchable gossip calls (one 32-byte secret
+  // key per set), 1% with a wrong message; gated on canAcceptWork like the gossip processor
+  const n = 4096;
+  const sks = Buffer.alloc(32 * n);
+  const msgs = Buffer.alloc(32 * n);
+  for (let i = 0; i < n; i++) {
+    sks.writeUInt32BE(i + 1, 32 * i + 28);
+    msgs.writeUInt32BE(0x5eed0000 + i, 32 * i);
+  }
+  const pks = pool.addon.skToPk(pool.ctx, sks);
+  const sigs = pool.addon.sign(pool.ctx, sks, msgs);
+  const wrong = new Set(Array.from({length: 41}, (_, k) => (k * 97 + 13) % n));
+  const vol = [];
+  for (let i = 0; i < n; i++) {
+    const m = wrong.has(i) ? msgs.subarray(32 * ((i + 1) % n), 32 * ((i + 1) % n) + 32) : msgs.subarray(32 * i, 32 * i + 32);
+    vol.push({type: V.SignatureSetType.single, pubkey: pks.subarray(96 * i, 96 * i + 96), signingRoot: m,
+              signature: sigs.subarray(96 * i, 96 * i + 96)});
+  }
+  const pv = [];
+  for (let i = 0; i < n; i++) {
+    while (!pool.canAcceptWork()) await sleep(1);
+    pv.push(pool.verifySignatureSets([vol[i]], {batchable: true}));
+  }
+  const verdicts = await Promise.all(pv);
+  verdicts.forEach((v, i) => assert.strictEqual(v, !wrong.has(i), `set ${i}`));
+  assert.ok(pool.stats.packages >= 1 && pool.stats.packageSigs >= n);
   await pool.close();
-  console.log("node host on GPU: all checks passed");
+  console.log("node host on GPU: all checks passed; packages", pool.stats.packages, "sets", pool.stats.packageSigs);
 })().catch((e) => {
   console.log("FAIL", e && e.stack);
   process.exit(1);

@@ -15,6 +15,23 @@ const assert = require("assert");
 const path = require("path");
 const V = require(path.join(__dirname, "..", "..", "lodestar_amd", "js", "blsGpuVerifier.js"));
 
+/** Decodes verifyPacked's arena / descriptors back into jobs (lsg_napi.c layout). */
+function unpack(arena, setDesc, jobDesc) {
+  const jobs = [];
+  let k = 0;
+  for (let j = 0; j < jobDesc.length / 2; j++) {
+    const sets = [];
+    for (let q = 0; q < jobDesc[2 * j]; q++, k++) {
+      const d = setDesc.subarray(7 * k, 7 * k + 7);
+      const pubkeys = [];
+      for (let p = 0; p < d[2]; p++) pubkeys.push(arena.slice(d[0] + p * d[1], d[0] + (p + 1) * d[1]));
+      sets.push({pubkeys, pkLen: d[1], message: arena.slice(d[3], d[3] + d[4]), signature: arena.slice(d[5], d[5] + d[6])});
+    }
+    jobs.push({sets, flags: jobDesc[2 * j + 1]});
+  }
+  return jobs;
+}
+
 function mockAddon(slots = 2, {holdWaits = false} = {}) {
   const m = {
     packages: [],
@@ -53,18 +70,25 @@ function mockAddon(slots = 2, {holdWaits = false} = {}) {
       }
       return {status: ok ? 1 : 0, errCode: 0};
     },
-    submitJobs(ctx, jobs, seed) {
-      if (m.pending.length >= slots) return null;
+    verifyPacked(ctx, arena, setDesc, jobDesc, seed) {
+      // the engine runs at most `slots` packages at once (one package thread each)
+      if (m.pending.length >= slots) throw Error("mock: more packages in flight than package threads");
+      const jobs = unpack(arena, setDesc, jobDesc);
       m.packages.push(jobs);
-      const t = {ticket: m.packages.length, nJobs: jobs.length, jobs};
+      const t = {ticket: m.packages.length, jobs};
       m.pending.push(t);
-      return t;
-    },
-    waitJobs(ctx, t) {
-      const results = t.jobs.map((j) => m.jobVerdict(j.sets));
+      const vs = jobs.map((j) => m.jobVerdict(j.sets));
       // GPU package start/end on process.hrtime's clock (lsg_stats is CLOCK_MONOTONIC)
       const startNs = Number(process.hrtime.bigint());
-      const done = {results, batchRetries: 0, batchSigsSuccess: 0, startNs, endNs: startNs + 1e6, workerId: t.ticket % 3};
+      const done = {
+        status: Uint8Array.from(vs.map((v) => v.status)),
+        errCode: Int32Array.from(vs.map((v) => v.errCode)),
+        batchRetries: 0,
+        batchSigsSuccess: 0,
+        startNs,
+        endNs: startNs + 1e6,
+        workerId: t.ticket % 3,
+      };
       const finish = () => {
         m.pending.splice(m.pending.indexOf(t), 1);
         return done;
@@ -184,9 +208,9 @@ test("> 128 sets are chunked (<= 128 per job) and the verdict is the AND over ch
   await pool.close();
 });
 
-test("a package holds at most 128 sigs of queued jobs (prepareWork, index.ts:400-418)", async () => {
+test("reference policy: a package holds at most 128 sigs of queued jobs (prepareWork, index.ts:400-418)", async () => {
   const a = mockAddon(1);
-  const pool = new V.BlsGpuVerifier({}, {addon: a});
+  const pool = new V.BlsGpuVerifier({maxSigsPerPackage: 128, eagerPackages: 1}, {addon: a});
   const sets100 = Array.from({length: 100}, (_, i) => set(i));
   const ps = [pool.verifySignatureSets(sets100), pool.verifySignatureSets(sets100), pool.verifySignatureSets(sets100)];
   assert.deepStrictEqual(await Promise.all(ps), [true, true, true]);
@@ -195,9 +219,9 @@ test("a package holds at most 128 sigs of queued jobs (prepareWork, index.ts:400
   await pool.close();
 });
 
-test("maxSigsPerPackage widens the package (GPU sizing) without changing verdicts", async () => {
+test("GPU sizing: one package takes every queued job (default 32768 sigs) without changing verdicts", async () => {
   const a = mockAddon(1);
-  const pool = new V.BlsGpuVerifier({maxSigsPerPackage: 4096}, {addon: a});
+  const pool = new V.BlsGpuVerifier({}, {addon: a});
   const sets100 = Array.from({length: 100}, (_, i) => set(i));
   const bad = Array.from({length: 100}, (_, i) => (i === 7 ? Object.assign({}, set(i), {signingRoot: new Uint8Array(32).fill(9)}) : set(i)));
   const ps = [pool.verifySignatureSets(sets100), pool.verifySignatureSets(bad), pool.verifySignatureSets(sets100)];
@@ -241,25 +265,82 @@ test("verifyOnMainThread runs synchronously through verifySets and throws errors
   await pool2.close();
 });
 
-test("canAcceptWork: false while every pipeline slot holds a package (index.ts:143-149)", async () => {
+test("canAcceptWork: back-pressure on sets pending (queued + buffered + in flight) (index.ts:143-149)", async () => {
   const a = mockAddon(2, {holdWaits: true});
-  const pool = new V.BlsGpuVerifier({}, {addon: a});
+  const pool = new V.BlsGpuVerifier({maxPendingSigs: 6}, {addon: a});
   assert.strictEqual(pool.canAcceptWork(), true);
-  const p1 = pool.verifySignatureSets([set(1)]);
+  const p1 = pool.verifySignatureSets([set(1), set(2)]);
+  const p2 = pool.verifySignatureSets([set(3), set(4)]);
   await sleep(2);
-  const p2 = pool.verifySignatureSets([set(2)]);
-  await sleep(2);
-  assert.strictEqual(a.pending.length, 2);
+  assert.strictEqual(a.packages.length, 1, "both jobs queued in one tick go as one package");
+  assert.strictEqual(pool.pendingSigs(), 4);
+  assert.strictEqual(pool.canAcceptWork(), true);
+  const p3 = pool.verifySignatureSets([set(5)], {batchable: true}); // buffered: counts too
+  const p4 = pool.verifySignatureSets([set(6)], {batchable: true});
+  assert.strictEqual(pool.pendingSigs(), 6);
   assert.strictEqual(pool.canAcceptWork(), false);
-  const p3 = pool.verifySignatureSets([set(3)]); // queued, no slot
-  await sleep(2);
-  assert.strictEqual(a.packages.length, 2);
   a.pending[0].release();
   await sleep(5);
+  assert.strictEqual(pool.pendingSigs(), 2);
+  assert.strictEqual(pool.canAcceptWork(), true);
+  assert.deepStrictEqual(await Promise.all([p1, p2]), [true, true]);
+  await sleep(120); // buffer timer: the two batchable jobs go out as one package
+  for (const t of a.pending.slice()) t.release();
+  assert.deepStrictEqual(await Promise.all([p3, p4]), [true, true]);
+  assert.strictEqual(pool.pendingSigs(), 0);
+  await pool.close();
+});
+
+test("GPU package policy: eager packages while the GPU is idle, then the queue grows into large packages", async () => {
+  const a = mockAddon(16, {holdWaits: true});
+  const pool = new V.BlsGpuVerifier({maxSigsPerPackage: 1000, eagerPackages: 2, minSigsWhenBusy: 250}, {addon: a});
+  const ps = [];
+  ps.push(pool.verifySignatureSets([set(1)]));
+  await sleep(2);
+  ps.push(pool.verifySignatureSets([set(2)]));
+  await sleep(2);
+  assert.deepStrictEqual(a.packages.map((p) => p.length), [1, 1], "two eager one-job packages");
+  for (let i = 0; i < 100; i++) ps.push(pool.verifySignatureSets([set(i % 7)]));
+  await sleep(2);
+  assert.strictEqual(a.packages.length, 2, "100 queued sigs < minSigsWhenBusy: held while 2 packages run");
+  for (let i = 0; i < 200; i++) ps.push(pool.verifySignatureSets([set(i % 7)]));
+  await sleep(2);
+  assert.deepStrictEqual(a.packages.map((p) => p.length), [1, 1, 300], "300 >= 250 queued sigs: one package");
+  for (let i = 0; i < 10; i++) ps.push(pool.verifySignatureSets([set(i % 7)]));
+  await sleep(2);
+  assert.strictEqual(a.packages.length, 3);
+  a.pending[0].release(); // a package completes: the queue goes out at once
+  await sleep(3);
+  assert.deepStrictEqual(a.packages.map((p) => p.length), [1, 1, 300, 10]);
+  for (let i = 0; i < 2500; i++) ps.push(pool.verifySignatureSets([set(i % 7)]));
+  await sleep(3);
+  // 2500 queued: packages of at most maxSigsPerPackage sigs
+  assert.deepStrictEqual(a.packages.slice(4).map((p) => p.length), [1000, 1000, 500]);
+  while (a.pending.length) {
+    for (const t of a.pending.slice()) t.release();
+    await sleep(2);
+  }
+  const res = await Promise.all(ps);
+  assert.strictEqual(res.length, 2812);
+  assert.ok(res.every((r) => r === true));
+  await pool.close();
+});
+
+test("at most one package per package thread (addon.slots) is in flight", async () => {
+  const a = mockAddon(2, {holdWaits: true});
+  const pool = new V.BlsGpuVerifier({eagerPackages: 8}, {addon: a});
+  const ps = [];
+  for (let i = 0; i < 3; i++) {
+    ps.push(pool.verifySignatureSets([set(i)]));
+    await sleep(2);
+  }
+  assert.strictEqual(a.pending.length, 2);
+  assert.strictEqual(a.packages.length, 2);
+  a.pending[0].release();
+  await sleep(3);
   assert.strictEqual(a.packages.length, 3, "freed slot picks up the queued job");
   for (const t of a.pending.slice()) t.release();
-  assert.deepStrictEqual(await Promise.all([p1, p2, p3]), [true, true, true]);
-  assert.strictEqual(pool.canAcceptWork(), true);
+  assert.deepStrictEqual(await Promise.all(ps), [true, true, true]);
   await pool.close();
 });
 

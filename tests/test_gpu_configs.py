@@ -311,3 +311,51 @@ def test_fused_miller_matches_split(ctx, keys, n, monkeypatch):
     assert "k_miller_fused" in names and "k_miller_lines" not in names
     assert fused == split
     assert ctx.verify_sets(sets) == (1, 0)
+
+
+def test_fresh_context_mostly_invalid_single_jobs(keys):
+    """the per-job phase of a package whose retried jobs outnumber phase A's
+    fallback buffer (single-set batchable jobs, most of them invalid) on a context that never
+    called lsg_reserve -- verdicts and counters against the C oracle."""
+    from lodestar_amd._native import Context
+    for n, frac in ((32, 0.75), (200, 0.7)):
+        c = Context(0)
+        try:
+            sets = single_sets(c, keys, b"mostbad%d" % n, n)
+            bad = [bd.corrupt_wrong_message(s) if (i * 7919) % 100 < frac * 100 else s for i, s in enumerate(sets)]
+            per = oracle_each(bad)
+            assert per.count(0) >= n // 2
+            check_against_oracle(c, [([s], 1) for s in bad], per)
+            # two bad signatures in different 16-job chunks of an otherwise valid package
+            two = list(sets)
+            for i in (3, n - 2):
+                two[i] = bd.corrupt_wrong_message(two[i])
+            check_against_oracle(c, [([s], 1) for s in two], oracle_each(two))
+        finally:
+            c.close()
+
+
+def test_multi_device_bad_key_rejects_package(keys):
+    """a key that does not deserialize on device 1 of a [0, 0] context
+    rejects EVERY job of the package (worker.ts:41-43 throws out of verifyManySignatureSets),
+    with the first bad key's code in caller order, exactly as on one device."""
+    from lodestar_amd._native import Context
+    c1 = Context(0)
+    c2 = Context(devices=[0, 0])
+    try:
+        sets = single_sets(c1, keys, b"badkey", 64)
+        jobs = [([s], 1) for s in sets[:32]] + [(sets[32 + 2 * k:34 + 2 * k], 1 if k % 3 else 0) for k in range(16)]
+        pk = bytearray(jobs[40][0][0][0][0])
+        pk[95] ^= 1  # off the curve: BLST_POINT_NOT_ON_CURVE
+        s0 = jobs[40][0][0]
+        jobs[40] = ([([bytes(pk)], s0[1], s0[2])] + list(jobs[40][0][1:]), jobs[40][1])
+        from lodestar_amd._native import assign_jobs
+        owner = assign_jobs([len(j[0]) for j in jobs], 2)
+        for c in (c1, c2):
+            got, st = c.verify_jobs(jobs, seed=5)
+            assert got == [(2, 2)] * len(jobs), got
+            assert st["key_error"] == 2 and st["key_error_job"] == 40
+        assert owner[40] == 1 and owner[0] == 0
+    finally:
+        c2.close()
+        c1.close()

@@ -28,7 +28,7 @@ def test_napi_addon_loads_and_fails_loudly_without_gpu():
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
     js = ("const a=require(process.argv[1]);"
-          "const want=['open','close','slots','deviceName','submitJobs','waitJobs','verifySets','aggregatePubkeys','hashToG2'];"
+          "const want=['open','close','slots','deviceName','verifyPacked','verifySets','aggregatePubkeys','hashToG2','sign','skToPk','pubkeyTableSet'];"
           "for(const k of want){if(typeof a[k]!=='function'){console.log('missing',k);process.exit(2);}}"
           "try{a.open(0);console.log('opened');process.exit(3);}catch(e){console.log(e.message);}")
     r = subprocess.run(["node", "-e", js, addon], capture_output=True, text=True, timeout=60)

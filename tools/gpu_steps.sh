@@ -1,0 +1,32 @@
+#!/bin/bash
+# GPU-box runner: named steps, each under its own time limit, stopping at the first failure.
+#   tools/gpu_steps.sh test smoke bench prof ...
+# Outputs go to gpurun_out/ (merged back by gpurun); copy the ones to keep into profiles/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${LSG_TAG:-r03}
+run() {  # name seconds command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  tail -3 "gpurun_out/${TAG}_$name.log"
+  if [ $rc -ne 0 ]; then echo "== $name FAILED rc=$rc"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ;;
+    test-*) run "pytest_${step#test-}" 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "${step#test-}" ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python -u bench.py ;;
+    bench-short) run bench_short 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench-*) w=${step#bench-}; run "bench_$w" 400 python -u bench.py --workload "$w" --no-cpu-baseline ;;
+    node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
+    prof) run rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== all steps ok"
