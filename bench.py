@@ -321,6 +321,9 @@ def main():
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     ap.add_argument("--node-max-sigs", type=int, default=32768, help="node workload: maxSigsPerPackage")
+    ap.add_argument("--devices", type=int, default=0,
+                    help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
+                         "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")
     args = ap.parse_args()
     if args.workload == "node":
         return run_node_workload(args)
@@ -340,8 +343,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from lodestar_amd._native import Context, PreparedJobs
-    ctx = Context(local)
-    wl = Workload(ctx, args.workload, rank, args.sets_per_step, args.packages)
+    n_dev = max(args.devices, 1)
+    if args.devices:
+        if world > 1:
+            raise SystemExit("--devices runs one process over several GPUs (no torch.distributed launch)")
+        ctx = Context(devices=list(range(args.devices)))
+    else:
+        ctx = Context(local)
+    wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages)
     prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
     n_sets = wl.sets_per_package
     max_pks = int(n_sets * wl.pks_per_set) + 1
@@ -359,14 +368,17 @@ def main():
         got[got[:, 0] != 2, 1] = 0
         return bool((got == e).all())
 
-    def gather_node(part):
-        """all-gather the 576-byte partials of one package over RCCL; -> node verdict ticket"""
+    def gather_node(t):
+        """all-gather the 576-byte partials of one package over RCCL, device-resident: the
+        library copies its partial into the collective's send buffer and reads the gathered
+        partials from its receive buffer (no host round trip); -> node verdict ticket"""
         import torch
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda(local)
-        out = torch.empty(world * 576, dtype=torch.uint8, device=t.device)
-        dist.all_gather_into_tensor(out, t)
-        b = out.cpu().numpy().tobytes()
-        ft = ctx.final_submit([b[576 * r:576 * r + 576] for r in range(world)])
+        send = torch.empty(576, dtype=torch.uint8, device=f"cuda:{local}")
+        recv = torch.empty(world * 576, dtype=torch.uint8, device=f"cuda:{local}")
+        ctx.jobs_partial_device(t, send.data_ptr())
+        dist.all_gather_into_tensor(recv, send)
+        torch.cuda.current_stream().synchronize()  # the gathered bytes are complete
+        ft = ctx.final_submit_device(recv.data_ptr(), world)
         if ft is None:
             raise SystemExit("final-exponentiation entries exhausted")
         return ft
@@ -400,8 +412,7 @@ def main():
         while pend:
             t, k, t_sub = pend.popleft()
             if dist is not None:  # node check of SURVEY.md 8e
-                part, _has = ctx.jobs_partial(t)
-                node_ok = ctx.final_wait(gather_node(part))
+                node_ok = ctx.final_wait(gather_node(t))
                 res, st = ctx.wait_jobs_node(t, 1 if node_ok else 0, raw=True)
             else:
                 res, st = ctx.wait_jobs(t, raw=True)
@@ -502,14 +513,14 @@ def main():
     per_set = {k: v for k, v in agg.items() if k in stage_of and k != "k_h2c_map"}
     dom = max(per_set, key=per_set.get)
     # one launch covers the package's sets
-    muls = sum(opc["stage_fp_muls"][st] for st in stage_of[dom]) * n_sets
+    muls = sum(opc["stage_fp_muls"][st] for st in stage_of[dom]) * (n_sets // n_dev)  # device 0's launch
     achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] / max(calls[dom], 1) * 1e-3) / 1e12
     peak = peak_mad / 1e12
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
             "unit": "Tmad/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
-            "traffic": pmc_traffic(dom, n_sets), "alone": pmc_alone(dom, n_sets),
+            "traffic": pmc_traffic(dom, n_sets // n_dev), "alone": pmc_alone(dom, n_sets // n_dev),
             "kernel_ms": round(agg[dom] / max(calls[dom], 1), 3), "work_per_launch_fp_muls": muls}
-    total_sets = n_sets * world * args.steps
+    total_sets = n_sets * world * args.steps  # (n_sets spans all devices of a --devices context)
     value = total_sets / elapsed
     # whole-path work per set: the per-set stages with the bucket-MSM signature sum (groups of
     # >= 256 sets) plus the package group's share of its per-group stages, plus one G1
@@ -550,13 +561,14 @@ def main():
             "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
         }[args.workload]
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world * n_dev, "steps": args.steps,
             "warmup": max(args.warmup, args.depth), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (interop keys, GPU-signed; fresh OS-CSPRNG randomizers per package)",
-            "config": {"workload": desc, "sets_per_step_per_gpu": n_sets, "global_batch": n_sets * world,
+            "config": {"workload": desc, "sets_per_step_per_gpu": n_sets // n_dev, "global_batch": n_sets * world,
                        "jobs_per_package": len(wl.packages[0][0]), "pubkeys_per_set": round(wl.pks_per_set, 1),
-                       "keys": N_KEYS, "parallelism": f"shard{world}"},
+                       "keys": N_KEYS,
+                       "parallelism": f"devices{args.devices} (one context, RCCL exchange)" if args.devices else f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
             "pipeline_depth": args.depth, "distinct_packages": len(prepared),
@@ -566,7 +578,7 @@ def main():
             "submit_call_ms_p50_max": [round(1e3 * statistics.median(submit_wall_timed), 3),
                                        round(1e3 * submit_wall_timed[-1], 3)],
             "roofline": roof,
-            "whole_path_mad_frac": round(node_mads / (peak_mad * world), 4),
+            "whole_path_mad_frac": round(node_mads / (peak_mad * world * n_dev), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},
             "probe_lane_fp_mul_per_s": probe_fp,
             "cpu_baseline": cpu,

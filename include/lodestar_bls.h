@@ -174,6 +174,10 @@ int lsg_wait_jobs(lsg_ctx* ctx, lsg_ticket ticket, lsg_job_result* results /* [n
  * decides, so a caller whose exchange went wrong (node_valid 1 but this share invalid) gets
  * the localised per-job verdicts, never a wrongly accepted package. */
 int lsg_jobs_partial(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* has_batch);
+/* The same partial copied device-to-device into dev_out576 (576 bytes of device memory on the
+ * context's device, e.g. the send buffer of an RCCL all-gather): the exchange never leaves the
+ * GPU.  Returns once the copy is done. */
+int lsg_jobs_partial_device(lsg_ctx* ctx, lsg_ticket ticket, void* dev_out576, int32_t* has_batch);
 int lsg_wait_jobs_node(lsg_ctx* ctx, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results,
                        lsg_stats* stats);
 /* Whole-job assignment of lsg_init_devices (host only, no device needed): owner[j] = device of
@@ -214,6 +218,9 @@ int lsg_batch_partial(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t
  * submit/wait pair runs on device 0's final-exponentiation entries, overlapping packages. */
 int lsg_final_verify(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, int32_t* valid);
 int lsg_final_submit(lsg_ctx* ctx, const uint8_t* partials576, size_t n_partials, lsg_ticket* ticket);
+/* lsg_final_submit over partials in device memory of device 0 (an all-gather's output); the
+ * caller's writes to them must be complete (e.g. its stream synchronised). */
+int lsg_final_submit_device(lsg_ctx* ctx, const void* dev_partials576, size_t n_partials, lsg_ticket* ticket);
 int lsg_final_wait(lsg_ctx* ctx, lsg_ticket ticket, int32_t* valid);
 /* Several RLC batches' final checks in one ticket (one launch per stage instead of one
  * ticket per batch): n_groups groups of per_group partials each, group g being partials

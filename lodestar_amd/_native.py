@@ -98,7 +98,7 @@ EXPORTS = [
     "lsg_final_submit", "lsg_final_wait", "lsg_pipeline_slots", "lsg_probe_mad_peak",
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
-    "lsg_signing_roots", "lsg_attestation_signing_roots",
+    "lsg_signing_roots", "lsg_attestation_signing_roots", "lsg_jobs_partial_device", "lsg_final_submit_device",
 ]
 
 
@@ -120,6 +120,8 @@ def load_library(path=LIB_PATH):
         lib.lsg_allocation_count.argtypes = [vp, ctypes.POINTER(u64)]
         lib.lsg_wait_jobs_node.argtypes = [vp, u64, i32, ctypes.POINTER(LsgJobResult), ctypes.POINTER(LsgStats)]
         lib.lsg_jobs_partial.argtypes = [vp, u64, ctypes.c_char_p, pi32]
+        lib.lsg_jobs_partial_device.argtypes = [vp, u64, vp, pi32]
+        lib.lsg_final_submit_device.argtypes = [vp, vp, sz, ctypes.POINTER(u64)]
         lib.lsg_assign_jobs.argtypes = [ctypes.POINTER(u32), sz, i32, pi32]
         lib.lsg_destroy.argtypes = [vp]
         lib.lsg_last_error.argtypes = [vp]
@@ -365,6 +367,23 @@ class Context:
         if raw:
             return res, {k: getattr(st, k) for k, _ in LsgStats._fields_ }
         return self._results(res, st, n)
+
+    def jobs_partial_device(self, ticket, dev_ptr):
+        """lsg_jobs_partial_device: the package partial copied device-to-device to dev_ptr (576
+        bytes on this context's device, e.g. a torch tensor's data_ptr()); -> has_batch"""
+        hb = ctypes.c_int32()
+        self._check(self.lib.lsg_jobs_partial_device(self.h, ticket[0], ctypes.c_void_p(dev_ptr), ctypes.byref(hb)),
+                    "lsg_jobs_partial_device")
+        return bool(hb.value)
+
+    def final_submit_device(self, dev_ptr, n):
+        """lsg_final_submit_device over n partials in device memory -> final ticket (None if busy)"""
+        t = ctypes.c_uint64()
+        rc = self.lib.lsg_final_submit_device(self.h, ctypes.c_void_p(dev_ptr), n, ctypes.byref(t))
+        if rc == LSG_ERR_BUSY:
+            return None
+        self._check(rc, "lsg_final_submit_device")
+        return t.value
 
     def jobs_partial(self, ticket):
         """lsg_jobs_partial: (576-byte Miller product of the package group, has_batch)."""

@@ -47,7 +47,7 @@ namespace {
 
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
-constexpr int LSG_SLOTS = 16;      // packages in flight per device
+constexpr int LSG_SLOTS = 64;      // packages in flight per device (created on first use)
 constexpr int LSG_FINALS = 64;     // final-exponentiation entries in flight (lsg_final_*)
 constexpr int LSG_FE_STREAMS = 8;  // streams the final-exponentiation entries share
 constexpr int LSG_MAX_DEVICES = 16;
@@ -528,6 +528,14 @@ void slot_destroy(Slot* s) {
     for (int k = 0; k < 2; k++)
       if (s->st[k]) (void)hipStreamDestroy(s->st[k]);
   s->d = nullptr;
+}
+
+// the pipeline slot `s` of device `d`, created on first use
+int slot_ready(Dev* d, Slot* s, int index) {
+  if (s->d) return LSG_OK;
+  const int rc = slot_create(d, s, index, nullptr);
+  if (rc) slot_destroy(s);
+  return rc;
 }
 
 // ---- sizes
@@ -1642,6 +1650,11 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
   }
   const int n = c->n_dev;
   const bool exch = n > 1 || force_exchange();
+  for (int d = 0; d < n; d++) {
+    (void)hipSetDevice(c->dev[d]->device);
+    LSG_RC(slot_ready(c->dev[d], &c->dev[d]->slots[p], p));
+  }
+  (void)hipSetDevice(c->dev[0]->device);
   std::vector<std::vector<size_t>> ids(n);
   {
     std::vector<uint32_t> sizes(n_jobs);
@@ -1756,7 +1769,7 @@ int presync_pkg(lsg_ctx* c, lsg_ticket t, bool partial_only) {
 }
 
 // ---- final-exponentiation entries (device 0): ng groups of pg partials
-int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg) {
+int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg, bool on_device = false) {
   timer_reset(s);
   s->plan.clear();
   const size_t n = ng * pg, np = std::max(n, (size_t)1), gq = std::max(ng, (size_t)1);
@@ -1776,8 +1789,12 @@ int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg) {
     SegPlan P = plan_seg(s->plan, 2, off, len, false, 0, 0);
     LSG_RC(upload_plan(s));
     hipStream_t S = s->st[0];
-    memcpy(s->h_blob.p, partials576, 576 * n);
-    LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, s->h_blob.p, 576 * n, hipMemcpyHostToDevice, S));
+    if (on_device) {  // the caller's device buffer (e.g. a collective's output): no host copy
+      LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, partials576, 576 * n, hipMemcpyDeviceToDevice, S));
+    } else {
+      memcpy(s->h_blob.p, partials576, 576 * n);
+      LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, s->h_blob.p, 576 * n, hipMemcpyHostToDevice, S));
+    }
     KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S, (int)n, P_<uint8_t>(s->d_Fb), P_<uint32_t>(s->d_aux)));
     LSG_RC(run_seg(s, 2, "fp12_product", P, P_<uint32_t>(s->d_aux), P_<uint32_t>(s->d_F)));
     KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_Fb)));
@@ -1832,7 +1849,8 @@ int dev_create(lsg_ctx* c, int ord, int device, Dev** out) {
   d->ord = ord;
   LSG_HIPC(c, hipSetDevice(device));
   LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_util, hipStreamNonBlocking));
-  for (int i = 0; i < LSG_SLOTS; i++) LSG_RC(slot_create(d, &d->slots[i], i, nullptr));
+  // pipeline slots are created on first use (slot_ready): 64 x 2 streams per device up front
+  // would cost init time nobody needs below a few packages in flight
   if (ord == 0) {
     for (int i = 0; i < LSG_FE_STREAMS; i++) LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_fe[i], hipStreamNonBlocking));
     for (int i = 0; i < LSG_FINALS; i++) LSG_RC(slot_create(d, &d->finals[i], i, d->s_fe[i % LSG_FE_STREAMS]));
@@ -1988,6 +2006,7 @@ int lsg_reserve(lsg_ctx* c, size_t max_sets, size_t max_pks, size_t max_msg_byte
     for (int i = 0; i < ns; i++) {
       Slot* s = &c->dev[d]->slots[i];
       if (s->kind != SLOT_FREE) continue;
+      LSG_RC(slot_ready(c->dev[d], s, i));
       LSG_RC(size_inputs(s, max_sets, max_pks, max_msg_bytes));
       // groups: as many as sets (the per-job phase of a failing package of single-set jobs)
       LSG_RC(size_state(s, max_sets, max_pks, max_sets, max_sets / 256 + 1, 1));
@@ -2064,6 +2083,28 @@ int lsg_jobs_partial(lsg_ctx* c, lsg_ticket ticket, uint8_t* out576, int32_t* ha
     memcpy(out576, H_<uint8_t>(s->h_blob) + 576 * (size_t)s->big_g, 576);
   else
     memcpy(out576, fp12_one_blob(), 576);
+  if (has_batch) *has_batch = has ? 1 : 0;
+  return LSG_OK;
+}
+
+int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int32_t* has_batch) {
+  if (!c || !dev_out576) return LSG_ERR_INVALID_ARG;
+  if (c->n_dev > 1) {
+    c->err = "lsg_jobs_partial_device: a multi-device context exchanges its partials itself";
+    return LSG_ERR_INVALID_ARG;
+  }
+  if (int prc = presync_pkg(c, ticket, true)) return prc;
+  LSG_ENTER(c);
+  const int p = ticket_pkg(c, ticket);
+  if (p < 0) return LSG_ERR_INVALID_ARG;
+  Slot* s = &c->dev[0]->slots[p];
+  const bool has = !s->phA.groups.empty() && s->big_g >= 0;
+  if (has) {
+    LSG_HIP(s, hipMemcpyAsync(dev_out576, pkg_partial_dev(s), 576, hipMemcpyDeviceToDevice, s->st[0]));
+  } else {
+    LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, s->st[0]));
+  }
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   if (has_batch) *has_batch = has ? 1 : 0;
   return LSG_OK;
 }
@@ -2173,6 +2214,28 @@ int lsg_final_submit_groups(lsg_ctx* c, const uint8_t* partials576, size_t n_gro
     return LSG_ERR_BUSY;
   }
   int rc = submit_final(s, partials576, n_groups, per_group);
+  if (rc) {
+    sync_slot(s);
+    return rc;
+  }
+  uint64_t serial;
+  *ticket = make_ticket(c, SLOT_FINAL, s->index, &serial);
+  s->kind = SLOT_FINAL;
+  s->serial = serial;
+  return LSG_OK;
+}
+
+int lsg_final_submit_device(lsg_ctx* c, const void* dev_partials576, size_t n_partials, lsg_ticket* ticket) {
+  if (!c || !ticket || (n_partials && !dev_partials576)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Slot* s = nullptr;
+  for (int i = 0; i < LSG_FINALS && !s; i++)
+    if (c->dev[0]->finals[i].kind == SLOT_FREE) s = &c->dev[0]->finals[i];
+  if (!s) {
+    c->err = "all final-exponentiation entries are busy";
+    return LSG_ERR_BUSY;
+  }
+  int rc = submit_final(s, (const uint8_t*)dev_partials576, n_partials ? 1 : 0, n_partials, true);
   if (rc) {
     sync_slot(s);
     return rc;

@@ -432,7 +432,7 @@ class BlsGpuVerifier {
     if (options.reserveSets && this.addon.reserve) {
       // preallocate every pipeline slot for packages of up to reserveSets sets (lsg_reserve)
       const pks = options.reservePubkeys || options.reserveSets;
-      this.addon.reserve(this.ctx, options.reserveSets, pks, 32 * options.reserveSets, 0);
+      this.addon.reserve(this.ctx, options.reserveSets, pks, 32 * options.reserveSets, this.poolSize);
     }
     this.jobs = new Fifo(); // queued blocks (index.ts `jobs`, a block at a time)
     this.priorityJobs = []; // blocks of non-batchable priority jobs: a stack, drained first

@@ -18,7 +18,7 @@
  *   reserve(ctx, maxSets, maxPks, maxMsgBytes, nSlots)                  lsg_reserve
  *   deviceCount(ctx) -> n                   lsg_device_count
  *   close(ctx)                              lsg_destroy
- *   slots(ctx) -> n                         lsg_pipeline_slots
+ *   slots(ctx) -> n                         packages in flight: min(lsg_pipeline_slots, 16 threads)
  *   deviceName(ctx) -> string               lsg_device_name
  *   verifyPacked(ctx, arena, setDesc, jobDesc, seed) -> Promise<{status: Uint8Array,
  *       errCode: Int32Array, batchRetries, batchSigsSuccess, startNs, endNs, finalExps,
@@ -41,6 +41,8 @@
 #include <string.h>
 
 #include "lodestar_bls.h"
+
+#define LSG_NAPI_THREADS 16 /* package threads per context: one outstanding package each */
 
 #define NAPI_CALL(env, call)                                              \
   do {                                                                    \
@@ -249,6 +251,8 @@ static napi_value js_device_count(napi_env env, napi_callback_info info) {
   return make_int(env, n);
 }
 
+/* the packages this addon keeps in flight per context: one per package thread, at most the
+ * library's pipeline slots (BlsGpuVerifier's poolSize, the reference's worker count) */
 static napi_value js_slots(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -258,7 +262,7 @@ static napi_value js_slots(napi_env env, napi_callback_info info) {
   int32_t n = 0;
   int rc = lsg_pipeline_slots(ctx, &n);
   if (rc) return throw_lsg(env, ctx, "lsg_pipeline_slots", rc);
-  return make_int(env, n);
+  return make_int(env, n < LSG_NAPI_THREADS ? n : LSG_NAPI_THREADS);
 }
 
 static napi_value js_device_name(napi_env env, napi_callback_info info) {
@@ -292,7 +296,6 @@ static napi_value js_device_name(napi_env env, napi_callback_info info) {
  * clone of multithread/index.ts:335) and resolves per-job promises. */
 #include <pthread.h>
 
-#define LSG_NAPI_THREADS 16 /* package threads per context: one outstanding package each */
 
 typedef struct pkg_req {
   struct pkg_req* next;

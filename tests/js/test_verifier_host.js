@@ -462,7 +462,7 @@ test("devices / reserveSets open one context over the node's GPUs and preallocat
   const a = mockAddon();
   const pool = new V.BlsGpuVerifier({devices: [0, 1, 2, 3], reserveSets: 32768, maxSigsPerPackage: 32768}, {addon: a});
   assert.deepStrictEqual(a.openedWith, [[0, 1, 2, 3]]);
-  assert.deepStrictEqual(a.reserved, [32768, 32768, 32 * 32768, 0]);
+  assert.deepStrictEqual(a.reserved, [32768, 32768, 32 * 32768, 2]);
   await pool.close();
 });
 

@@ -359,3 +359,27 @@ def test_multi_device_bad_key_rejects_package(keys):
     finally:
         c2.close()
         c1.close()
+
+
+def test_node_mode_partials_device_resident(ctx, keys):
+    """The one-process-per-GPU exchange without a host round trip (lsg_jobs_partial_device /
+    lsg_final_submit_device over torch device buffers, as bench.py's RCCL path uses them): same
+    partial bytes as the host copy, same node verdicts."""
+    import torch
+    sets = single_sets(ctx, keys, b"nodedev", 200)
+    bad = list(sets)
+    bad[77] = bd.corrupt_wrong_message(bad[77])
+    for pkg, ok in ((sets, True), (bad, False)):
+        t = ctx.submit_jobs([([s], 1) for s in pkg])
+        host, has = ctx.jobs_partial(t)
+        dev = torch.empty(3 * 576, dtype=torch.uint8, device="cuda:0")
+        assert ctx.jobs_partial_device(t, dev.data_ptr()) == has
+        dev[576:1152].copy_(dev[:576])  # a 3-rank "gather": this partial and two identities
+        one = bytearray(576)
+        one[47] = 1
+        dev[1152:].copy_(torch.tensor(list(one), dtype=torch.uint8))
+        torch.cuda.synchronize()
+        assert bytes(dev[:576].cpu().numpy().tobytes()) == host
+        assert ctx.final_wait(ctx.final_submit_device(dev[576:].data_ptr(), 2)) == ok
+        got, _ = ctx.wait_jobs_node(t, 1 if ok else 0)
+        assert [g[0] for g in got] == [0 if (not ok and i == 77) else 1 for i in range(200)]
