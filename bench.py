@@ -271,7 +271,7 @@ def run_node_workload(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         raise SystemExit("--workload node runs one Node process per node (use --gpus 1)")
-    cmd = ["node", os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
+    cmd = ["node"] + args.node_flags.split() + [os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--sets-per-step", str(args.sets_per_step), "--max-sigs-per-package",
            str(args.node_max_sigs), "--device", str(local)]
     w0 = time.monotonic_ns()
@@ -296,7 +296,8 @@ def run_node_workload(args):
                                "([set], {batchable: true}) per single-pubkey gossip set, intake gated on canAcceptWork, "
                                "through the N-API addon's package threads",
                    "sets_per_step_per_gpu": args.sets_per_step, "global_batch": args.sets_per_step,
-                   "max_sigs_per_package": nb["max_sigs_per_package"], "parallelism": "shard1", "node": nb["node"]},
+                   "max_sigs_per_package": nb["max_sigs_per_package"], "parallelism": "shard1", "node": nb["node"],
+                   "node_flags": args.node_flags},
         "p50_batch_latency_ms": round(nb["p50_call_latency_ms"], 3),
         "p99_call_latency_ms": round(nb["p99_call_latency_ms"], 3),
         "p50_unloaded_latency_ms": round(nb["p50_lone_call_latency_ms"], 3),
@@ -321,6 +322,7 @@ def main():
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     ap.add_argument("--node-max-sigs", type=int, default=32768, help="node workload: maxSigsPerPackage")
+    ap.add_argument("--node-flags", default="", help="node workload: extra node/V8 flags (e.g. --cpu-prof)")
     ap.add_argument("--devices", type=int, default=0,
                     help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
                          "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")

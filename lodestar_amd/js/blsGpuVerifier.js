@@ -214,28 +214,27 @@ const JOB_FAILED = 3; // settled with a JS Error (queue aborted, serialisation)
 const MAX_JOBS_PER_BLOCK = 4096;
 
 class VerdictBlock {
-  constructor(withTimes) {
-    this.sets = []; // per job: its sets
-    this.flags = []; // per job: JOB_BATCHABLE | JOB_PRIORITY
+  /** batchable: the block's jobs are batchable (a buffered block) or not (one job) */
+  constructor(batchable, withTimes) {
+    this.sets = []; // per job (queue order): its sets
+    this.batchable = batchable;
+    this.nFront = 0; // jobs put in front (priority): queue positions 0 .. nFront-1
     this.added = withTimes ? [] : null; // per job: Date.now() at queueing (jobWaitTime metric)
-    this.status = [];
-    this.codes = [];
+    this.order = null; // queue position -> verdict index, once a priority job went in front
+    this.status = null; // per verdict index, allocated when the block is sealed
+    this.codes = null;
     this.errors = null;
     this.nSigs = 0;
     this.remaining = 0;
     this.sealed = false;
-    this.order = null;
     this.promise = new Promise((resolve) => {
       this._resolve = resolve;
     });
   }
   /** appends a job; priority jobs of a buffer go to its head (index.ts:296 unshift).
-   * Returns the job's verdict index; `order` maps queue positions to verdict indices once
-   * a job has been put in front. */
-  add(sets, flags, front) {
-    const idx = this.status.length;
-    this.status.push(JOB_PENDING);
-    this.codes.push(0);
+   * Returns the job's verdict index (the order of arrival). */
+  add(sets, front) {
+    const idx = this.sets.length;
     if (front) {
       if (!this.order) {
         this.order = [];
@@ -243,25 +242,29 @@ class VerdictBlock {
       }
       this.order.unshift(idx);
       this.sets.unshift(sets);
-      this.flags.unshift(flags);
+      this.nFront++;
       if (this.added) this.added.unshift(Date.now());
     } else {
       if (this.order) this.order.push(idx);
       this.sets.push(sets);
-      this.flags.push(flags);
       if (this.added) this.added.push(Date.now());
     }
     this.nSigs += sets.length;
-    this.remaining++;
     return idx;
   }
   /** verdict index of the job at queue position k */
   at(k) {
     return this.order ? this.order[k] : k;
   }
+  /** no more jobs: verdict storage for all of them */
   seal() {
+    if (this.sealed) return;
     this.sealed = true;
-    if (this.remaining === 0) this._resolve(this);
+    const n = this.sets.length;
+    this.status = new Int8Array(n).fill(JOB_PENDING);
+    this.codes = new Int32Array(n);
+    this.remaining = n;
+    if (n === 0) this._resolve(this);
   }
   settle(idx, status, code, error) {
     if (this.status[idx] !== JOB_PENDING) return;
@@ -271,9 +274,10 @@ class VerdictBlock {
       if (!this.errors) this.errors = [];
       this.errors[idx] = error;
     }
-    if (--this.remaining === 0 && this.sealed) this._resolve(this);
+    if (--this.remaining === 0) this._resolve(this);
   }
   failAll(error) {
+    this.seal();
     for (let k = 0; k < this.status.length; k++) this.settle(k, JOB_FAILED, 0, error);
   }
   verdict(idx) {
@@ -369,7 +373,7 @@ function packBlocks(blocks, nSigs, into) {
         continue;
       }
       jobDescBuf[2 * j] = sets.length;
-      jobDescBuf[2 * j + 1] = block.flags[q];
+      jobDescBuf[2 * j + 1] = (block.batchable ? JOB_BATCHABLE : 0) | (q < block.nFront ? JOB_PRIORITY : 0);
       jobBlock.push(block);
       jobIdx.push(block.at(q));
       j++;
@@ -449,6 +453,8 @@ class BlsGpuVerifier {
     this.kick = false; // a package completed: the next dispatch goes out whatever its size
     this._runJob = this._runJob.bind(this);
     this._runBufferedJobs = this._runBufferedJobs.bind(this);
+    this._onBufferTimer = this._onBufferTimer.bind(this);
+    this.bufferTimer = null;
     const m = this.metrics && this.metrics.blsThreadPool;
     if (m && m.queueLength && m.workersBusy && typeof m.queueLength.addCollect === "function") {
       // index.ts:135-140: sampled at scrape time
@@ -538,10 +544,12 @@ class BlsGpuVerifier {
 
   async close() {
     const aborted = new QueueError({code: QueueErrorCode.QUEUE_ABORTED});
+    if (this.bufferTimer) {
+      clearTimeout(this.bufferTimer);
+      this.bufferTimer = null;
+    }
     if (this.bufferedJobs) {
-      clearTimeout(this.bufferedJobs.timeout);
       this.bufferedJobs.block.failAll(aborted);
-      this.bufferedJobs.block.seal();
       this.bufferedJobs = null;
     }
     for (const b of this.priorityJobs) b.failAll(aborted);
@@ -566,24 +574,17 @@ class BlsGpuVerifier {
     if (opts.batchable === true) {
       let buf = this.bufferedJobs;
       if (!buf) {
-        buf = this.bufferedJobs = {
-          sigCount: 0,
-          firstPush: Date.now(),
-          timeout: setTimeout(this._runBufferedJobs, this.bufferWaitMs),
-          block: new VerdictBlock(this.metrics !== null),
-        };
+        buf = this.bufferedJobs = {sigCount: 0, firstPush: Date.now(), block: new VerdictBlock(true, this.metrics !== null)};
+        this._armBufferTimer();
       }
-      const idx = buf.block.add(sets, JOB_BATCHABLE | (priority ? JOB_PRIORITY : 0), priority);
+      const idx = buf.block.add(sets, priority);
       const p = buf.block.promise.then(PICK[idx]);
       buf.sigCount += sets.length;
-      if (buf.sigCount > MAX_BUFFERED_SIGS || buf.block.sets.length >= MAX_JOBS_PER_BLOCK) {
-        clearTimeout(buf.timeout);
-        this._runBufferedJobs();
-      }
+      if (buf.sigCount > MAX_BUFFERED_SIGS || buf.block.sets.length >= MAX_JOBS_PER_BLOCK) this._runBufferedJobs();
       return p;
     }
-    const block = new VerdictBlock(this.metrics !== null);
-    block.add(sets, priority ? JOB_PRIORITY : 0, false);
+    const block = new VerdictBlock(false, this.metrics !== null);
+    block.add(sets, priority);
     block.seal();
     if (priority) this.priorityJobs.push(block);
     else this.jobs.push(block);
@@ -591,6 +592,22 @@ class BlsGpuVerifier {
     this.queuedSigs += sets.length;
     this._schedule();
     return block.promise.then(PICK[0]);
+  }
+
+  /** One timer for the buffer's 100 ms limit (index.ts:291-293 arms one per buffer; a buffer
+   * that fills first would cost a setTimeout + clearTimeout pair per ~33 sigs): on firing it
+   * flushes the buffer if it is old enough, else re-arms for the rest of its wait. */
+  _armBufferTimer() {
+    if (!this.bufferTimer) this.bufferTimer = setTimeout(this._onBufferTimer, this.bufferWaitMs);
+  }
+
+  _onBufferTimer() {
+    this.bufferTimer = null;
+    const buf = this.bufferedJobs;
+    if (!buf) return;
+    const age = Date.now() - buf.firstPush;
+    if (age >= this.bufferWaitMs) this._runBufferedJobs();
+    else this.bufferTimer = setTimeout(this._onBufferTimer, this.bufferWaitMs - age);
   }
 
   _schedule() {
