@@ -322,7 +322,10 @@ def main():
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     ap.add_argument("--node-max-sigs", type=int, default=32768, help="node workload: maxSigsPerPackage")
-    ap.add_argument("--node-flags", default="", help="node workload: extra node/V8 flags (e.g. --cpu-prof)")
+    ap.add_argument("--node-flags", default="--max-old-space-size=4096 --max-semi-space-size=64",
+                    help="node workload: node/V8 flags -- the reference's production heap setting (Dockerfile:45 "
+                         "NODE_OPTIONS=--max-old-space-size=4096) plus a 64 MB young generation for the verifier's "
+                         "per-call promises (INTEGRATION.md)")
     ap.add_argument("--devices", type=int, default=0,
                     help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
                          "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")

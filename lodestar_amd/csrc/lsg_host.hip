@@ -258,6 +258,9 @@ struct PhasePlan {
   // reuse: the groups' products take their items from an earlier phase (given item ranges)
   bool reuse_items = false;
   std::vector<std::pair<int32_t, int32_t>> given;
+  // host copy of the items (first set, set count): phase C's item-aligned job groups
+  std::vector<int32_t> it_first, it_cnt;
+  bool single_items = false;  // every item is one set: the list form of the Miller loop runs
 };
 
 struct JobRec {
@@ -288,6 +291,7 @@ struct Slot {
   DevBuf binv_lv[2], binv_iv[2];
   DevBuf d_lines;
   bool rs2_ready = false;
+  std::vector<uint8_t> rs2_scaled;  // per set: [r_i] sig_i is in d_rs2 (fallback phases share it)
   // groups
   DevBuf d_S, d_F, d_verdict, d_Sb, d_fgb, d_Fb, d_bkt, d_bits, d_aux, d_gath, d_nodeF, d_nodeV;
   DevBuf seg_tmp[3][2];  // reduction scratch per use: [0] pubkeys, [1] signature sums, [2] Fp12 products
@@ -654,7 +658,9 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, int pkg = 
   for (auto& x : dev) LSG_RC(ensure(s, *x.b, x.bytes));
   if (pkg == 1) {  // Miller lines (split kernels only) and items; fall also holds phase B's chunk terms
     if (!miller_fused()) LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * nn));
-    LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (nn + gg + nn / 16 + 1)));
+    // items, phase A's group terms, then the terms of a reusing phase (phase B's chunks, or
+    // phase C's item-aligned job groups: at most one per item)
+    LSG_RC(ensure(s, s->d_fall, 4 * W_F12 * (2 * nn + gg + 2)));
   }
   if (pkg) {  // fallback signature sums and Miller items: a phase C of single-set jobs needs
               // one item and one term slot per retried set
@@ -876,7 +882,8 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
 // ---- Miller items: <= K consecutive sets of one range (group); item_first / item_cnt go to
 // the arena.  Returns the number of items; set_item (optional) maps set -> item.
 size_t plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges, size_t* off,
-                  std::vector<int32_t>* set_item, std::vector<std::pair<int32_t, int32_t>>* range_items) {
+                  std::vector<int32_t>* set_item, std::vector<std::pair<int32_t, int32_t>>* range_items,
+                  std::vector<int32_t>* host_first = nullptr, std::vector<int32_t>* host_cnt = nullptr) {
   const size_t K = (size_t)s->K;
   std::vector<int32_t> first, cnt;
   for (auto& r : ranges) {
@@ -893,6 +900,8 @@ size_t plan_items(Slot* s, const std::vector<std::pair<size_t, size_t>>& ranges,
   *off = s->plan.size();
   s->plan.insert(s->plan.end(), first.begin(), first.end());
   s->plan.insert(s->plan.end(), cnt.begin(), cnt.end());
+  if (host_first) *host_first = first;
+  if (host_cnt) *host_cnt = cnt;
   return first.size();
 }
 
@@ -971,7 +980,9 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
       }
     }
     Ph.sub_items.clear();
-    Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &Ph.sub_items);
+    Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &Ph.sub_items, &Ph.it_first, &Ph.it_cnt);
+    Ph.single_items = true;
+    for (int32_t c : Ph.it_cnt) Ph.single_items = Ph.single_items && c == 1;
     Ph.term_base = Ph.n_items;
     size_t r = 0;
     for (size_t g = 0; g < ng; g++) {
@@ -993,9 +1004,20 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
 }
 
 // Miller accumulation of planned items (after ev_sig on the main stream)
-int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall) {
+int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall, bool single = false) {
   const int ni = (int)n_items;
   const int32_t* items = PL(s, item_off);
+  if (single && ni > 0) {
+    // every item is one pair (a fallback phase of single-set jobs): the fused kernel would run
+    // four waves per item for one pair; the list form computes each set's lines once and
+    // accumulates them alone (item k = set items[k])
+    LSG_RC(ensure(s, s->d_lines, 4 * (size_t)ML_STEPS * W_LINE * n_items));
+    KL(s, "k_miller_lines_list", lsgk::miller_lines_list(S_(s), ni, items, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
+    KL(s, "k_miller_accum_list",
+       lsgk::miller_accum_list(S_(s), ni, items, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf), P_<uint8_t>(s->d_hinf),
+                               P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_lines), fall));
+    return LSG_OK;
+  }
   if (miller_fused()) {
     KL(s, "k_miller_fused", lsgk::miller_fused(S_(s), ni, items, items + ni, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
                                               P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_H),
@@ -1202,6 +1224,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   s->batch_order.clear();
   s->big_g = -1;
   s->rs2_ready = false;
+  s->rs2_scaled.clear();
   s->has_node = n_node > 0;
   std::vector<const lsg_set*> flat;
   std::vector<size_t> nonb;
@@ -1375,23 +1398,48 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   PhasePlan Ph;
   Ph.groups = groups;
   for (auto& g : Ph.groups) g.msm = false;
+  // groups of one set each (the per-job phase of single-set jobs): one-set Miller items in
+  // the list form instead of four-wave fused items holding one pair
+  size_t singles = 0;
+  for (auto& g : groups) singles += g.len == 1 ? 1 : 0;
+  const int K0 = s->K;
+  if (!given && 2 * singles >= groups.size()) s->K = 1;
   if (given) {
     Ph.reuse_items = true;
     Ph.given = *given;
     Ph.n_items = s->phA.n_items;
     Ph.term_base = s->phA.n_items + s->phA.groups.size();  // after phase A's own terms
   }
-  LSG_RC(plan_phase(s, Ph));
+  const int prc = plan_phase(s, Ph);
+  s->K = K0;
+  LSG_RC(prc);
   LSG_RC(upload_plan(s));
+  // [r_i] sig_i into d_rs2 for the sets no earlier fallback phase of this package scaled
+  if (s->rs2_scaled.size() != s->n_sets) s->rs2_scaled.assign(s->n_sets, 0);
   std::vector<uint8_t> mode(s->n_sets, 0);
-  for (auto& g : groups) memset(mode.data() + g.first, 1, g.len);
+  bool any = false;
+  for (auto& g : groups)
+    for (size_t i = g.first; i < g.first + g.len; i++)
+      if (!s->rs2_scaled[i]) {
+        mode[i] = s->rs2_scaled[i] = 1;
+        any = true;
+      }
   // the side stream needs the plan: order it after the upload on the main stream
   LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
-  LSG_RC(launch_sig_prep(s, true, &mode, P_<uint32_t>(s->d_rs2)));
+  if (any) {
+    s->cur = 1;
+    const int n = (int)s->n_sets;
+    LSG_RC(ensure_host(s, s->h_mode, (size_t)n));
+    memcpy(s->h_mode.p, mode.data(), (size_t)n);
+    LSG_HIP(s, hipMemcpyAsync(s->d_mode.p, s->h_mode.p, (size_t)n, hipMemcpyHostToDevice, s->st[1]));
+    KL(s, "k_sig_scale", lsgk::sig_scale_only(S_(s), n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
+                                              P_<int32_t>(s->d_seterr), P_<uint8_t>(s->d_pinf), P_<uint64_t>(s->d_rnd),
+                                              P_<uint8_t>(s->d_mode), P_<uint32_t>(s->d_rs2)));
+  }
   s->cur = 0;
   uint32_t* fall = given ? P_<uint32_t>(s->d_fall) : P_<uint32_t>(s->d_fall2);
-  if (!given) LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, fall));
+  if (!given) LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, fall, Ph.single_items));
   LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), fall, false));
   LSG_RC(launch_fe(s, groups.size()));
   LSG_RC(launch_readback(s, false));
@@ -1522,8 +1570,9 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     }
   }
   std::vector<int32_t> v;
+  std::vector<size_t> fail_chunks;  // phase-B chunks that failed, whose phase-A items phase C1 reuses
+  bool reuse = true;
   if (!chk.empty()) {  // phase B
-    bool reuse = true;
     for (auto& r : chk_items) reuse = reuse && r.first >= 0;
     LSG_RC(run_fallback_phase(s, lk, chk, reuse ? &chk_items : nullptr, v));
     for (size_t c = 0; c < chk.size(); c++) {
@@ -1532,11 +1581,63 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         s->stats.batch_sigs_success += (uint32_t)chk[c].len;
       } else {
         s->stats.batch_retries++;
-        for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) retry.push_back(s->batch_order[q]);
+        if (reuse) {
+          fail_chunks.push_back(c);
+        } else {
+          for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) retry.push_back(s->batch_order[q]);
+        }
       }
     }
   }
-  if (!retry.empty()) {  // phase C
+  // Phase C1: the jobs of a failing chunk, localised over its phase-A items.  A group is a
+  // run of whole items ending on a job boundary (for single-set jobs: one item = four jobs),
+  // checked with its resident items -- no new Miller work.  A passing group answers its jobs
+  // (valid); a one-job group's verdict is that job's maybeBatch verdict (the same RLC check,
+  // worker.ts:88-96); the jobs of a failing multi-job group are checked one by one (C2).
+  // Per-job verdicts and the batch counters are unchanged: only the work is (a chunk with one
+  // bad set costs 4 group checks + 4 one-set checks instead of 16 one-set checks).
+  if (!fail_chunks.empty()) {
+    const PhasePlan& A0 = s->phA;
+    std::vector<Grp> g1;
+    std::vector<std::pair<int32_t, int32_t>> g1_items;
+    std::vector<std::pair<size_t, size_t>> g1_jobs;  // batch_order positions [a, b)
+    for (size_t c : fail_chunks) {
+      size_t q = chk_jobs[c].first;
+      const size_t qe = chk_jobs[c].second;
+      int32_t ia = chk_items[c].first;
+      for (int32_t it = chk_items[c].first; it < chk_items[c].second; it++) {
+        const size_t end = (size_t)A0.it_first[(size_t)it] + (size_t)A0.it_cnt[(size_t)it];
+        // jobs of this group: those ending at or before `end`; close the group on a boundary
+        size_t qb = q;
+        while (qb < qe && s->jobs[s->batch_order[qb]].first + s->jobs[s->batch_order[qb]].count <= end) qb++;
+        const bool boundary = qb > q && s->jobs[s->batch_order[qb - 1]].first + s->jobs[s->batch_order[qb - 1]].count == end;
+        if (!boundary && it + 1 < chk_items[c].second) continue;
+        Grp g;
+        g.first = (size_t)A0.it_first[(size_t)ia];
+        g.len = end - g.first;
+        g1.push_back(g);
+        g1_items.push_back({ia, it + 1});
+        g1_jobs.push_back({q, qb});
+        q = qb;
+        ia = it + 1;
+      }
+      for (; q < qe; q++) retry.push_back(s->batch_order[q]);  // (not reached: items cover the chunk)
+    }
+    LSG_RC(run_fallback_phase(s, lk, g1, &g1_items, v));
+    for (size_t g = 0; g < g1.size(); g++) {
+      const size_t nj = g1_jobs[g].second - g1_jobs[g].first;
+      for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) {
+        const size_t j = s->batch_order[q];
+        if (v[g])
+          s->results[j] = {LSG_VALID, 0};
+        else if (nj == 1)
+          s->results[j] = {LSG_INVALID, 0};
+        else
+          retry.push_back(j);
+      }
+    }
+  }
+  if (!retry.empty()) {  // phase C2: one group per job
     std::vector<Grp> g3;
     std::vector<size_t> g3job;
     for (size_t j : retry) {

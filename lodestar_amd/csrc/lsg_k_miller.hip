@@ -67,6 +67,28 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
              }));
 }
 
+// ---- list form (fallback phases of single-set jobs): item k is the one pair of set list[k];
+// its lines are stored at position k (a fallback phase touches a few thousand of a package's
+// sets), then accumulated alone -- the fused kernel would spend four waves on one pair
+__global__ void LSG_KERNEL_ATTR k_miller_lines_list(int n, const int32_t* __restrict__ list, const uint32_t* __restrict__ H,
+                                                    uint32_t* __restrict__ lines) {
+  LANE_ITEM(n);
+  (void)lead;
+  const g2a_t Q = lane_load<g2a_t>(H, (size_t)list[item]);
+  miller_lines(Q, [&](int st, const line_t& L) { line_store(lines, (size_t)n, item, st, L); });
+}
+__global__ void LSG_KERNEL_ATTR_W(LSG_ACCUM_WAVES)
+    k_miller_accum_list(int n, const int32_t* __restrict__ list, const uint32_t* __restrict__ P,
+                        const uint8_t* __restrict__ pinf, const uint8_t* __restrict__ hinf, const int32_t* __restrict__ err,
+                        const uint32_t* __restrict__ lines, uint32_t* __restrict__ f) {
+  LANE_ITEM(n);
+  (void)lead;
+  const int i = list[item];
+  g1a_t Pk[1] = {lane_load<g1a_t>(P, (size_t)i)};
+  bool use[1] = {err[i] == 0 && !pinf[i] && !hinf[i]};
+  lane_store(f, item, miller_accum_multi<1>(Pk, use, [&](int, int st) { return line_load(lines, (size_t)n, item, st); }));
+}
+
 // ---- Fused Miller kernel: lines computed and consumed in LDS (north_star: "line coefficients
 // staged in LDS"), the Fp12 accumulator of each item shared by four waves.
 //
@@ -394,6 +416,13 @@ hipError_t miller_fused(hipStream_t st, int n_items, const int32_t* item_first, 
   hipLaunchKernelGGL(k_miller_fused, dim3((n_items + MF_ITEMS - 1) / MF_ITEMS), dim3(256), MF_LDS_BYTES, st, n_items, item_first,
                      item_cnt, P, pinf, hinf, err, H, f);
   return hipGetLastError();
+}
+hipError_t miller_lines_list(hipStream_t st, int n, const int32_t* list, const uint32_t* H, uint32_t* lines) {
+  LSG_LAUNCH_ITEMS(k_miller_lines_list, n, st, n, list, H, lines);
+}
+hipError_t miller_accum_list(hipStream_t st, int n, const int32_t* list, const uint32_t* P, const uint8_t* pinf,
+                             const uint8_t* hinf, const int32_t* err, const uint32_t* lines, uint32_t* f) {
+  LSG_LAUNCH_ITEMS(k_miller_accum_list, n, st, n, list, P, pinf, hinf, err, lines, f);
 }
 hipError_t miller_lines(hipStream_t st, int n, const uint32_t* H, uint32_t* lines) {
   LSG_LAUNCH_ITEMS(k_miller_lines, n, st, n, H, lines);

@@ -149,6 +149,10 @@ hipError_t sig_prep(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_
   }
   LSG_LAUNCH_ITEMS(k_sig_scale, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
 }
+hipError_t sig_scale_only(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                          const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_sig_scale, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
+}
 hipError_t g2a_to_bytes(hipStream_t st, int n, const uint32_t* pts, const uint8_t* inf, uint8_t* out192) {
   LSG_LAUNCH_ITEMS(k_g2a_to_bytes, n, st, n, pts, inf, out192);
 }

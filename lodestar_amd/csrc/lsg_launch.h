@@ -33,6 +33,10 @@ hipError_t sig_subgroup(hipStream_t st, int n, const uint32_t* sig_aff, const ui
 // (mode == null or mode[i] != 0), else sig_i itself (the bucket MSM scales later).
 hipError_t sig_prep(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
                     const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out);
+// [r_i] sig_i (or the identity, as sig_prep) for the sets with mode[i] != 0 only; other
+// entries of out are left as they are (fallback phases fill one scaled array in turns)
+hipError_t sig_scale_only(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                          const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out);
 hipError_t g2a_to_bytes(hipStream_t st, int n, const uint32_t* pts, const uint8_t* inf, uint8_t* out192);
 hipError_t g2p_compress(hipStream_t st, int n, const uint32_t* pts, uint8_t* out96);
 hipError_t g2p_to_canon(hipStream_t st, int n, const uint32_t* pts, uint8_t* out288);
@@ -55,6 +59,10 @@ hipError_t miller_fused(hipStream_t st, int n_items, const int32_t* item_first, 
                         const uint32_t* P, const uint8_t* pinf, const uint8_t* hinf, const int32_t* err,
                         const uint32_t* H, uint32_t* f);
 hipError_t miller_lines(hipStream_t st, int n, const uint32_t* H, uint32_t* lines);
+// list form, one pair per item: item k = set list[k]; lines stored by item (n items)
+hipError_t miller_lines_list(hipStream_t st, int n, const int32_t* list, const uint32_t* H, uint32_t* lines);
+hipError_t miller_accum_list(hipStream_t st, int n, const int32_t* list, const uint32_t* P, const uint8_t* pinf,
+                             const uint8_t* hinf, const int32_t* err, const uint32_t* lines, uint32_t* f);
 // K = pairs per item (1, 2 or 4)
 hipError_t miller_accum(hipStream_t st, int K, int n_items, const int32_t* item_first, const int32_t* item_cnt,
                         const uint32_t* P, const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, int n_sets,

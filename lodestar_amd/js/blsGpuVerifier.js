@@ -301,8 +301,8 @@ const SET_DESC_WORDS = 7; // pkOff, pkLen, nPks, msgOff, msgLen, sigOff, sigLen 
  * be serialized fails on its own and is left out.  `into` (optional) is a previous package's
  * buffers, reused when large enough (fresh multi-MB typed arrays per package cost GC time).
  */
-function packBlocks(blocks, nSigs, into) {
-  let cap = nSigs * 224 + 256;
+function packBlocks(blocks, nSigs, into, minSigs = 0) {
+  let cap = Math.max(nSigs, minSigs) * 224 + 256;
   let arena = into && into.arenaBuf.length >= cap ? into.arenaBuf : new Uint8Array(cap);
   cap = arena.length;
   let off = 0;
@@ -319,10 +319,11 @@ function packBlocks(blocks, nSigs, into) {
     off += n;
     return o;
   };
-  const setDescBuf = into && into.setDescBuf.length >= SET_DESC_WORDS * nSigs ? into.setDescBuf : new Uint32Array(SET_DESC_WORDS * nSigs);
+  const setDescBuf =
+    into && into.setDescBuf.length >= SET_DESC_WORDS * nSigs ? into.setDescBuf : new Uint32Array(SET_DESC_WORDS * Math.max(nSigs, minSigs));
   let nJobs = 0;
   for (const b of blocks) nJobs += b.sets.length;
-  const jobDescBuf = into && into.jobDescBuf.length >= 2 * nJobs ? into.jobDescBuf : new Uint32Array(2 * nJobs);
+  const jobDescBuf = into && into.jobDescBuf.length >= 2 * nJobs ? into.jobDescBuf : new Uint32Array(2 * Math.max(nJobs, minSigs));
   const jobBlock = [];
   const jobIdx = [];
   const sd = setDescBuf;
@@ -334,8 +335,30 @@ function packBlocks(blocks, nSigs, into) {
       const off0 = off;
       const k0 = k;
       try {
-        for (const set of sets) {
+        for (let si = 0; si < sets.length; si++) {
+          const set = sets[si];
           const d = SET_DESC_WORDS * k;
+          const pk1 = set.pubkeyIndices === undefined && set.type === SignatureSetType.single ? set.pubkey : null;
+          const root = set.signingRoot;
+          const sig = set.signature;
+          if (pk1 instanceof Uint8Array && off + pk1.length + root.length + sig.length <= cap) {
+            // the common shape (one raw key): three copies, no helper calls
+            arena.set(pk1, off);
+            sd[d] = off;
+            sd[d + 1] = pk1.length;
+            sd[d + 2] = 1;
+            off += pk1.length;
+            arena.set(root, off);
+            sd[d + 3] = off;
+            sd[d + 4] = root.length;
+            off += root.length;
+            arena.set(sig, off);
+            sd[d + 5] = off;
+            sd[d + 6] = sig.length;
+            off += sig.length;
+            k++;
+            continue;
+          }
           if (set.pubkeyIndices !== undefined) {
             const ix = set.pubkeyIndices instanceof Uint32Array ? set.pubkeyIndices : Uint32Array.from(set.pubkeyIndices);
             sd[d] = put(new Uint8Array(ix.buffer, ix.byteOffset, 4 * ix.length));
@@ -360,10 +383,10 @@ function packBlocks(blocks, nSigs, into) {
           } else {
             throw Error("Unknown signature set type");
           }
-          sd[d + 3] = put(set.signingRoot);
-          sd[d + 4] = set.signingRoot.length;
-          sd[d + 5] = put(set.signature);
-          sd[d + 6] = set.signature.length;
+          sd[d + 3] = put(root);
+          sd[d + 4] = root.length;
+          sd[d + 5] = put(sig);
+          sd[d + 6] = sig.length;
           k++;
         }
       } catch (e) {
@@ -654,7 +677,8 @@ class BlsGpuVerifier {
     const run = (async () => {
       let pkg = null;
       try {
-        pkg = packBlocks(blocks, startedSigSets, this.spare.pop());
+        // buffers sized for a full package, so that every one can be reused
+        pkg = packBlocks(blocks, startedSigSets, this.spare.pop(), this.maxSigsPerPackage);
         const n = pkg.jobBlock.length;
         if (n === 0) return;
         const jobStartNs = process.hrtime.bigint();
@@ -681,7 +705,7 @@ class BlsGpuVerifier {
           m.batchRetries.inc(workResult.batchRetries);
           m.batchSigsSuccess.inc(workResult.batchSigsSuccess);
         }
-        if (this.spare.length < 4) this.spare.push(pkg);
+        if (this.spare.length < this.poolSize) this.spare.push(pkg);
       } catch (e) {
         if (!this.closed && this.logger) this.logger.error("BlsGpuVerifier error", {}, e);
         for (const b of blocks) b.failAll(e);

@@ -26,8 +26,8 @@ for step in "$@"; do
     depth-*) a=${step#depth-}; w=${a%%:*}; d=${a#*:}; run "bench_${w}_d$d" 400 python -u bench.py --workload "$w" --depth "$d" --no-cpu-baseline ;;
     devices1) run bench_devices1 400 python -u bench.py --devices 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
-    node-semi) run bench_node_semi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags "--max-semi-space-size=64" ;;
-    node-prof) mkdir -p gpurun_out/nodeprof && run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 --node-flags "--cpu-prof --cpu-prof-dir=gpurun_out/nodeprof" ;;
+    node-nosemi) run bench_node_nosemi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags=--max-old-space-size=4096 ;;
+    node-prof) mkdir -p gpurun_out/nodeprof && run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 "--node-flags=--max-old-space-size=4096 --max-semi-space-size=64 --cpu-prof --cpu-prof-dir=gpurun_out/nodeprof" ;;
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
