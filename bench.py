@@ -71,8 +71,8 @@ class Workload:
         pks = ctx.sk_to_pk(sks)
         self.packages = []
         tag = name.encode()
-        if name in ("jobs", "adversarial", "gossip"):
-            n = 128 if name == "gossip" else sets_per_step
+        if name in ("jobs", "adversarial", "gossip", "single"):
+            n = 128 if name == "gossip" else (1 if name == "single" else sets_per_step)
             for p in range(n_packages):
                 base = (rank * n_packages + p) * n
                 msgs = [msg(tag, base + i) for i in range(n)]
@@ -80,6 +80,8 @@ class Workload:
                 sets = [([pks[(base + i) % N_KEYS]], msgs[i], sigs[i]) for i in range(n)]
                 if name == "gossip":
                     self.packages.append(([(sets, 1)], None))
+                elif name == "single":  # verifyOnMainThread / BlsSingleThreadVerifier: one set, one verify
+                    self.packages.append(([(sets, 0)], None))
                 elif name == "jobs":
                     self.packages.append(([([s], 1) for s in sets], None))
                 else:
@@ -314,7 +316,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30, help="timed packages per GPU")
     ap.add_argument("--warmup", type=int, default=5, help="untimed packages per GPU (at least --depth are run)")
-    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node"], default="jobs")
+    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node", "single"], default="jobs")
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
@@ -333,7 +335,7 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 6, "gossip": 8}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 6, "gossip": 8, "single": 1}[args.workload]
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
         args.packages = 2 if args.workload == "block" else args.depth + 1
 
@@ -516,7 +518,7 @@ def main():
                 "k_miller_fused": ["miller_fused_per_set"], "k_sig_subgroup": ["sig_subgroup"],
                 "k_sig_decode": ["sig_decode"], "k_pk_scale": ["pk_scale"], "k_h2c_map": ["hash_map"]}
     per_set = {k: v for k, v in agg.items() if k in stage_of and k != "k_h2c_map"}
-    dom = max(per_set, key=per_set.get)
+    dom = max(per_set, key=per_set.get) if per_set else "k_miller_fused"
     # one launch covers the package's sets
     muls = sum(opc["stage_fp_muls"][st] for st in stage_of[dom]) * (n_sets // n_dev)  # device 0's launch
     achieved = muls * opc["mads_per_fp_mul"] / (agg[dom] / max(calls[dom], 1) * 1e-3) / 1e12
@@ -544,7 +546,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            if args.workload in ("jobs", "adversarial", "gossip"):
+            if args.workload in ("jobs", "adversarial", "gossip", "single"):
                 sets = [s for job, _ in wl.packages[0][0] for s in job]
                 if args.workload == "adversarial":
                     sets = [s for (job, _), e in zip(wl.packages[0][0], wl.packages[0][1]) if e == (1, 0) for s in job]
@@ -564,6 +566,8 @@ def main():
             "sync": "sync-committee contributions (SURVEY 8d config B): 256 batchable jobs per package, each one "
                     "512-signer aggregate set (keys by index)",
             "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
+            "single": "one set per call (verifyOnMainThread / BlsSingleThreadVerifier, maybeBatch.ts:34-38 verify): "
+                      "latency of a lone verification",
         }[args.workload]
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world * n_dev, "steps": args.steps,

@@ -108,11 +108,29 @@ async function main() {
     });
   }
 
+  // optional CPU profile of the timed run (env LSG_NODE_CPUPROF=<file>), started through the
+  // inspector after the GPU context exists: node's --cpu-prof samples with SIGPROF from
+  // process start, and the runtime's device initialisation does not survive it
+  let prof = null;
+  if (process.env.LSG_NODE_CPUPROF) {
+    const inspector = require("inspector");
+    prof = new inspector.Session();
+    prof.connect();
+    await new Promise((r) => prof.post("Profiler.enable", () => prof.post("Profiler.start", r)));
+  }
   const statsBefore = {...pool.stats};
   await run(perStep * warmup, 0);
   const pk0 = pool.stats.packages;
   const ps0 = pool.stats.packageSigs;
   const timed = await run(perStep * steps, perStep * warmup);
+  if (prof) {
+    await new Promise((r) =>
+      prof.post("Profiler.stop", (err, res) => {
+        if (!err) require("fs").writeFileSync(process.env.LSG_NODE_CPUPROF, JSON.stringify(res.profile));
+        r();
+      })
+    );
+  }
   const packages = pool.stats.packages - pk0;
   const packageSigs = pool.stats.packageSigs - ps0;
   // unloaded: one call at a time (a lone batchable job waits for the 100 ms buffer timer in

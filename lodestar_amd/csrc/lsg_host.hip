@@ -1393,7 +1393,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   // a phase with more groups than phase A had grows d_fall2 (and the group buffers), and a
   // pointer saved earlier would name the freed allocation
   LSG_RC(size_state(s, s->n_sets, s->n_pks, groups.size(), 0, 2));
-  timer_reset(s);
+  s->cur = 0;  // the phase's kernel timers follow phase A's (lsg_last_kernel_times: the whole ticket)
   s->plan.clear();
   PhasePlan Ph;
   Ph.groups = groups;

@@ -27,7 +27,8 @@ for step in "$@"; do
     devices1) run bench_devices1 400 python -u bench.py --devices 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
     node-nosemi) run bench_node_nosemi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags=--max-old-space-size=4096 ;;
-    node-prof) mkdir -p gpurun_out/nodeprof && run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 "--node-flags=--max-old-space-size=4096 --max-semi-space-size=64 --cpu-prof --cpu-prof-dir=gpurun_out/nodeprof" ;;
+    node-prof) mkdir -p gpurun_out/nodeprof && export LSG_NODE_CPUPROF=gpurun_out/nodeprof/bench_node.cpuprofile &&
+               run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 && unset LSG_NODE_CPUPROF ;;
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
