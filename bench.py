@@ -275,7 +275,7 @@ def run_node_workload(args):
         raise SystemExit("--workload node runs one Node process per node (use --gpus 1)")
     cmd = ["node"] + args.node_flags.split() + [os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--sets-per-step", str(args.sets_per_step), "--max-sigs-per-package",
-           str(args.node_max_sigs), "--device", str(local)]
+           str(args.node_max_sigs), "--device", str(local), "--max-pending-sigs", str(args.node_max_pending)]
     w0 = time.monotonic_ns()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     w1 = time.monotonic_ns()
@@ -324,6 +324,7 @@ def main():
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
                     help="one GPU: wait each ticket on its own thread (as the Node host) or inline")
     ap.add_argument("--node-max-sigs", type=int, default=32768, help="node workload: maxSigsPerPackage")
+    ap.add_argument("--node-max-pending", type=int, default=0, help="node workload: maxPendingSigs (0: default)")
     ap.add_argument("--node-flags", default="--max-old-space-size=4096 --max-semi-space-size=64",
                     help="node workload: node/V8 flags -- the reference's production heap setting (Dockerfile:45 "
                          "NODE_OPTIONS=--max-old-space-size=4096) plus a 64 MB young generation for the verifier's "

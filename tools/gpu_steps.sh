@@ -26,6 +26,8 @@ for step in "$@"; do
     depth-*) a=${step#depth-}; w=${a%%:*}; d=${a#*:}; run "bench_${w}_d$d" 400 python -u bench.py --workload "$w" --depth "$d" --no-cpu-baseline ;;
     devices1) run bench_devices1 400 python -u bench.py --devices 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
+    node-semi128) run bench_node_semi128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" ;;
+    node-p98k) run bench_node_p98k 400 python -u bench.py --workload node --no-cpu-baseline --node-max-pending 98304 ;;
     node-nosemi) run bench_node_nosemi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags=--max-old-space-size=4096 ;;
     node-prof) mkdir -p gpurun_out/nodeprof && export LSG_NODE_CPUPROF=gpurun_out/nodeprof/bench_node.cpuprofile &&
                run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 && unset LSG_NODE_CPUPROF ;;
