@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
 # kernel translation units compile in parallel; lsg_host.hip is the orchestration + C ABI
 SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip", "lsg_k_reduce.hip", "lsg_serial.hip", "lsg_serial_wide.hip",
-           "lsg_host.hip"]
+           "lsg_serial_pair.hip", "lsg_serial_pair_wide.hip", "lsg_host.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
            "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp",
            "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h"]

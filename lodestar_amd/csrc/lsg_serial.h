@@ -21,14 +21,36 @@ LSG_ROW_DECL(lsg_row_miller_neg_g1, int ng, const uint8_t* S288, uint8_t* out576
 // out576[g] = ML(-G1, sum_k 2^k C_{g,k}) for ng groups of 64 canonical 288-byte projective G2
 // points each (the bucket MSM's per-bit sums): Horner and the Miller loop in one row chain
 LSG_ROW_DECL(lsg_row_horner_miller, int ng, const uint8_t* C288, uint8_t* out576)
+// The same stages on the pair backend (lsg_serial_pair.hip): _ps one group per wave with its
+// product batches split over the lane pairs (latency), _pw one group per lane pair (groups).
+#define LSG_PAIR_DECL(name, ...)                     \
+  hipError_t name##_ps(hipStream_t st, __VA_ARGS__); \
+  hipError_t name##_pw(hipStream_t st, __VA_ARGS__);
+LSG_PAIR_DECL(lsg_pair_final_exp, int ng, const uint8_t* F576, int32_t* verdict)
+LSG_PAIR_DECL(lsg_pair_miller_neg_g1, int ng, const uint8_t* S288, uint8_t* out576)
+LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out576)
+#ifndef LSG_PAIR_WIDE_MIN
+#define LSG_PAIR_WIDE_MIN 512
+#endif
+// env LSG_SERIAL=row: the round-2 row kernels (A/B); default: the pair kernels
+#include <stdlib.h>
+#include <string.h>
+inline bool lsg_serial_rows() {
+  static const int v = [] {
+    const char* e = getenv("LSG_SERIAL");
+    return e && strcmp(e, "row") == 0 ? 1 : 0;
+  }();
+  return v != 0;
+}
+#define LSG_SERIAL_PICK(name, ng, ...)                                                                \
+  (lsg_serial_rows() ? ((ng) >= LSG_ROW_WIDE_MIN ? lsg_row_##name##_r1(__VA_ARGS__) : lsg_row_##name##_r4(__VA_ARGS__)) \
+                     : ((ng) >= LSG_PAIR_WIDE_MIN ? lsg_pair_##name##_pw(__VA_ARGS__) : lsg_pair_##name##_ps(__VA_ARGS__)))
 inline hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
-  return ng >= LSG_ROW_WIDE_MIN ? lsg_row_final_exp_r1(st, ng, F576, verdict) : lsg_row_final_exp_r4(st, ng, F576, verdict);
+  return LSG_SERIAL_PICK(final_exp, ng, st, ng, F576, verdict);
 }
 inline hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
-  return ng >= LSG_ROW_WIDE_MIN ? lsg_row_miller_neg_g1_r1(st, ng, S288, out576)
-                                : lsg_row_miller_neg_g1_r4(st, ng, S288, out576);
+  return LSG_SERIAL_PICK(miller_neg_g1, ng, st, ng, S288, out576);
 }
 inline hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
-  return ng >= LSG_ROW_WIDE_MIN ? lsg_row_horner_miller_r1(st, ng, C288, out576)
-                                : lsg_row_horner_miller_r4(st, ng, C288, out576);
+  return LSG_SERIAL_PICK(horner_miller, ng, st, ng, C288, out576);
 }

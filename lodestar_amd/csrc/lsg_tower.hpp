@@ -138,7 +138,10 @@ LSG_INL fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& k) {
 template <int N>
 LSG_INL void fp_mul_list(fp_t* r, const fp_t* x, const fp_t* y) {
 #ifdef LSG_ROW_SPLIT
-  if (N >= 4) {  // the rows of a wave share one item: split the batch over them
+#ifndef LSG_SPLIT_MIN
+#define LSG_SPLIT_MIN 4
+#endif
+  if (N >= LSG_SPLIT_MIN) {  // the rows (lane pairs) of a wave share one item: split the batch
     fp_mul_list_rows<N>(r, x, y);
     return;
   }
