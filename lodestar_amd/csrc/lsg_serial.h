@@ -32,13 +32,17 @@ LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out5
 #ifndef LSG_PAIR_WIDE_MIN
 #define LSG_PAIR_WIDE_MIN 512
 #endif
-// env LSG_SERIAL=row: the round-2 row kernels (A/B); default: the pair kernels
+// Default: the row kernels.  env LSG_SERIAL=pair selects the pair kernels (A/B): measured
+// slower -- final exponentiation 9.3 ms against 4.0 ms for one group, 51 against 26 ms for a
+// fallback phase's thousands (profiles/r03_serial_pair_ab.txt).  A pair Fp12 is 84 VGPRs
+// (12 on a row), so the exponentiation's live state spills around every product leaf call
+// (2.3 KB of scratch per lane) and one wave per SIMD has nothing to hide that latency.
 #include <stdlib.h>
 #include <string.h>
 inline bool lsg_serial_rows() {
   static const int v = [] {
     const char* e = getenv("LSG_SERIAL");
-    return e && strcmp(e, "row") == 0 ? 1 : 0;
+    return e && strcmp(e, "pair") == 0 ? 0 : 1;
   }();
   return v != 0;
 }

@@ -16,8 +16,8 @@ run() {  # name seconds command...
   if [ $rc -ne 0 ]; then echo "== $name FAILED rc=$rc"; exit $rc; fi
 }
 for step in "$@"; do
-  # row:<step> runs <step> with the round-2 row kernels for the serial stages (A/B)
-  if [ "${step#row:}" != "$step" ]; then export LSG_SERIAL=row TAG=${TAG%_row}_row; step=${step#row:}; else unset LSG_SERIAL; TAG=${LSG_TAG:-r03}; fi
+  # pair:<step> runs <step> with the pair-backend serial kernels (A/B against the row default)
+  if [ "${step#pair:}" != "$step" ]; then export LSG_SERIAL=pair TAG=${LSG_TAG:-r03}_pair; step=${step#pair:}; else unset LSG_SERIAL; TAG=${LSG_TAG:-r03}; fi
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ;;
     test-*) run "pytest_${step#test-}" 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "${step#test-}" ;;
@@ -31,6 +31,8 @@ for step in "$@"; do
     node-semi128) run bench_node_semi128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" ;;
     node-semi256) run bench_node_semi256 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=256" ;;
     node-s128p98k) run bench_node_s128p98k 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" --node-max-pending 98304 ;;
+    node-mm128) run bench_node_mm128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --min-semi-space-size=128 --max-semi-space-size=128" ;;
+    node-mm64) run bench_node_mm64 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --min-semi-space-size=64 --max-semi-space-size=64" ;;
     node-p98k) run bench_node_p98k 400 python -u bench.py --workload node --no-cpu-baseline --node-max-pending 98304 ;;
     node-nosemi) run bench_node_nosemi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags=--max-old-space-size=4096 ;;
     node-prof) mkdir -p gpurun_out/nodeprof && export LSG_NODE_CPUPROF=gpurun_out/nodeprof/bench_node.cpuprofile &&
