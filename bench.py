@@ -273,6 +273,10 @@ def run_node_workload(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         raise SystemExit("--workload node runs one Node process per node (use --gpus 1)")
+    # at least 150 timed steps (~2.5 s): over a 30-step window (~0.6 s) the JIT, the heap
+    # growth and single collections moved the rate by +-25 % between runs
+    args.steps = max(args.steps, 150)
+    args.warmup = max(args.warmup, 10)
     cmd = ["node"] + args.node_flags.split() + [os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--sets-per-step", str(args.sets_per_step), "--max-sigs-per-package",
            str(args.node_max_sigs), "--device", str(local), "--max-pending-sigs", str(args.node_max_pending)]

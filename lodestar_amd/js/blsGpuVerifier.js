@@ -438,7 +438,8 @@ class BlsGpuVerifier {
    *     one launch filling all 256 CUs) and light load keeps the latency of small packages;
    *   - at most one package per pipeline slot / package thread (addon.slots) is in flight.
    * Back-pressure (canAcceptWork, index.ts:143-149) is on SETS: queued + buffered + in flight
-   * < `maxPendingSigs` (4 x maxSigsPerPackage).  Per-job verdicts do not depend on any of it:
+   * < `maxPendingSigs` (3 x maxSigsPerPackage: enough to keep the GPU pipelined, and every
+   * pending call is live JS state the young-generation collector copies).  Per-job verdicts do not depend on any of it:
    * the GPU applies worker.ts's batch + retry rules to whatever package it gets.
    * The reference's policy is {maxSigsPerPackage: 128, eagerPackages: slots}.
    */
@@ -454,7 +455,7 @@ class BlsGpuVerifier {
     this.maxSigsPerPackage = options.maxSigsPerPackage || DEFAULT_MAX_SIGS_PER_PACKAGE;
     this.eagerPackages = options.eagerPackages === undefined ? DEFAULT_EAGER_PACKAGES : options.eagerPackages;
     this.minSigsWhenBusy = options.minSigsWhenBusy || Math.max(1, Math.floor(this.maxSigsPerPackage / 4));
-    this.maxPendingSigs = options.maxPendingSigs || 4 * this.maxSigsPerPackage;
+    this.maxPendingSigs = options.maxPendingSigs || 3 * this.maxSigsPerPackage;
     this.bufferWaitMs = options.bufferWaitMs === undefined ? MAX_BUFFER_WAIT_MS : options.bufferWaitMs;
     if (options.reserveSets && this.addon.reserve) {
       // preallocate every pipeline slot for packages of up to reserveSets sets (lsg_reserve)

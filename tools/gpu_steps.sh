@@ -33,12 +33,17 @@ for step in "$@"; do
     node-s128p98k) run bench_node_s128p98k 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" --node-max-pending 98304 ;;
     node-mm128) run bench_node_mm128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --min-semi-space-size=128 --max-semi-space-size=128" ;;
     node-mm64) run bench_node_mm64 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --min-semi-space-size=64 --max-semi-space-size=64" ;;
+    node-gc) run node_gc 300 node --max-old-space-size=4096 --max-semi-space-size=64 --trace-gc bench/bench_node.js --steps 150 --warmup 10 ;;
+    node-long) run bench_node_long 400 python -u bench.py --workload node --no-cpu-baseline --steps 150 --warmup 10 ;;
+    node-long128) run bench_node_long128 400 python -u bench.py --workload node --no-cpu-baseline --steps 150 --warmup 10 "--node-flags=--max-old-space-size=4096 --min-semi-space-size=128 --max-semi-space-size=128" ;;
+    hwq32-*) w=${step#hwq32-}; export LSG_HW_QUEUES=32 && run "bench_${w}_hwq32" 400 python -u bench.py --workload "$w" --depth 16 --no-cpu-baseline && unset LSG_HW_QUEUES ;;
     node-p98k) run bench_node_p98k 400 python -u bench.py --workload node --no-cpu-baseline --node-max-pending 98304 ;;
     node-nosemi) run bench_node_nosemi 400 python -u bench.py --workload node --no-cpu-baseline --node-flags=--max-old-space-size=4096 ;;
     node-prof) mkdir -p gpurun_out/nodeprof && export LSG_NODE_CPUPROF=gpurun_out/nodeprof/bench_node.cpuprofile &&
                run bench_node_prof 400 python -u bench.py --workload node --no-cpu-baseline --steps 15 && unset LSG_NODE_CPUPROF ;;
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc) run pmc 900 bash tools/gpu_pmc.sh ;;
+    trace-*) w=${step#trace-}; run "trace_$w" 400 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/trace_$w" -o run -- python3 bench.py --workload "$w" --steps 20 --warmup 4 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
