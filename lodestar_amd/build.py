@@ -14,10 +14,10 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
 # kernel translation units compile in parallel; lsg_host.hip is the orchestration + C ABI
 SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip", "lsg_k_reduce.hip", "lsg_serial.hip", "lsg_serial_wide.hip",
-           "lsg_serial_pair.hip", "lsg_serial_pair_wide.hip", "lsg_host.hip"]
+           "lsg_serial_pair.hip", "lsg_serial_pair_wide.hip", "lsg_slp.hip", "lsg_host.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
            "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp",
-           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h"]
+           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h", "lsg_slp_progs.h", "lsg_slp_exec.hpp"]
 OBJ = os.path.join(HERE, "_obj")
 
 
@@ -78,6 +78,10 @@ def build(force=False, verbose=True, extra=None, out=None):
     const = os.path.join(CSRC, "lsg_constants.hpp")
     if not os.path.exists(const) or os.path.getmtime(gen) > os.path.getmtime(const):
         subprocess.check_call([sys.executable, gen, const])
+    gen_slp = os.path.join(ROOT, "tools", "gen_slp.py")
+    progs = os.path.join(CSRC, "lsg_slp_progs.h")
+    if not os.path.exists(progs) or os.path.getmtime(gen_slp) > os.path.getmtime(progs):
+        subprocess.check_call([sys.executable, gen_slp, progs])
     extra = list(extra or [])
     out = out or OUT
     if not force and not extra and out == OUT and not needs_rebuild():

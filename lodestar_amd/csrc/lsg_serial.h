@@ -32,23 +32,34 @@ LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out5
 #ifndef LSG_PAIR_WIDE_MIN
 #define LSG_PAIR_WIDE_MIN 512
 #endif
-// Default: the row kernels.  env LSG_SERIAL=pair selects the pair kernels (A/B): measured
-// slower -- final exponentiation 9.3 ms against 4.0 ms for one group, 51 against 26 ms for a
-// fallback phase's thousands (profiles/r03_serial_pair_ab.txt).  A pair Fp12 is 84 VGPRs
-// (12 on a row), so the exponentiation's live state spills around every product leaf call
-// (2.3 KB of scratch per lane) and one wave per SIMD has nothing to hide that latency.
+// The same stages as straight-line programs (lsg_slp.hip, tools/gen_slp.py): one group per
+// workgroup, each step's independent products spread over the lane pairs.
+hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict);
+hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576);
+hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576);
+// Default: the straight-line programs.  env LSG_SERIAL=row selects the row kernels, =pair
+// the pair kernels (A/B).  The pair kernels were measured slower than the rows -- final
+// exponentiation 9.3 ms against 4.0 ms for one group, 51 against 26 ms for a fallback phase's
+// thousands (profiles/r03_serial_pair_ab.txt): a pair Fp12 is 84 VGPRs (12 on a row), so the
+// exponentiation's live state spills around every product leaf call.
 #include <stdlib.h>
 #include <string.h>
-inline bool lsg_serial_rows() {
+enum { LSG_SERIAL_SLP = 0, LSG_SERIAL_ROW = 1, LSG_SERIAL_PAIR = 2 };
+inline int lsg_serial_mode() {
   static const int v = [] {
     const char* e = getenv("LSG_SERIAL");
-    return e && strcmp(e, "pair") == 0 ? 0 : 1;
+    if (e && strcmp(e, "row") == 0) return (int)LSG_SERIAL_ROW;
+    if (e && strcmp(e, "pair") == 0) return (int)LSG_SERIAL_PAIR;
+    return (int)LSG_SERIAL_SLP;
   }();
-  return v != 0;
+  return v;
 }
-#define LSG_SERIAL_PICK(name, ng, ...)                                                                \
-  (lsg_serial_rows() ? ((ng) >= LSG_ROW_WIDE_MIN ? lsg_row_##name##_r1(__VA_ARGS__) : lsg_row_##name##_r4(__VA_ARGS__)) \
-                     : ((ng) >= LSG_PAIR_WIDE_MIN ? lsg_pair_##name##_pw(__VA_ARGS__) : lsg_pair_##name##_ps(__VA_ARGS__)))
+#define LSG_SERIAL_PICK(name, ng, ...)                                                                    \
+  (lsg_serial_mode() == LSG_SERIAL_SLP                                                                     \
+       ? lsg_slp_##name(__VA_ARGS__)                                                                       \
+       : lsg_serial_mode() == LSG_SERIAL_ROW                                                               \
+             ? ((ng) >= LSG_ROW_WIDE_MIN ? lsg_row_##name##_r1(__VA_ARGS__) : lsg_row_##name##_r4(__VA_ARGS__)) \
+             : ((ng) >= LSG_PAIR_WIDE_MIN ? lsg_pair_##name##_pw(__VA_ARGS__) : lsg_pair_##name##_ps(__VA_ARGS__)))
 inline hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   return LSG_SERIAL_PICK(final_exp, ng, st, ng, F576, verdict);
 }

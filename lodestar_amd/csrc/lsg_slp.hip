@@ -1,0 +1,151 @@
+// lsg_slp.hip -- the per-group serial stages as straight-line programs (tools/gen_slp.py):
+// the final exponentiation (blst finalverify under packages/beacon-node/src/chain/bls/
+// maybeBatch.ts:18,37), the signature-side Miller loop ML(-G1, S_g) of an RLC group and the
+// bucket MSM's Horner fused with that loop.
+//
+// One group per workgroup of W waves.  The program's values live in LDS slots (64 bytes: the
+// pair backend's 7 limbs per lane, lsg_fp_pair.hpp, padded to 8 words); a step holds up to
+// 32 W independent operations and lane pair q of the workgroup executes operation q:
+//   gather its operand forms (up to 7 slots each, 64-bit accumulation of coef * limb, one
+//   carry round), then LIN: store their sum; MUL: store the Montgomery product; LOADMUL:
+//   the product of the item's input Fp #j (read from global memory) with its B form.
+// A dependency chain of ~10^4 products thus runs in ~10^3 steps of one product each, where
+// the row kernels (lsg_serial.hip) spend ~2 us per dependent product.  Inputs and outputs are
+// the canonical byte blobs of lsg_io.hpp, exactly as for the row kernels.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lsg_serial.h"
+
+namespace {
+#include "lsg_fp_pair.hpp"
+#include "lsg_slp_exec.hpp"
+}  // namespace
+
+#define LSG_SLP_ARRAY __device__ const
+#include "lsg_slp_progs.h"
+
+namespace {
+
+enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2 };
+
+template <int PROG>
+struct Prog;
+#define LSG_SLP_PROG(ID, NAME, UP)                                         \
+  template <>                                                              \
+  struct Prog<ID> {                                                        \
+    static constexpr int n_steps = LSG_SLP_##UP##_N_STEPS;                 \
+    static constexpr int n_slots = LSG_SLP_##UP##_N_SLOTS;                 \
+    static constexpr int n_consts = LSG_SLP_##UP##_N_CONSTS;               \
+    static constexpr int n_in = LSG_SLP_##UP##_N_IN;                       \
+    static constexpr int n_load = LSG_SLP_##UP##_N_LOAD;                   \
+    static constexpr int n_out = LSG_SLP_##UP##_N_OUT;                     \
+    static __device__ const uint32_t* ops() { return lsg_slp_##NAME##_ops; }     \
+    static __device__ const uint32_t* steps() { return lsg_slp_##NAME##_steps; } \
+    static __device__ const uint32_t* consts() { return lsg_slp_##NAME##_consts; } \
+    static __device__ const uint16_t* in() { return lsg_slp_##NAME##_in; }       \
+    static __device__ const uint16_t* out() { return lsg_slp_##NAME##_out; }     \
+  };
+LSG_SLP_PROG(SLP_FE, final_exp, FINAL_EXP)
+LSG_SLP_PROG(SLP_ML, miller_neg_g1, MILLER_NEG_G1)
+LSG_SLP_PROG(SLP_HORNER, horner_miller, HORNER_MILLER)
+
+// MODE: 0 = verdict (outputs == Fp12 one), 1 = Fp12 blob with the S = O test (outputs 12, 13
+// are S.Z: the group's term is 1 when S is the point at infinity)
+template <int PROG, int W, int MODE>
+__global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __restrict__ in, uint32_t in_stride,
+                                                uint8_t* __restrict__ out, int32_t* __restrict__ verdict) {
+  using PR = Prog<PROG>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int item = blockIdx.x;
+  if (item >= n_items) return;
+  const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
+  constexpr uint32_t NQ = 32 * W;
+  const uint8_t* inp = in + (size_t)in_stride * item;
+  for (uint32_t j = q; j < (uint32_t)PR::n_consts; j += NQ) {
+    const uint32_t* c = PR::consts() + 14 * j + 7 * h;
+    fp_t v;
+#pragma unroll
+    for (int k = 0; k < 7; k++) v.l[k] = c[k];
+    slot_store(lds, j, h, v);
+  }
+  for (uint32_t j = q; j < (uint32_t)PR::n_in; j += NQ) slot_store(lds, PR::in()[j], h, fp_from_be_bytes(inp + 48 * j, 12));
+  __syncthreads();
+  const uint32_t* ops = PR::ops();
+  const uint32_t* steps = PR::steps();
+#pragma unroll 1
+  for (int s = 0; s < PR::n_steps; s++) {
+    const uint32_t d = steps[s];
+    if (q < (d & 255u)) {
+      const uint4* e = (const uint4*)(ops + 8 * ((d >> 8) + q));
+      const uint4 e0 = e[0], e1 = e[1];
+      const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      slp_exec(lds, ew, inp, h);
+    }
+    __syncthreads();
+  }
+  // outputs: canonical values; lane pair j holds output j (n_out <= 32 W)
+  static_assert(PR::n_out <= 32, "one output per lane pair");
+  __shared__ uint32_t s_flag;
+  fp_t c = fp_zero();
+  bool nz = false;
+  if (q < (uint32_t)PR::n_out) {
+    c = slp_output(lds, PR::out()[q], h);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) x |= c.l[k];
+    x |= pswap(x);
+    nz = x != 0u;
+  }
+  if (MODE == 0) {
+    // FE(F) == 1: output 0 is 1, the others 0
+    bool bad = false;
+    if (q < (uint32_t)PR::n_out) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < 7; k++) x |= (q == 0 && h == 0 && k == 0) ? (c.l[k] ^ 1u) : c.l[k];
+      x |= pswap(x);
+      bad = x != 0u;
+    }
+    if (tid == 0) s_flag = 0;
+    __syncthreads();
+    if (bad) s_flag = 1;  // benign race: every writer stores 1
+    __syncthreads();
+    if (tid == 0) verdict[item] = s_flag ? 0 : 1;
+  } else {
+    // S = O (outputs 12, 13 zero): the group's term is 1
+    if (tid == 0) s_flag = 0;
+    __syncthreads();
+    if ((q == 12 || q == 13) && nz) s_flag = 1;
+    __syncthreads();
+    const bool inf = s_flag == 0;
+    if (q < 12) {
+      fp_t v = c;
+      if (inf) {
+        v = fp_zero();
+        if (q == 0 && h == 0) v.l[0] = 1u;
+      }
+      fp_to_be48(out + (size_t)576 * item + 48 * q, v);
+    }
+  }
+}
+
+template <int PROG, int W, int MODE>
+hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, uint8_t* out, int32_t* verdict) {
+  if (n <= 0) return hipSuccess;
+  const size_t shm = (size_t)Prog<PROG>::n_slots * 64;
+  hipLaunchKernelGGL((k_slp<PROG, W, MODE>), dim3(n), dim3(64 * W), shm, st, n, in, in_stride, out, verdict);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
+  return launch<SLP_FE, 1, 0>(st, ng, F576, 576, nullptr, verdict);
+}
+hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
+  return launch<SLP_ML, 1, 1>(st, ng, S288, 288, out576, nullptr);
+}
+hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
+  return launch<SLP_HORNER, 1, 1>(st, ng, C288, 288 * 64, out576, nullptr);
+}

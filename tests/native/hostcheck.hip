@@ -339,3 +339,42 @@ void hc_opcount(const uint8_t* sig96, const uint8_t* pk96, const uint8_t* msg32,
   counts[10] = lsg_mul_count;
 }
 }
+
+#ifdef LSG_HOSTCHECK_PAIR
+// ---- the straight-line programs of the serial stages (tools/gen_slp.py), executed op by op
+// with the gfx950 interpreter's own operation code (lsg_slp_exec.hpp) on the host
+#include <vector>
+#include "lsg_slp_exec.hpp"
+#include "lsg_slp_progs.h"
+struct HcProg {
+  const uint32_t *ops, *steps, *consts;
+  const uint16_t *in, *out;
+  int n_steps, n_slots, n_consts, n_in, n_out;
+};
+#define HC_PROG(NAME, UP)                                                                                  \
+  HcProg{lsg_slp_##NAME##_ops, lsg_slp_##NAME##_steps, lsg_slp_##NAME##_consts, lsg_slp_##NAME##_in,       \
+         lsg_slp_##NAME##_out, LSG_SLP_##UP##_N_STEPS, LSG_SLP_##UP##_N_SLOTS, LSG_SLP_##UP##_N_CONSTS,      \
+         LSG_SLP_##UP##_N_IN, LSG_SLP_##UP##_N_OUT}
+extern "C" {
+// prog: 0 final_exp, 1 miller_neg_g1, 2 horner_miller; in: the item's input blob; out: the
+// canonical outputs (48 bytes each).  Returns the output count.
+int hc_slp_run(int prog, const uint8_t* in, uint8_t* out) {
+  const HcProg P[3] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
+                       HC_PROG(horner_miller, HORNER_MILLER)};
+  const HcProg& p = P[prog];
+  std::vector<uint32_t> lds((size_t)p.n_slots * 16, 0xdeadbeefu);
+  for (int j = 0; j < p.n_consts; j++) {
+    fp_t v;
+    for (int k = 0; k < 14; k++) v.l[k] = p.consts[14 * j + k];
+    slot_store(lds.data(), j, 0, v);
+  }
+  for (int j = 0; j < p.n_in; j++) slot_store(lds.data(), p.in[j], 0, fp_from_be_bytes(in + 48 * j, 12));
+  for (int s = 0; s < p.n_steps; s++) {
+    const uint32_t d = p.steps[s];
+    for (uint32_t q = 0; q < (d & 255u); q++) slp_exec(lds.data(), p.ops + 8 * ((d >> 8) + q), in, 0);
+  }
+  for (int j = 0; j < p.n_out; j++) fp_to_be48(out + 48 * j, slp_output(lds.data(), p.out[j], 0));
+  return p.n_out;
+}
+}
+#endif

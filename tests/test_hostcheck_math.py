@@ -298,3 +298,46 @@ def test_g1_subgroup_check(hc):
     for pt in pts:
         assert hc.hc_g1_in_group(g1_serialize(pt)) == (1 if in_g1(pt) else 0)
     assert hc.hc_g1_in_group(g1_serialize(None)) == 1
+
+
+def _g2_proj_blob(Q, z):
+    """homogeneous projective blob (X, Y, Z) = (x z, y z, z) of an affine point; None -> (0, 1, 0)"""
+    if Q is None:
+        return b2((0, 0)) + b2((1, 0)) + b2((0, 0))
+    x, y = Q
+    return b2(f2_mul(x, z)) + b2(f2_mul(y, z)) + b2(z)
+
+
+def test_slp_programs_match_oracle(hc):
+    """The straight-line programs of the serial stages (tools/gen_slp.py), run op by op with
+    the gfx950 interpreter's own operation code (lsg_slp_exec.hpp) in the host build of the
+    pair backend: final exponentiation, ML(-G1, S) and Horner + ML(-G1, S) against the
+    oracle (oracle/pairing.py final_exp_fast, miller_loop_fast)."""
+    if hc.backend != "pair":
+        pytest.skip("programs run on the pair backend")
+    from oracle.fields import f12_mul, F12_ONE
+    neg_g1 = E1.neg(G1_GEN) if hasattr(E1, "neg") else (G1_GEN[0], (-G1_GEN[1]) % P)
+    o = buf(48 * 14)
+    # final exponentiation: a random element and a pairing product that is 1 after it
+    pk = E1.mul(G1_GEN, 4242)
+    Q = E2.mul(G2_GEN, 31337)
+    prod = f12_mul(miller_loop_fast(pk, Q), miller_loop_fast(neg_g1, E2.mul(Q, 4242)))
+    for f in (rf12(), prod):
+        assert hc.hc_slp_run(0, b12(f), o) == 12
+        assert ub12(o.raw[:576]) == final_exp_fast(f)
+    assert final_exp_fast(prod) == F12_ONE
+    # ML(-G1, S) of a projective S, and S.Z
+    for k in (1, 77, 123456789):
+        S = E2.mul(G2_GEN, k)
+        z = rf2()
+        assert hc.hc_slp_run(1, _g2_proj_blob(S, z), o) == 14
+        assert ub12(o.raw[:576]) == miller_loop_fast(neg_g1, S)
+        assert ub2(o.raw[576:672]) == z
+    # Horner over 64 per-bit sums (some at infinity), then ML(-G1, S)
+    Cs = [None if k % 5 == 3 else E2.mul(G2_GEN, 1000 + 17 * k) for k in range(64)]
+    blob = b"".join(_g2_proj_blob(C, rf2()) for C in Cs)
+    S = None
+    for k in range(63, -1, -1):
+        S = E2.add(E2.add(S, S), Cs[k])
+    assert hc.hc_slp_run(2, blob, o) == 14
+    assert ub12(o.raw[:576]) == miller_loop_fast(neg_g1, S)

@@ -1,0 +1,1016 @@
+#!/usr/bin/env python3
+"""Build tool: straight-line programs (SLPs) for the per-group serial stages.
+
+A final exponentiation (blst finalverify under packages/beacon-node/src/chain/bls/
+maybeBatch.ts:18,37) or the signature-side Miller loop ML(-G1, sum r_i sig_i) of one RLC
+group is a single dependency chain of ~10^4 Fp products.  Run as ordinary code it leaves a
+wave64 waiting on one product at a time.  Here the chain is traced ONCE, at build time, into
+a data-independent program of Fp operations over numbered value slots:
+
+    MUL      dst = mont(sum_k a_k slot_k, sum_k b_k slot_k)      (Montgomery product)
+    LIN      dst = sum_k c_k slot_k                              (small signed coefficients)
+    LOADMUL  dst = mont(input Fp #j of the item, sum_k b_k slot_k)  (input conversion)
+
+list-scheduled into steps of at most 32*W independent operations (critical path first) and
+register-allocated into LDS slots.  lodestar_amd/csrc/lsg_slp.hip interprets the program
+with one item per workgroup: in every step each lane PAIR of the W waves takes one operation
+(pair backend: 14 limbs of 29 bits, lsg_fp_pair.hpp), gathers its operand forms from LDS,
+multiplies and writes the result back.  A batch of 18 independent products then costs about
+what one product costs, so a chain of 10^4 products runs in ~10^3 steps.
+
+Linear combinations never get a step of their own when they can ride along: an operand of a
+MUL is a form of up to 7 slots with coefficients in [-32, 31], gathered with 64-bit
+accumulation and one carry round.  Value bounds are tracked (|v| < B p with B <= 2^12, the
+pair backend's lazy range); a form that would exceed the limits is materialised by a LIN op,
+a value that grows too large is tamed by a product with Montgomery one.
+
+The algorithms below restate lodestar_amd/csrc/lsg_pairing.hpp (itself the mirror of
+oracle/pairing.py): the Miller loop uses exactly the same projective doubling/addition steps
+and line scalings, so Miller values are bit-identical to the other kernels'; field
+arithmetic formulas (Karatsuba towers, Granger-Scott squaring) only have to be correct.
+Every program is checked here, at generation time, by running the emitted op list
+(scheduling and slot allocation included) on random inputs against a direct evaluation of the
+same algorithm with Python integers.  Standalone: does not import oracle/ (the checker).
+
+usage: gen_slp.py OUT.h [--check N]
+"""
+import heapq
+import os
+import random
+import sys
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+X_ABS = 0xD201000000010000
+NLIMB, LBITS = 14, 29
+R = 1 << (NLIMB * LBITS)  # Montgomery radix of the pair backend (2^406)
+RINV = pow(R, -1, P)
+# Bounds (|v| < B p).  The pair backend's product w = (a b + m p) / R, 0 <= m < R = 2^406,
+# satisfies -p < w < 2p whenever B_a B_b <= 2^25 (p / R < 2^-25); stored values stay below
+# 2^20 p (the signed top limb then holds < 2^24, the 64-bit accumulators never overflow).
+MUL_BB = 1 << 24  # B_a * B_b of a product's operands
+MAXB = 1 << 12  # operand bound when both operands are large
+LIN_MAX = 1 << 20  # any stored value
+MAX_TERMS = 7  # terms per operand form (A and B each)
+COEF_MIN, COEF_MAX = -32, 31
+SLOT_BITS = 10
+MAX_SLOTS = 1 << SLOT_BITS
+W_LAT = {"mul": 1.0, "loadmul": 1.0, "lin": 0.25}  # step costs relative to one product
+COMBINE_TERMS = int(os.environ.get("LSG_SLP_COMBINE", "12"))  # a form built by +/- keeps up to this many terms
+COMBINE_KEEP = int(os.environ.get("LSG_SLP_KEEP", "7"))  # ... and is cut back to this many
+
+
+# ----------------------------------------------------------------------------- engines
+class IntF:
+    """concrete Fp element (standard representation) -- the generator's reference evaluator"""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v % P
+
+    def __add__(self, o):
+        return IntF(self.v + o.v)
+
+    def __sub__(self, o):
+        return IntF(self.v - o.v)
+
+    def __neg__(self):
+        return IntF(-self.v)
+
+    def __mul__(self, o):
+        if isinstance(o, int):
+            return IntF(self.v * o)
+        return IntF(self.v * o.v)
+
+    __rmul__ = __mul__
+
+
+class IntEngine:
+    def const(self, v):
+        return IntF(v)
+
+    def zero(self):
+        return IntF(0)
+
+
+class Sym:
+    """a linear form sum_k c_k * value_k over the program's values (Montgomery domain)"""
+    __slots__ = ("cx", "t")
+
+    def __init__(self, cx, t):
+        self.cx = cx
+        self.t = t
+
+    def _combine(self, o, sign):
+        t = dict(self.t)
+        for v, c in o.t.items():
+            t[v] = t.get(v, 0) + sign * c
+        return Sym(self.cx, self.cx.shape({v: c for v, c in t.items() if c}))
+
+    def __add__(self, o):
+        return self._combine(o, 1)
+
+    def __sub__(self, o):
+        return self._combine(o, -1)
+
+    def __neg__(self):
+        return Sym(self.cx, {k: -c for k, c in self.t.items()})
+
+    def __mul__(self, o):
+        if isinstance(o, int):
+            t = self.t
+            if self.cx._fbound(t.items()) * abs(o) > LIN_MAX // 64:
+                t = dict(self.cx.fit(t, MAX_TERMS, max(2, LIN_MAX // (64 * abs(o)))))
+            return Sym(self.cx, self.cx.shape({k: c * o for k, c in t.items() if c * o}))
+        return self.cx.mul(self, o)
+
+    def __rmul__(self, o):
+        assert isinstance(o, int)
+        return self.__mul__(o)
+
+
+class Ctx:
+    """records a program: values are inputs, constants or op results.  Forms are kept
+    expanded over op results as long as they stay small; when one must shrink, its OLDEST
+    terms (earliest ready-time estimate) are collapsed into one LIN value -- that value is
+    ready long before the recent terms (the products just made), so the LIN stays off the
+    critical path of the chain"""
+
+    def __init__(self, name, n_inputs, load_inputs=False):
+        self.name = name
+        self.ops = []  # [kind, dst, A terms, B terms, input index]
+        self.bound = []  # per value: |v| < bound * p
+        self.est = []  # per value: ready time estimate (products = 1, LIN = 0.25)
+        self.prod = []  # per value: producing op index, or -1 (input/constant)
+        self.consts = {}  # raw slot content -> value id
+        self.const_list = []  # (value id, raw content)
+        self.inputs = []  # value ids of raw inputs (non-LOADMUL programs)
+        self.outputs = []
+        self.memo = {}  # materialised term tuples -> value id
+        self.n_inputs = n_inputs
+        self.load_inputs = load_inputs
+        self.one = self._raw_const(R % P)  # Montgomery one (taming)
+
+    def _new(self, bound, prod, est=0.0):
+        self.bound.append(bound)
+        self.prod.append(prod)
+        self.est.append(est)
+        return len(self.bound) - 1
+
+    def _raw_const(self, raw):
+        if raw not in self.consts:
+            v = self._new(1, -1)
+            self.consts[raw] = v
+            self.const_list.append((v, raw))
+        return self.consts[raw]
+
+    def form_est(self, vs):
+        return max((self.est[v] for v in vs), default=0.0)
+
+    # ---- engine interface
+    def const(self, value):
+        return Sym(self, {self._raw_const(value * R % P): 1})
+
+    def zero(self):
+        return Sym(self, {})
+
+    def input(self, j):
+        """input Fp #j of the item in Montgomery form"""
+        if self.load_inputs:
+            v = self._new(2, len(self.ops), 1.0)
+            self.ops.append(["loadmul", v, [], [(self._raw_const(R * R % P), 1)], j])
+            return Sym(self, {v: 1})
+        raw = self._new(1, -1)
+        self.inputs.append(raw)
+        return self._mul_forms([(raw, 1)], [(self._raw_const(R * R % P), 1)])
+
+    # ---- forms
+    def _fbound(self, terms):
+        return sum(abs(c) * self.bound[v] for v, c in terms)
+
+    def _lin(self, terms):
+        d = self._new(self._fbound(terms), len(self.ops), self.form_est(v for v, _ in terms) + W_LAT["lin"])
+        assert self.bound[d] <= LIN_MAX, self.bound[d]
+        self.ops.append(["lin", d, terms[:MAX_TERMS], terms[MAX_TERMS:], -1])
+        return d
+
+    def _tame_id(self, v):
+        d = self._new(2, len(self.ops), self.est[v] + 1)
+        self.ops.append(["mul", d, [(v, 1)], [(self.one, 1)], -1])
+        return d
+
+    def mat_terms(self, items, tame=False):
+        """one value id holding sum c v over items (memoised); tame: reduced below 2p by a
+        product with Montgomery one"""
+        items = [(v, c) for v, c in items if c]
+        if not items:
+            return self._raw_const(0)
+        if len(items) == 1 and items[0][1] == 1 and (not tame or self.bound[items[0][0]] <= 2):
+            return items[0][0]
+        key = (tuple(sorted(items)), tame)
+        if key in self.memo:
+            return self.memo[key]
+        terms = []
+        for v, c in items:  # coefficients outside the encodable range: repeat the term
+            while c > COEF_MAX or c < COEF_MIN:
+                step = COEF_MAX if c > 0 else COEF_MIN
+                terms.append((v, step))
+                c -= step
+            if c:
+                terms.append((v, c))
+        while self._fbound(terms) > LIN_MAX:  # tame the largest contributions until it fits
+            k = max(range(len(terms)), key=lambda i: abs(terms[i][1]) * self.bound[terms[i][0]])
+            v, c = terms[k]
+            if self.bound[v] <= 2:
+                raise ValueError("form too large even with tamed terms")
+            terms[k] = (self._tame_id(v), c)
+        while len(terms) > 2 * MAX_TERMS:
+            head = self._lin(terms[:2 * MAX_TERMS])
+            terms = [(head, 1)] + terms[2 * MAX_TERMS:]
+        d = self._lin(terms) if not (len(terms) == 1 and terms[0][1] == 1) else terms[0][0]
+        if tame and self.bound[d] > 2:
+            d = self._tame_id(d)
+        self.memo[key] = d
+        return d
+
+    def fit(self, t, max_terms, max_bound):
+        """the form t as <= max_terms encodable terms of bound <= max_bound: its oldest terms
+        collapsed into one value (tamed when the bound needs it) when necessary"""
+        items = [(v, c) for v, c in t.items() if c]
+
+        def enc(it):
+            return all(COEF_MIN <= c <= COEF_MAX for _, c in it)
+
+        if len(items) <= max_terms and enc(items) and self._fbound(items) <= max_bound:
+            return items
+        # out-of-range coefficients first, then oldest first
+        items.sort(key=lambda vc: (COEF_MIN <= vc[1] <= COEF_MAX, self.est[vc[0]], vc[0]))
+        for m in range(1, len(items) + 1):
+            old, rest = items[:m], items[m:]
+            if len(rest) + 1 > max_terms or not enc(rest):
+                continue
+            b_rest, b_old = self._fbound(rest), self._fbound(old)
+            if b_rest + min(b_old, 2) > max_bound:
+                continue
+            tame = b_rest + b_old > max_bound or b_old > LIN_MAX
+            if m == 1 and not tame and enc(old):
+                continue
+            return [(self.mat_terms(old, tame), 1)] + rest
+        return [(self.mat_terms(items, True), 1)]
+
+    def shape(self, t):
+        """keep a combined form within the working size"""
+        if len(t) <= COMBINE_TERMS and self._fbound(t.items()) <= LIN_MAX // 64:
+            return t
+        return dict(self.fit(t, COMBINE_KEEP, LIN_MAX // 64))
+
+    def _mul_forms(self, A, B):
+        d = self._new(2, len(self.ops), self.form_est(v for v, _ in A + B) + 1)
+        self.ops.append(["mul", d, A, B, -1])
+        return Sym(self, {d: 1})
+
+    def mul(self, a, b):
+        if not a.t or not b.t:
+            return self.zero()
+        # the smaller operand first; the other may then be as large as the product allows
+        if self._fbound(a.t.items()) < self._fbound(b.t.items()):
+            a, b = b, a
+        B = self.fit(b.t, MAX_TERMS, MAXB)
+        A = self.fit(a.t, MAX_TERMS, min(LIN_MAX, MUL_BB // max(1, self._fbound(B))))
+        return self._mul_forms(A, B)
+
+    def output(self, s):
+        """an output Fp: converted out of Montgomery form (in (-p, 2p), canonicalised by the
+        kernel)"""
+        A = self.fit(s.t, MAX_TERMS, LIN_MAX) if s.t else [(self._raw_const(0), 1)]
+        B = [(self._raw_const(1), 1)]
+        d = self._new(2, len(self.ops))
+        self.ops.append(["mul", d, A, B, -1])
+        self.outputs.append(d)
+
+
+# ----------------------------------------------------------------------------- tower
+# Fp2 = Fp[u]/(u^2 + 1), Fp6 = Fp2[v]/(v^3 - xi), xi = 1 + u, Fp12 = Fp6[w]/(w^2 - v)
+# (lsg_tower.hpp); elements are tuples of engine values.
+def f2_add(a, b):
+    return (a[0] + b[0], a[1] + b[1])
+
+
+def f2_sub(a, b):
+    return (a[0] - b[0], a[1] - b[1])
+
+
+def f2_neg(a):
+    return (-a[0], -a[1])
+
+
+def f2_conj(a):
+    return (a[0], -a[1])
+
+
+def f2_muls(a, k):
+    return (a[0] * k, a[1] * k)
+
+
+def f2_mul(a, b):
+    t0 = a[0] * b[0]
+    t1 = a[1] * b[1]
+    t2 = (a[0] + a[1]) * (b[0] + b[1])
+    return (t0 - t1, t2 - t0 - t1)
+
+
+def f2_sqr(a):
+    return ((a[0] + a[1]) * (a[0] - a[1]), 2 * (a[0] * a[1]))
+
+
+def f2_mul_fp(a, s):
+    return (a[0] * s, a[1] * s)
+
+
+def f2_mul_xi(a):
+    return (a[0] - a[1], a[0] + a[1])
+
+
+def f2_zero(E):
+    return (E.zero(), E.zero())
+
+
+def f2_one(E):
+    return (E.const(1), E.zero())
+
+
+def f2_const(E, c):
+    return (E.const(c[0]), E.const(c[1]))
+
+
+def fp_pow(E, a, e):
+    """a^e, sliding window of 4 (fixed public exponent)"""
+    a2 = a * a
+    T = [a]
+    for _ in range(7):
+        T.append(T[-1] * a2)
+    bits = bin(e)[2:]
+    i = 0
+    r = None
+    while i < len(bits):
+        if bits[i] == "0":
+            r = r * r
+            i += 1
+            continue
+        j = min(i + 4, len(bits))
+        while bits[j - 1] == "0":
+            j -= 1
+        val = int(bits[i:j], 2)
+        if r is not None:
+            for _ in range(j - i):
+                r = r * r
+            r = r * T[val >> 1]
+        else:
+            r = T[val >> 1]
+        i = j
+    return r
+
+
+def fp_inv(E, a):
+    return fp_pow(E, a, P - 2)
+
+
+def f2_inv(E, a):
+    n = a[0] * a[0] + a[1] * a[1]
+    ni = fp_inv(E, n)
+    return (a[0] * ni, -(a[1] * ni))
+
+
+def f6_add(a, b):
+    return tuple(f2_add(x, y) for x, y in zip(a, b))
+
+
+def f6_sub(a, b):
+    return tuple(f2_sub(x, y) for x, y in zip(a, b))
+
+
+def f6_neg(a):
+    return tuple(f2_neg(x) for x in a)
+
+
+def f6_mul_v(a):
+    return (f2_mul_xi(a[2]), a[0], a[1])
+
+
+def f6_mul(a, b):
+    v0 = f2_mul(a[0], b[0])
+    v1 = f2_mul(a[1], b[1])
+    v2 = f2_mul(a[2], b[2])
+    c0 = f2_add(v0, f2_mul_xi(f2_sub(f2_sub(f2_mul(f2_add(a[1], a[2]), f2_add(b[1], b[2])), v1), v2)))
+    c1 = f2_add(f2_sub(f2_sub(f2_mul(f2_add(a[0], a[1]), f2_add(b[0], b[1])), v0), v1), f2_mul_xi(v2))
+    c2 = f2_add(f2_sub(f2_sub(f2_mul(f2_add(a[0], a[2]), f2_add(b[0], b[2])), v0), v2), v1)
+    return (c0, c1, c2)
+
+
+def f6_mul_01(a, b0, b1):
+    v0 = f2_mul(a[0], b0)
+    v1 = f2_mul(a[1], b1)
+    c0 = f2_add(f2_mul_xi(f2_mul(a[2], b1)), v0)
+    c1 = f2_sub(f2_sub(f2_mul(f2_add(a[0], a[1]), f2_add(b0, b1)), v0), v1)
+    c2 = f2_add(f2_mul(a[2], b0), v1)
+    return (c0, c1, c2)
+
+
+def f6_mul_1(a, b1):
+    return (f2_mul_xi(f2_mul(a[2], b1)), f2_mul(a[0], b1), f2_mul(a[1], b1))
+
+
+def f6_inv(E, a):
+    t0 = f2_sub(f2_sqr(a[0]), f2_mul_xi(f2_mul(a[1], a[2])))
+    t1 = f2_sub(f2_mul_xi(f2_sqr(a[2])), f2_mul(a[0], a[1]))
+    t2 = f2_sub(f2_sqr(a[1]), f2_mul(a[0], a[2]))
+    den = f2_add(f2_mul(a[0], t0), f2_mul_xi(f2_add(f2_mul(a[2], t1), f2_mul(a[1], t2))))
+    di = f2_inv(E, den)
+    return (f2_mul(t0, di), f2_mul(t1, di), f2_mul(t2, di))
+
+
+def f12_mul(a, b):
+    t0 = f6_mul(a[0], b[0])
+    t1 = f6_mul(a[1], b[1])
+    t2 = f6_mul(f6_add(a[0], a[1]), f6_add(b[0], b[1]))
+    return (f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(t2, t0), t1))
+
+
+def f12_sqr(a):
+    t = f6_mul(a[0], a[1])
+    u = f6_mul(f6_add(a[0], a[1]), f6_add(a[0], f6_mul_v(a[1])))
+    return (f6_sub(f6_sub(u, t), f6_mul_v(t)), f6_add(t, t))
+
+
+def f12_conj(a):
+    return (a[0], f6_neg(a[1]))
+
+
+def f12_inv(E, a):
+    t = f6_sub(f6_mul(a[0], a[0]), f6_mul_v(f6_mul(a[1], a[1])))
+    ti = f6_inv(E, t)
+    return (f6_mul(a[0], ti), f6_neg(f6_mul(a[1], ti)))
+
+
+def f12_one(E):
+    z = f2_zero(E)
+    return ((f2_one(E), z, z), (z, z, z))
+
+
+def f12_mul_line(f, l00, l01, l11):
+    t0 = f6_mul_01(f[0], l00, l01)
+    u = f6_mul_01(f6_add(f[0], f[1]), l00, f2_add(l01, l11))
+    t1 = f6_mul_1(f[1], l11)
+    return (f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(u, t0), t1))
+
+
+def _f2pow(a, e):
+    def m(x, y):
+        return ((x[0] * y[0] - x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = m(r, a)
+        a = m(a, a)
+        e >>= 1
+    return r
+
+
+XI = (1, 1)
+G1C = [_f2pow(XI, j * (P - 1) // 6) for j in range(6)]  # frobenius: coefficient of w^j
+G2C = [_f2pow(XI, j * (P * P - 1) // 6) for j in range(6)]
+
+
+def f12_frob(E, a):
+    # w^j order: c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2
+    c = [a[0][0], a[1][0], a[0][1], a[1][1], a[0][2], a[1][2]]
+    r = [f2_conj(c[0])] + [f2_mul(f2_conj(c[j]), f2_const(E, G1C[j])) for j in range(1, 6)]
+    return ((r[0], r[2], r[4]), (r[1], r[3], r[5]))
+
+
+def f12_frob2(E, a):
+    c = [a[0][0], a[1][0], a[0][1], a[1][1], a[0][2], a[1][2]]
+    r = [c[0]] + [f2_mul_fp(c[j], E.const(G2C[j][0])) for j in range(1, 6)]
+    assert all(G2C[j][1] == 0 for j in range(6))
+    return ((r[0], r[2], r[4]), (r[1], r[3], r[5]))
+
+
+def fp4_square(a, b):
+    t0 = f2_sqr(a)
+    t1 = f2_sqr(b)
+    c0 = f2_add(f2_mul_xi(t1), t0)
+    c1 = f2_sub(f2_sub(f2_sqr(f2_add(a, b)), t0), t1)
+    return c0, c1
+
+
+def f12_cyc_sqr(f):
+    """Granger-Scott squaring (f in the cyclotomic subgroup), lsg_tower.hpp:412"""
+    z0, z4, z3 = f[0]
+    z2, z1, z5 = f[1]
+    t0, t1 = fp4_square(z0, z1)
+    u0, u1 = fp4_square(z2, z3)
+    t2, t3 = fp4_square(z4, z5)
+    z0 = f2_add(f2_muls(f2_sub(t0, z0), 2), t0)
+    z1 = f2_add(f2_muls(f2_add(t1, z1), 2), t1)
+    z4 = f2_add(f2_muls(f2_sub(u0, z4), 2), u0)
+    z5 = f2_add(f2_muls(f2_add(u1, z5), 2), u1)
+    t0 = f2_mul_xi(t3)
+    z2 = f2_add(f2_muls(f2_add(t0, z2), 2), t0)
+    z3 = f2_add(f2_muls(f2_sub(t2, z3), 2), t2)
+    return ((z0, z4, z3), (z2, z1, z5))
+
+
+def f12_exp_by_x(g):
+    r = g
+    for b in range(62, -1, -1):
+        r = f12_cyc_sqr(r)
+        if (X_ABS >> b) & 1:
+            r = f12_mul(r, g)
+    return f12_conj(r)
+
+
+def final_exp(E, f):
+    """f^(3 (p^12 - 1)/r), lsg_pairing.hpp:318"""
+    f1 = f12_mul(f12_conj(f), f12_inv(E, f))
+    g = f12_mul(f12_frob2(E, f1), f1)
+    t0 = f12_mul(f12_exp_by_x(g), f12_conj(g))
+    t0 = f12_mul(f12_exp_by_x(t0), f12_conj(t0))
+    t1 = f12_mul(f12_exp_by_x(t0), f12_frob(E, t0))
+    t2 = f12_mul(f12_mul(f12_exp_by_x(f12_exp_by_x(t1)), f12_frob2(E, t1)), f12_conj(t1))
+    return f12_mul(t2, f12_mul(f12_sqr(g), g))
+
+
+# ----------------------------------------------------------------------------- curve
+B3 = 12  # 3 b' with b' = 4 (1 + u): fp2_mul_b3(a) = 12 xi a
+
+
+def f2_mul_b3(a):
+    return f2_muls(f2_mul_xi(a), B3)
+
+
+def g2_add(p, q):
+    """RCB 2016 algorithm 7 (complete addition, a = 0), lsg_curve.hpp:82"""
+    X1, Y1, Z1 = p
+    X2, Y2, Z2 = q
+    t0 = f2_mul(X1, X2)
+    t1 = f2_mul(Y1, Y2)
+    t2 = f2_mul(Z1, Z2)
+    t3 = f2_sub(f2_mul(f2_add(X1, Y1), f2_add(X2, Y2)), f2_add(t0, t1))
+    t4 = f2_sub(f2_mul(f2_add(Y1, Z1), f2_add(Y2, Z2)), f2_add(t1, t2))
+    Y3 = f2_sub(f2_mul(f2_add(X1, Z1), f2_add(X2, Z2)), f2_add(t0, t2))
+    t0 = f2_muls(t0, 3)
+    t2 = f2_mul_b3(t2)
+    Z3 = f2_add(t1, t2)
+    t1 = f2_sub(t1, t2)
+    Y3 = f2_mul_b3(Y3)
+    X3 = f2_sub(f2_mul(t3, t1), f2_mul(t4, Y3))
+    Y3 = f2_add(f2_mul(t1, Z3), f2_mul(Y3, t0))
+    Z3 = f2_add(f2_mul(Z3, t4), f2_mul(t0, t3))
+    return (X3, Y3, Z3)
+
+
+def g2_dbl(p):
+    """RCB 2016 algorithm 9 (doubling, a = 0), lsg_curve.hpp:151"""
+    X, Y, Z = p
+    t0 = f2_sqr(Y)
+    Z3 = f2_muls(t0, 8)
+    t1 = f2_mul(Y, Z)
+    t2 = f2_mul_b3(f2_sqr(Z))
+    X3 = f2_mul(t2, Z3)
+    Y3 = f2_add(t0, t2)
+    Z3 = f2_mul(t1, Z3)
+    t0 = f2_sub(t0, f2_muls(t2, 3))
+    Y3 = f2_add(X3, f2_mul(t0, Y3))
+    X3 = f2_muls(f2_mul(t0, f2_mul(X, Y)), 2)
+    return (X3, Y3, Z3)
+
+
+def ml_dbl_step(T):
+    """T <- 2T and its unevaluated line, lsg_pairing.hpp:17 (same representatives)"""
+    X, Y, Z = T
+    t0 = f2_sqr(Y)
+    t1 = f2_mul(Y, Z)
+    t2 = f2_mul_b3(f2_sqr(Z))
+    XX = f2_sqr(X)
+    l00 = f2_sub(t2, t0)
+    l01 = f2_muls(XX, 3)
+    l11 = f2_neg(f2_muls(t1, 2))
+    Z3 = f2_muls(t0, 8)
+    X3 = f2_mul(t2, Z3)
+    Y3 = f2_add(t0, t2)
+    Z3 = f2_mul(t1, Z3)
+    s0 = f2_sub(t0, f2_muls(t2, 3))
+    Y3 = f2_add(X3, f2_mul(s0, Y3))
+    X3 = f2_muls(f2_mul(s0, f2_mul(X, Y)), 2)
+    return (X3, Y3, Z3), (l00, l01, l11)
+
+
+def ml_add_step(T, Q):
+    """T <- T + Q (Q affine) and its unevaluated line, lsg_pairing.hpp:48"""
+    X, Y, Z = T
+    qx, qy = Q
+    theta = f2_sub(Y, f2_mul(qy, Z))
+    delta = f2_sub(X, f2_mul(qx, Z))
+    l00 = f2_sub(f2_mul(delta, qy), f2_mul(theta, qx))
+    l01 = theta
+    l11 = f2_neg(delta)
+    C = f2_sqr(theta)
+    D = f2_sqr(delta)
+    Ee = f2_mul(D, delta)
+    F = f2_mul(Z, C)
+    G = f2_mul(X, D)
+    H = f2_sub(f2_add(Ee, F), f2_muls(G, 2))
+    X3 = f2_mul(delta, H)
+    Y3 = f2_sub(f2_mul(theta, f2_sub(G, H)), f2_mul(Ee, Y))
+    Z3 = f2_mul(Ee, Z)
+    return (X3, Y3, Z3), (l00, l01, l11)
+
+
+def miller_loop(E, Pxy, Q):
+    """f_{|x|,Q}(P) conjugated, lsg_pairing.hpp:173 (P affine G1, Q affine G2)"""
+    xP, yP = Pxy
+
+    def ev(L):
+        return (L[0], f2_mul_fp(L[1], xP), f2_mul_fp(L[2], yP))
+
+    T = (Q[0], Q[1], f2_one(E))
+    T, L = ml_dbl_step(T)
+    L = ev(L)
+    z = f2_zero(E)
+    f = ((L[0], L[1], z), (z, L[2], z))
+    T, L = ml_add_step(T, Q)
+    f = f12_mul_line(f, *ev(L))
+    for b in range(61, -1, -1):
+        f = f12_sqr(f)
+        T, L = ml_dbl_step(T)
+        f = f12_mul_line(f, *ev(L))
+        if (X_ABS >> b) & 1:
+            T, L = ml_add_step(T, Q)
+            f = f12_mul_line(f, *ev(L))
+    return f12_conj(f)
+
+
+G1X = 0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB
+G1Y = 0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1
+
+
+def proj_to_aff(E, p):
+    zi = f2_inv(E, p[2])
+    return (f2_mul(p[0], zi), f2_mul(p[1], zi))
+
+
+def ml_neg_g1(E, S):
+    """ML(-G1, S) for S projective (lsg_serial.hip:44); the caller substitutes 1 when S = O"""
+    return miller_loop(E, (E.const(G1X), E.const(P - G1Y)), proj_to_aff(E, S))
+
+
+def horner(Cs):
+    """S = sum_k 2^k C_k by Horner over the 64 per-bit sums (lsg_serial.hip:63)"""
+    s = Cs[63]
+    for k in range(62, -1, -1):
+        s = g2_add(g2_dbl(s), Cs[k])
+    return s
+
+
+# ----------------------------------------------------------------------------- programs
+def flat12(f):
+    return [x for c6 in f for c2 in c6 for x in c2]
+
+
+def unflat12(v):
+    return tuple(tuple((v[6 * a + 2 * b], v[6 * a + 2 * b + 1]) for b in range(3)) for a in range(2))
+
+
+def g2p_from(v, o=0):
+    return ((v[o], v[o + 1]), (v[o + 2], v[o + 3]), (v[o + 4], v[o + 5]))
+
+
+def prog_final_exp(E, inp):
+    """in: F (12 Fp, tower order); out: FE(F) (12 Fp) -- the kernel compares with one"""
+    return flat12(final_exp(E, unflat12(inp(12))))
+
+
+def prog_miller_neg_g1(E, inp):
+    """in: S projective (6 Fp); out: ML(-G1, S) (12 Fp) and S.Z (2 Fp: S = O test)"""
+    v = inp(6)
+    S = g2p_from(v)
+    return flat12(ml_neg_g1(E, S)) + list(S[2])
+
+
+def prog_horner_miller(E, inp):
+    """in: 64 per-bit sums C_k (64 x 6 Fp); out: ML(-G1, S) (12 Fp) and S.Z (2 Fp)"""
+    v = inp(384)
+    S = horner([g2p_from(v, 6 * k) for k in range(64)])
+    return flat12(ml_neg_g1(E, S)) + list(S[2])
+
+
+PROGRAMS = {
+    # name: (builder, n_inputs, inputs loaded by LOADMUL ops inside the program)
+    "final_exp": (prog_final_exp, 12, False),
+    "miller_neg_g1": (prog_miller_neg_g1, 6, False),
+    "horner_miller": (prog_horner_miller, 384, True),
+}
+
+
+def trace(name):
+    fn, n_in, load = PROGRAMS[name]
+    cx = Ctx(name, n_in, load)
+    ins = [None]
+
+    def inp(n):
+        assert n == n_in
+        ins[0] = [cx.input(j) for j in range(n)]
+        return ins[0]
+
+    outs = fn(cx, inp)
+    for o in outs:
+        cx.output(o)
+    return cx
+
+
+# ----------------------------------------------------------------------------- schedule
+def dce(cx):
+    live = [False] * len(cx.ops)
+    stack = [cx.prod[v] for v in cx.outputs if cx.prod[v] >= 0]
+    while stack:
+        i = stack.pop()
+        if live[i]:
+            continue
+        live[i] = True
+        for v, _ in cx.ops[i][2] + cx.ops[i][3]:
+            if cx.prod[v] >= 0 and not live[cx.prod[v]]:
+                stack.append(cx.prod[v])
+    return [i for i in range(len(cx.ops)) if live[i]]
+
+
+def schedule(cx, W, earliest=None):
+    """list scheduling: steps of <= 32 W ops, longest remaining path first"""
+    cap = 32 * W
+    ops = dce(cx)
+    idx = {o: k for k, o in enumerate(ops)}
+    n = len(ops)
+    preds = [[] for _ in range(n)]
+    succs = [[] for _ in range(n)]
+    for k, o in enumerate(ops):
+        seen = set()
+        for v, _ in cx.ops[o][2] + cx.ops[o][3]:
+            p = cx.prod[v]
+            if p >= 0 and p not in seen:
+                seen.add(p)
+                preds[k].append(idx[p])
+                succs[idx[p]].append(k)
+    lat = [W_LAT[cx.ops[o][0]] for o in ops]
+    prio = [0.0] * n
+    for k in range(n - 1, -1, -1):  # ops are recorded in a topological order
+        prio[k] = lat[k] + max((prio[s] for s in succs[k]), default=0.0)
+    npred = [len(p) for p in preds]
+    ready_at = [0] * n
+    heap = [(-prio[k], k) for k in range(n) if npred[k] == 0]
+    heapq.heapify(heap)
+    steps = []
+    waiting = []  # (step, k): ready only from that step on
+    t = 0
+    done = 0
+    while done < n:
+        cur = []
+        deferred = []
+        while heap and len(cur) < cap:
+            pr, k = heapq.heappop(heap)
+            if ready_at[k] > t or (earliest and earliest.get(ops[k], 0) > t):
+                deferred.append((pr, k))
+                continue
+            cur.append(k)
+        for x in deferred:
+            heapq.heappush(heap, x)
+        if not cur:
+            t += 1
+            steps.append([])
+            continue
+        steps.append([ops[k] for k in cur])
+        done += len(cur)
+        for k in cur:
+            for s in succs[k]:
+                npred[s] -= 1
+                ready_at[s] = max(ready_at[s], t + 1)
+                if npred[s] == 0:
+                    heapq.heappush(heap, (-prio[s], s))
+        t += 1
+    return [s for s in steps if s]
+
+
+def schedule_loads(cx, W):
+    """LOADMUL inputs: schedule once, then hold each load back to a few steps before its
+    first consumer (otherwise the loads run first and all 384 inputs sit in LDS)"""
+    steps = schedule(cx, W)
+    if not cx.load_inputs:
+        return steps
+    step_of = {}
+    for t, s in enumerate(steps):
+        for o in s:
+            step_of[o] = t
+    first_use = {}
+    for t, s in enumerate(steps):
+        for o in s:
+            for v, _ in cx.ops[o][2] + cx.ops[o][3]:
+                p = cx.prod[v]
+                if p >= 0 and cx.ops[p][0] == "loadmul":
+                    first_use[p] = min(first_use.get(p, 1 << 30), t)
+    earliest = {p: max(0, u - 3) for p, u in first_use.items()}
+    return schedule(cx, W, earliest)
+
+
+def allocate(cx, steps):
+    """LDS slots: constants first (kept), then values by their lifetime in steps"""
+    n_val = len(cx.bound)
+    slot = [-1] * n_val
+    for k, (v, _) in enumerate(cx.const_list):
+        slot[v] = k
+    base = len(cx.const_list)
+    last = [-1] * n_val
+    for t, s in enumerate(steps):
+        for o in s:
+            for v, _ in cx.ops[o][2] + cx.ops[o][3]:
+                last[v] = max(last[v], t)
+    for v in cx.outputs:
+        last[v] = 1 << 30
+    free = []
+    nxt = base
+    expire = {}  # step -> slots freed after it
+    for v in cx.inputs:
+        if nxt >= MAX_SLOTS:
+            raise ValueError("slots")
+        slot[v] = nxt
+        nxt += 1
+        expire.setdefault(last[v], []).append(slot[v])
+    for t, s in enumerate(steps):
+        # slots last read before step t are free for writes in step t
+        for sl in expire.pop(t - 1, []):
+            heapq.heappush(free, sl)
+        for o in s:
+            d = cx.ops[o][1]
+            if free:
+                sl = heapq.heappop(free)
+            else:
+                sl = nxt
+                nxt += 1
+            slot[d] = sl
+            if last[d] < 0:
+                last[d] = t  # dead value (cannot happen after dce except outputs)
+            expire.setdefault(max(last[d], t), []).append(sl)
+    if nxt > MAX_SLOTS:
+        raise ValueError("%s: %d slots > %d" % (cx.name, nxt, MAX_SLOTS))
+    return slot, nxt
+
+
+# ----------------------------------------------------------------------------- check
+def run_program(cx, steps, slot, n_slots, raw_inputs):
+    """execute the scheduled, allocated program (values mod p, Montgomery semantics)"""
+    mem = [None] * n_slots
+    for v, raw in cx.const_list:
+        mem[slot[v]] = raw % P
+    for v, x in zip(cx.inputs, raw_inputs):
+        mem[slot[v]] = x % P
+
+    def form(terms):
+        s = 0
+        for v, c in terms:
+            x = mem[slot[v]]
+            assert x is not None, "read of an unwritten slot"
+            s += c * x
+        return s % P
+
+    for s in steps:
+        res = []
+        for o in s:
+            kind, d, A, B, j = cx.ops[o]
+            if kind == "lin":
+                r = (form(A) + form(B)) % P
+            elif kind == "mul":
+                r = form(A) * form(B) * RINV % P
+            else:
+                r = raw_inputs[j] * form(B) * RINV % P
+            res.append((slot[d], r))
+        for sl, r in res:  # writes after every read of the step
+            mem[sl] = r
+    return [mem[slot[v]] for v in cx.outputs]
+
+
+def reference(name, raw_inputs):
+    fn, n_in, _ = PROGRAMS[name]
+    E = IntEngine()
+    outs = fn(E, lambda n: [IntF(x) for x in raw_inputs])
+    return [o.v for o in outs]
+
+
+def rand_inputs(name, rng):
+    """inputs for which the program's algorithm is meaningful (points on the curve, nonzero
+    field elements); the check is an identity of the op list anyway"""
+    _, n_in, _ = PROGRAMS[name]
+    return [rng.randrange(1, P) for _ in range(n_in)]
+
+
+# ----------------------------------------------------------------------------- emit
+def limbs29(v):
+    return [(v >> (LBITS * i)) & ((1 << LBITS) - 1) for i in range(NLIMB)]
+
+
+def enc_term(sl, c):
+    assert 0 <= sl < MAX_SLOTS and COEF_MIN <= c <= COEF_MAX
+    return sl | ((c & 63) << SLOT_BITS)
+
+
+def encode(cx, steps, slot):
+    """8 words per op: w0 = dst | kind << 10 | nA << 12 | nB << 16 | input << 20; w1..w7 = 14
+    16-bit terms (slot | coef << 10), the A terms at positions 0..6, the B terms at 7..13"""
+    kinds = {"lin": 0, "mul": 1, "loadmul": 2}
+    words = []
+    desc = []
+    for s in steps:
+        assert len(s) < 256
+        desc.append(len(words) // 8 << 8 | len(s))
+        for o in s:
+            kind, d, A, B, j = cx.ops[o]
+            assert len(A) <= MAX_TERMS and len(B) <= MAX_TERMS
+            ta = [enc_term(slot[v], c) for v, c in A]
+            tb = [enc_term(slot[v], c) for v, c in B]
+            terms = ta + [0] * (7 - len(ta)) + tb + [0] * (7 - len(tb))
+            assert 0 <= j < 4096 or kind != "loadmul"
+            w0 = slot[d] | kinds[kind] << 10 | len(A) << 12 | len(B) << 16 | (max(j, 0) << 20)
+            words.append(w0)
+            for k in range(7):
+                words.append(terms[2 * k] | terms[2 * k + 1] << 16)
+    return words, desc
+
+
+def stats(cx, steps):
+    nm = sum(1 for s in steps for o in s if cx.ops[o][0] != "lin")
+    nl = sum(1 for s in steps for o in s if cx.ops[o][0] == "lin")
+    sm = sum(1 for s in steps if any(cx.ops[o][0] != "lin" for o in s))
+    cost = sum(max((W_LAT[cx.ops[o][0]] for o in s), default=0) + (0.25 if any(cx.ops[o][0] == "lin" for o in s) and
+               any(cx.ops[o][0] != "lin" for o in s) else 0) for s in steps)
+    return nm, nl, len(steps), sm, cost
+
+
+def build(name, W):
+    cx = trace(name)
+    steps = schedule_loads(cx, W)
+    slot, n_slots = allocate(cx, steps)
+    return cx, steps, slot, n_slots
+
+
+def emit(out_path, n_check=1, W=1, verbose=True):
+    rng = random.Random(20261017)
+    lines = ["// GENERATED by tools/gen_slp.py -- do not edit.",
+             "// Straight-line programs of the per-group serial stages (lsg_slp.hip).",
+             "#pragma once", "#include <stdint.h>",
+             "#ifndef LSG_SLP_ARRAY", "#define LSG_SLP_ARRAY static const", "#endif", ""]
+    for name in PROGRAMS:
+        cx, steps, slot, n_slots = build(name, W)
+        for _ in range(n_check):
+            x = rand_inputs(name, rng)
+            got = run_program(cx, steps, slot, n_slots, x)
+            want = reference(name, x)
+            want = [w * 1 % P for w in want]
+            if got != want:
+                raise SystemExit("gen_slp: program %s does not reproduce its algorithm" % name)
+        words, desc = encode(cx, steps, slot)
+        nm, nl, ns, sm, cost = stats(cx, steps)
+        if verbose:
+            print("[gen_slp] %-14s W=%d ops %6d (mul %6d lin %5d) steps %5d (with mul %5d) cost %.0f slots %d" %
+                  (name, W, nm + nl, nm, nl, ns, sm, cost, n_slots), flush=True)
+        cn = "lsg_slp_%s" % name
+        lines.append("// %s: %d ops (%d products), %d steps, %d LDS slots" % (name, nm + nl, nm, ns, n_slots))
+        lines.append("LSG_SLP_ARRAY uint32_t %s_ops[%d] __attribute__((aligned(32))) = {" % (cn, len(words)))
+        for i in range(0, len(words), 8):
+            lines.append("  " + ", ".join("0x%08xu" % w for w in words[i:i + 8]) + ",")
+        lines.append("};")
+        lines.append("LSG_SLP_ARRAY uint32_t %s_steps[%d] = {" % (cn, len(desc)))
+        for i in range(0, len(desc), 12):
+            lines.append("  " + ", ".join("0x%08xu" % w for w in desc[i:i + 12]) + ",")
+        lines.append("};")
+        consts = [c for _, c in cx.const_list]
+        lines.append("LSG_SLP_ARRAY uint32_t %s_consts[%d] = {" % (cn, 14 * len(consts)))
+        for c in consts:
+            lines.append("  " + ", ".join("0x%08xu" % w for w in limbs29(c)) + ",")
+        lines.append("};")
+        ins = [slot[v] for v in cx.inputs] or [0]
+        outs = [slot[v] for v in cx.outputs]
+        lines.append("LSG_SLP_ARRAY uint16_t %s_in[%d] = {%s};" % (cn, len(ins), ", ".join(map(str, ins))))
+        lines.append("LSG_SLP_ARRAY uint16_t %s_out[%d] = {%s};" % (cn, len(outs), ", ".join(map(str, outs))))
+        lines.append("#define %s_N_STEPS %d" % (cn.upper(), ns))
+        lines.append("#define %s_N_SLOTS %d" % (cn.upper(), n_slots))
+        lines.append("#define %s_N_CONSTS %d" % (cn.upper(), len(consts)))
+        lines.append("#define %s_N_IN %d" % (cn.upper(), len(cx.inputs)))
+        lines.append("#define %s_N_LOAD %d" % (cn.upper(), cx.n_inputs if cx.load_inputs else 0))
+        lines.append("#define %s_N_OUT %d" % (cn.upper(), len(outs)))
+        lines.append("")
+    tmp = out_path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, out_path)
+
+
+if __name__ == "__main__":
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "lodestar_amd", "csrc",
+                                                                  "lsg_slp_progs.h")
+    nc = int(sys.argv[sys.argv.index("--check") + 1]) if "--check" in sys.argv else 1
+    emit(out, nc)

@@ -16,8 +16,11 @@ run() {  # name seconds command...
   if [ $rc -ne 0 ]; then echo "== $name FAILED rc=$rc"; exit $rc; fi
 }
 for step in "$@"; do
-  # pair:<step> runs <step> with the pair-backend serial kernels (A/B against the row default)
-  if [ "${step#pair:}" != "$step" ]; then export LSG_SERIAL=pair TAG=${LSG_TAG:-r03}_pair; step=${step#pair:}; else unset LSG_SERIAL; TAG=${LSG_TAG:-r03}; fi
+  # row:<step> / pair:<step> run <step> with the row / pair serial kernels (A/B against the
+  # straight-line-program default)
+  if [ "${step#pair:}" != "$step" ]; then export LSG_SERIAL=pair TAG=${LSG_TAG:-r03}_pair; step=${step#pair:};
+  elif [ "${step#row:}" != "$step" ]; then export LSG_SERIAL=row TAG=${LSG_TAG:-r03}_row; step=${step#row:};
+  else unset LSG_SERIAL; TAG=${LSG_TAG:-r03}; fi
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ;;
     test-*) run "pytest_${step#test-}" 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "${step#test-}" ;;
