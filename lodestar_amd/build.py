@@ -17,7 +17,7 @@ SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip"
            "lsg_serial_pair.hip", "lsg_serial_pair_wide.hip", "lsg_slp.hip", "lsg_host.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
            "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp",
-           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h", "lsg_slp_progs.h", "lsg_slp_exec.hpp"]
+           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h", "lsg_slp_progs.h", "lsg_slp_exec.hpp", "lsg_inv.hpp"]
 OBJ = os.path.join(HERE, "_obj")
 
 

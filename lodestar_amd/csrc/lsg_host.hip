@@ -553,8 +553,17 @@ bool miller_fused() {
   return !(e && atoi(e) == 0);
 }
 
+// Packages of up to LSG_SLP_ITEMS sets (default 2048; 0: never) run one-set Miller items as
+// straight-line programs (lsg_slp.hip, one workgroup per set, ~0.8 ms) instead of the fused
+// kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
+size_t slp_items_max() {
+  const char* e = getenv("LSG_SLP_ITEMS");
+  const size_t v = e ? (size_t)atol(e) : (size_t)2048;
+  return lsg_serial_mode() == LSG_SERIAL_SLP ? v : 0;
+}
+
 int miller_k_for(size_t n_sets) {
-  if (miller_fused()) return 4;  // an item is four waves' lane pairs, whatever the package size
+  if (miller_fused()) return n_sets <= slp_items_max() ? 1 : 4;  // fused: four waves' lane pairs per item
   const char* e = getenv("LSG_MILLER_K");
   if (e) {
     const int v = atoi(e);
@@ -1007,6 +1016,14 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
 int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall, bool single = false) {
   const int ni = (int)n_items;
   const int32_t* items = PL(s, item_off);
+  if (ni > 0 && (single || s->K == 1) && miller_fused() && (size_t)ni <= std::max(slp_items_max(), (size_t)8192) &&
+      slp_items_max() > 0) {
+    // one-set items (small packages, per-job fallback phases): straight-line programs
+    KL(s, "k_slp_items1", lsg_slp_miller_items1(S_(s), ni, items, P_<uint32_t>(s->d_P), P_<uint8_t>(s->d_pinf),
+                                                P_<uint8_t>(s->d_hinf), P_<int32_t>(s->d_seterr), P_<uint32_t>(s->d_H),
+                                                fall));
+    return LSG_OK;
+  }
   if (single && ni > 0) {
     // every item is one pair (a fallback phase of single-set jobs): the fused kernel would run
     // four waves per item for one pair; the list form computes each set's lines once and

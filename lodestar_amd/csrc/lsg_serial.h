@@ -37,6 +37,11 @@ LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out5
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict);
 hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576);
 hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576);
+// Miller items of one set each (lane-form P, pinf, hinf, err, H as for k_miller_fused):
+// f[item] = ML(P_i, H_i) of set item_first[item], 1 for a set that does not take part
+hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,
+                                 const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, const uint32_t* H,
+                                 uint32_t* f);
 // Default: the straight-line programs.  env LSG_SERIAL=row selects the row kernels, =pair
 // the pair kernels (A/B).  The pair kernels were measured slower than the rows -- final
 // exponentiation 9.3 ms against 4.0 ms for one group, 51 against 26 ms for a fallback phase's

@@ -24,10 +24,13 @@ namespace {
 
 #define LSG_SLP_ARRAY __device__ const
 #include "lsg_slp_progs.h"
+#include "lsg_layout.h"
+// lane-form words per lane of one item (lsg_layout.h counts both lanes of the pair)
+constexpr size_t lsgl_w_g1a = lsgl::W_G1A / 2, lsgl_w_g2a = lsgl::W_G2A / 2, lsgl_w_f12 = lsgl::W_F12 / 2;
 
 namespace {
 
-enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2 };
+enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3 };
 
 template <int PROG>
 struct Prog;
@@ -49,6 +52,51 @@ struct Prog;
 LSG_SLP_PROG(SLP_FE, final_exp, FINAL_EXP)
 LSG_SLP_PROG(SLP_ML, miller_neg_g1, MILLER_NEG_G1)
 LSG_SLP_PROG(SLP_HORNER, horner_miller, HORNER_MILLER)
+LSG_SLP_PROG(SLP_ITEM1, miller_item1, MILLER_ITEM1)
+
+// the program's steps (inputs and constants already in their slots): in every step lane pair
+// q executes operation q; the next step's descriptor and this lane pair's entry of it are in
+// flight while the current step computes (the program lives in global memory / L2)
+template <class PR>
+__device__ __forceinline__ void slp_steps(uint32_t* lds, const uint8_t* inp, uint32_t q, uint32_t h) {
+  const uint32_t* ops = PR::ops();
+  const uint32_t* steps = PR::steps();
+  uint32_t d = steps[0];
+  uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
+  if (q < (d & 255u)) {
+    const uint4* e = (const uint4*)(ops + 8 * ((d >> 16) + q));
+    e0 = e[0];
+    e1 = e[1];
+  }
+#pragma unroll 1
+  for (int s = 0; s < PR::n_steps; s++) {
+    const uint32_t dn = steps[s + 1];  // (a zero sentinel follows the last step)
+    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
+    if (q < (dn & 255u)) {
+      const uint4* e = (const uint4*)(ops + 8 * ((dn >> 16) + q));
+      f0 = e[0];
+      f1 = e[1];
+    }
+    if (q < (d & 255u)) {
+      const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      slp_exec(lds, ew, inp, h, d);
+    }
+    __syncthreads();
+    d = dn;
+    e0 = f0;
+    e1 = f1;
+  }
+}
+template <class PR>
+__device__ __forceinline__ void slp_consts(uint32_t* lds, uint32_t q, uint32_t h, uint32_t nq) {
+  for (uint32_t j = q; j < (uint32_t)PR::n_consts; j += nq) {
+    const uint32_t* c = PR::consts() + 14 * j + 7 * h;
+    fp_t v;
+#pragma unroll
+    for (int k = 0; k < 7; k++) v.l[k] = c[k];
+    slot_store(lds, j, h, v);
+  }
+}
 
 // MODE: 0 = verdict (outputs == Fp12 one), 1 = Fp12 blob with the S = O test (outputs 12, 13
 // are S.Z: the group's term is 1 when S is the point at infinity)
@@ -62,28 +110,10 @@ __global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __re
   const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
   constexpr uint32_t NQ = 32 * W;
   const uint8_t* inp = in + (size_t)in_stride * item;
-  for (uint32_t j = q; j < (uint32_t)PR::n_consts; j += NQ) {
-    const uint32_t* c = PR::consts() + 14 * j + 7 * h;
-    fp_t v;
-#pragma unroll
-    for (int k = 0; k < 7; k++) v.l[k] = c[k];
-    slot_store(lds, j, h, v);
-  }
+  slp_consts<PR>(lds, q, h, NQ);
   for (uint32_t j = q; j < (uint32_t)PR::n_in; j += NQ) slot_store(lds, PR::in()[j], h, fp_from_be_bytes(inp + 48 * j, 12));
   __syncthreads();
-  const uint32_t* ops = PR::ops();
-  const uint32_t* steps = PR::steps();
-#pragma unroll 1
-  for (int s = 0; s < PR::n_steps; s++) {
-    const uint32_t d = steps[s];
-    if (q < (d & 255u)) {
-      const uint4* e = (const uint4*)(ops + 8 * ((d >> 8) + q));
-      const uint4 e0 = e[0], e1 = e[1];
-      const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-      slp_exec(lds, ew, inp, h);
-    }
-    __syncthreads();
-  }
+  slp_steps<PR>(lds, inp, q, h);
   // outputs: canonical values; lane pair j holds output j (n_out <= 32 W)
   static_assert(PR::n_out <= 32, "one output per lane pair");
   __shared__ uint32_t s_flag;
@@ -130,10 +160,52 @@ __global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __re
   }
 }
 
+// Miller items of one set each (SURVEY 8a M5 for small packages and per-job fallback items):
+// the pair (P_i, H(m_i)) of set item_first[item] -> that item's Miller value in lane form in
+// f (the layout k_miller_fused writes).  A set with an error or an infinite point takes part
+// as (0, 0) with use flag 0: its lines are the identity and it contributes 1.
+__global__ void __launch_bounds__(64) k_slp_items1(int n_items, const int32_t* __restrict__ item_first,
+                                                   const uint32_t* __restrict__ P, const uint8_t* __restrict__ pinf,
+                                                   const uint8_t* __restrict__ hinf, const int32_t* __restrict__ err,
+                                                   const uint32_t* __restrict__ H, uint32_t* __restrict__ f) {
+  using PR = Prog<SLP_ITEM1>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int item = blockIdx.x;
+  if (item >= n_items) return;
+  const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
+  slp_consts<PR>(lds, q, h, 32);
+  static_assert(PR::n_in == 7, "P.x, P.y, H.x.c0, H.x.c1, H.y.c0, H.y.c1, use");
+  if (q < 7) {
+    const size_t s = (size_t)item_first[item];
+    const bool use = err[s] == 0 && !pinf[s] && !hinf[s];
+    fp_t v = fp_zero();
+    const uint32_t* src = nullptr;
+    if (q < 2) {
+      if (use) src = P + (s * lsgl_w_g1a + 7 * q) * 2 + h;
+    } else if (q < 6) {
+      src = H + (s * lsgl_w_g2a + 7 * (q - 2)) * 2 + h;
+    } else if (use) {
+      v = fp_t(FP_ONE);
+    }
+    if (src)
+#pragma unroll
+      for (int w = 0; w < 7; w++) v.l[w] = src[2 * w];
+    slot_store(lds, PR::in()[q], h, v);
+  }
+  __syncthreads();
+  slp_steps<PR>(lds, nullptr, q, h);
+  if (q < 12) {  // Montgomery outputs (< 2p) straight into the lane form
+    const fp_t v = slot_load(lds, PR::out()[q], h);
+    uint32_t* dst = f + ((size_t)item * lsgl_w_f12 + 7 * q) * 2 + h;
+#pragma unroll
+    for (int w = 0; w < 7; w++) dst[2 * w] = v.l[w];
+  }
+}
+
 template <int PROG, int W, int MODE>
 hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, uint8_t* out, int32_t* verdict) {
   if (n <= 0) return hipSuccess;
-  const size_t shm = (size_t)Prog<PROG>::n_slots * 64;
+  const size_t shm = (size_t)Prog<PROG>::n_slots * LSG_SLP_STRIDE * 4;
   hipLaunchKernelGGL((k_slp<PROG, W, MODE>), dim3(n), dim3(64 * W), shm, st, n, in, in_stride, out, verdict);
   return hipGetLastError();
 }
@@ -148,4 +220,12 @@ hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, ui
 }
 hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
   return launch<SLP_HORNER, 1, 1>(st, ng, C288, 288 * 64, out576, nullptr);
+}
+hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,
+                                 const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, const uint32_t* H,
+                                 uint32_t* f) {
+  if (n_items <= 0) return hipSuccess;
+  const size_t shm = (size_t)Prog<SLP_ITEM1>::n_slots * LSG_SLP_STRIDE * 4;
+  hipLaunchKernelGGL(k_slp_items1, dim3(n_items), dim3(64), shm, st, n_items, item_first, P, pinf, hinf, err, H, f);
+  return hipGetLastError();
 }

@@ -4,14 +4,20 @@
 // limbs in one "lane"), so the exact device arithmetic -- gathers, carry round, lazy bounds,
 // LDS layout -- is checked against the oracle without a GPU.  Include after lsg_fp_pair.hpp.
 #pragma once
+#include "lsg_inv.hpp"
 
-// LDS slot s: 16 words; lane h of a pair holds its LSG_PL limbs at words s*16 + h*8 ..
+// LDS slot s: LSG_SLP_STRIDE words; lane h of a pair holds its LSG_PL limbs at words
+// s*STRIDE + h*8 ..  (a stride that is not a multiple of the bank count spreads the lane
+// pairs of a step, which read unrelated slots, over the LDS banks)
+#ifndef LSG_SLP_STRIDE
+#define LSG_SLP_STRIDE 16
+#endif
 LSG_PFN fp_t slot_load(const uint32_t* lds, uint32_t s, uint32_t h) {
-  const uint32_t* p = lds + s * 16 + h * 8;
   fp_t r;
 #if LSG_PAIR_G == 2
-  const uint4 a = *(const uint4*)p;
-  const uint3 b = *(const uint3*)(p + 4);
+  // two aligned 16-byte reads (word 7 is padding)
+  const uint4* p = reinterpret_cast<const uint4*>(lds) + s * (LSG_SLP_STRIDE / 4) + h * 2;
+  const uint4 a = p[0], b = p[1];
   r.l[0] = a.x;
   r.l[1] = a.y;
   r.l[2] = a.z;
@@ -20,31 +26,48 @@ LSG_PFN fp_t slot_load(const uint32_t* lds, uint32_t s, uint32_t h) {
   r.l[5] = b.y;
   r.l[6] = b.z;
 #else
+  const uint32_t* p = lds + s * LSG_SLP_STRIDE + h * 8;
   for (int k = 0; k < LSG_PL; k++) r.l[k] = p[k];
 #endif
   return r;
 }
 LSG_PFN void slot_store(uint32_t* lds, uint32_t s, uint32_t h, const fp_t& v) {
-  uint32_t* p = lds + s * 16 + h * 8;
 #if LSG_PAIR_G == 2
-  *(uint4*)p = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
-  *(uint3*)(p + 4) = make_uint3(v.l[4], v.l[5], v.l[6]);
+  uint4* p = reinterpret_cast<uint4*>(lds) + s * (LSG_SLP_STRIDE / 4) + h * 2;
+  p[0] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+  p[1] = make_uint4(v.l[4], v.l[5], v.l[6], 0u);
 #else
+  uint32_t* p = lds + s * LSG_SLP_STRIDE + h * 8;
   for (int k = 0; k < LSG_PL; k++) p[k] = v.l[k];
 #endif
 }
 
-// acc += coef * slot for the terms [0, n) of a 7-term half (t: slot | coef << 10, 16 bits)
+// acc += coef * slot over the first N terms of a 7-term half (t: slot | coef << 10, 16
+// bits): straight-line code, every load issued before the first multiply-add
+template <int N>
+LSG_PFN void slp_gather_n(int64_t* acc, const uint32_t* lds, const uint32_t* t, uint32_t h) {
+  fp_t v[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = slot_load(lds, t[k] & 1023u, h);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const int32_t c = (int32_t)(t[k] << 16) >> 26;  // bits 10..15, signed
+#pragma unroll
+    for (int j = 0; j < LSG_PL; j++) acc[j] += (int64_t)c * (int64_t)(int32_t)v[k].l[j];
+  }
+}
+// n: the step's maximum term count (uniform, from the step descriptor); lanes with fewer
+// terms hold zero terms (slot 0, coefficient 0), so nothing diverges
 LSG_PFN void slp_gather(int64_t* acc, const uint32_t* lds, const uint32_t* t, uint32_t n, uint32_t h) {
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    if ((uint32_t)k < n) {
-      const uint32_t w = t[k];
-      const fp_t v = slot_load(lds, w & 1023u, h);
-      const int32_t c = (int32_t)(w << 16) >> 26;  // bits 10..15, signed
-#pragma unroll
-      for (int j = 0; j < LSG_PL; j++) acc[j] += (int64_t)c * (int64_t)(int32_t)v.l[j];
-    }
+  switch (n) {
+    case 1: slp_gather_n<1>(acc, lds, t, h); break;
+    case 2: slp_gather_n<2>(acc, lds, t, h); break;
+    case 3: slp_gather_n<3>(acc, lds, t, h); break;
+    case 4: slp_gather_n<4>(acc, lds, t, h); break;
+    case 5: slp_gather_n<5>(acc, lds, t, h); break;
+    case 6: slp_gather_n<6>(acc, lds, t, h); break;
+    case 7: slp_gather_n<7>(acc, lds, t, h); break;
+    default: break;
   }
 }
 
@@ -64,11 +87,13 @@ LSG_PFN fp_t slp_carry(const int64_t* acc) {
   return o;
 }
 
-// operation entry e (8 words): w0 = dst | kind << 10 | nA << 12 | nB << 16 | input << 20,
-// then 14 16-bit terms (A at 0..6, B at 7..13).  inp: the item's input blob (LOADMUL).
-LSG_PFN void slp_exec(uint32_t* lds, const uint32_t* e, const uint8_t* inp, uint32_t h) {
+// operation entry e (8 words): w0 = dst | kind << 10 (0 LIN, 1 MUL, 2 LOADMUL, 3 INV) | nA << 12 | nB << 16 | input << 20,
+// then 14 16-bit terms (A at 0..6, B at 7..13).  d: the step descriptor (uniform: the term
+// counts to gather, whether any LIN / any product is in the step).  inp: the item's input
+// blob (LOADMUL).
+LSG_PFN void slp_exec(uint32_t* lds, const uint32_t* e, const uint8_t* inp, uint32_t h, uint32_t d) {
   const uint32_t w0 = e[0];
-  const uint32_t kind = (w0 >> 10) & 3u, nA = (w0 >> 12) & 15u, nB = (w0 >> 16) & 15u;
+  const uint32_t kind = (w0 >> 10) & 3u, na = (d >> 8) & 7u, nb = (d >> 11) & 7u;
   uint32_t ta[7], tb[7];
 #pragma unroll
   for (int k = 0; k < 7; k++) {
@@ -79,15 +104,18 @@ LSG_PFN void slp_exec(uint32_t* lds, const uint32_t* e, const uint8_t* inp, uint
   int64_t acc[LSG_PL], bcc[LSG_PL];
 #pragma unroll
   for (int j = 0; j < LSG_PL; j++) acc[j] = bcc[j] = 0;
-  slp_gather(acc, lds, ta, nA, h);
-  slp_gather(bcc, lds, tb, nB, h);
+  slp_gather(acc, lds, ta, na, h);
+  slp_gather(bcc, lds, tb, nb, h);
   fp_t r;
-  if (kind == 0u) {
+  if ((d >> 14) & 1u) {  // the step has LIN ops (a product lane overwrites r below)
+    int64_t s[LSG_PL];
 #pragma unroll
-    for (int j = 0; j < LSG_PL; j++) acc[j] += bcc[j];
-    r = slp_carry(acc);
-  } else {
+    for (int j = 0; j < LSG_PL; j++) s[j] = acc[j] + bcc[j];
+    r = slp_carry(s);
+  }
+  if (((d >> 15) & 1u) && kind != 0u) {
     fp_t a = kind == 2u ? fp_from_be_bytes(inp + 48 * (w0 >> 20), 12) : slp_carry(acc);
+    if (kind == 3u) a = pair_inv_gcd(pair_canon_small(a));  // INV: the GCD inverse, then * R^3
     const fp_t b = slp_carry(bcc);
     pair_mont_mul_n<1>(&r, &a, &b);
   }

@@ -356,11 +356,14 @@ struct HcProg {
          lsg_slp_##NAME##_out, LSG_SLP_##UP##_N_STEPS, LSG_SLP_##UP##_N_SLOTS, LSG_SLP_##UP##_N_CONSTS,      \
          LSG_SLP_##UP##_N_IN, LSG_SLP_##UP##_N_OUT}
 extern "C" {
-// prog: 0 final_exp, 1 miller_neg_g1, 2 horner_miller; in: the item's input blob; out: the
-// canonical outputs (48 bytes each).  Returns the output count.
+// prog: 0 final_exp, 1 miller_neg_g1, 2 horner_miller, 3 miller_item1 (whose lane-form
+// Montgomery inputs/outputs are converted here); in: the item's inputs as canonical 48-byte
+// values; out: the canonical outputs (48 bytes each).  Returns the output count.
 int hc_slp_run(int prog, const uint8_t* in, uint8_t* out) {
-  const HcProg P[3] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
-                       HC_PROG(horner_miller, HORNER_MILLER)};
+  const HcProg P[4] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
+                       HC_PROG(horner_miller, HORNER_MILLER), HC_PROG(miller_item1, MILLER_ITEM1)};
+  const bool mont = prog == 3;  // Montgomery-form inputs and outputs (lane-form programs)
+  const fp_t r2 = fp_t(FP_R2), one = fp_t(FP_ONE_CANON);
   const HcProg& p = P[prog];
   std::vector<uint32_t> lds((size_t)p.n_slots * 16, 0xdeadbeefu);
   for (int j = 0; j < p.n_consts; j++) {
@@ -368,13 +371,44 @@ int hc_slp_run(int prog, const uint8_t* in, uint8_t* out) {
     for (int k = 0; k < 14; k++) v.l[k] = p.consts[14 * j + k];
     slot_store(lds.data(), j, 0, v);
   }
-  for (int j = 0; j < p.n_in; j++) slot_store(lds.data(), p.in[j], 0, fp_from_be_bytes(in + 48 * j, 12));
+  for (int j = 0; j < p.n_in; j++) {
+    fp_t x = fp_from_be_bytes(in + 48 * j, 12);
+    if (mont) {
+      fp_t m;
+      pair_mont_mul_n<1>(&m, &x, &r2);
+      x = m;
+    }
+    slot_store(lds.data(), p.in[j], 0, x);
+  }
   for (int s = 0; s < p.n_steps; s++) {
     const uint32_t d = p.steps[s];
-    for (uint32_t q = 0; q < (d & 255u); q++) slp_exec(lds.data(), p.ops + 8 * ((d >> 8) + q), in, 0);
+    for (uint32_t q = 0; q < (d & 255u); q++) slp_exec(lds.data(), p.ops + 8 * ((d >> 16) + q), in, 0, d);
   }
-  for (int j = 0; j < p.n_out; j++) fp_to_be48(out + 48 * j, slp_output(lds.data(), p.out[j], 0));
+  for (int j = 0; j < p.n_out; j++) {
+    if (mont) {
+      fp_t c, v = slot_load(lds.data(), p.out[j], 0);
+      pair_mont_mul_n<1>(&c, &v, &one);
+      fp_to_be48(out + 48 * j, pair_canon_small(c));
+    } else {
+      fp_to_be48(out + 48 * j, slp_output(lds.data(), p.out[j], 0));
+    }
+  }
   return p.n_out;
+}
+}
+#endif
+
+#ifdef LSG_HOSTCHECK_PAIR
+#include "lsg_inv.hpp"
+extern "C" {
+// x^-1 mod p by the divstep GCD of the INV operation (lsg_inv.hpp), canonical in and out
+void hc_inv_gcd(const uint8_t* a48, uint8_t* out48) {
+  const fp_t d = pair_inv_gcd(fp_from_be_bytes(a48, 12));
+  fp_t m, c;
+  const fp_t r2 = fp_t(FP_R2), one = fp_t(FP_ONE_CANON);
+  pair_mont_mul_n<1>(&m, &d, &r2);  // d R mod p
+  pair_mont_mul_n<1>(&c, &m, &one);  // d mod p, in (-p, 2p)
+  fp_to_be48(out48, pair_canon_small(c));
 }
 }
 #endif

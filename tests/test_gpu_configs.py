@@ -299,17 +299,25 @@ def test_rccl_exchange_single_device(keys, monkeypatch):
         c.close()
 
 
-# ---- the fused Miller kernel (lines in LDS, four waves per item) against the split kernels
+# ---- the fused Miller kernel (lines in LDS, four waves per item) and the one-set straight-line
+# program items against the split kernels
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 37, 300])
 def test_fused_miller_matches_split(ctx, keys, n, monkeypatch):
     sets = single_sets(ctx, keys, b"fused", n)
     monkeypatch.setenv("LSG_MILLER_FUSED", "0")
     split, _, _ = ctx.batch_partial(sets, seed=11)
     monkeypatch.setenv("LSG_MILLER_FUSED", "1")
+    monkeypatch.setenv("LSG_SLP_ITEMS", "0")
     fused, _, _ = ctx.batch_partial(sets, seed=11)
     names = [k for k, _ in ctx.last_kernel_times()]
     assert "k_miller_fused" in names and "k_miller_lines" not in names
     assert fused == split
+    # one-set Miller items as straight-line programs (the small-package default)
+    monkeypatch.setenv("LSG_SLP_ITEMS", "4096")
+    slp, _, _ = ctx.batch_partial(sets, seed=11)
+    names = [k for k, _ in ctx.last_kernel_times()]
+    assert "k_slp_items1" in names and "k_miller_fused" not in names
+    assert slp == split
     assert ctx.verify_sets(sets) == (1, 0)
 
 

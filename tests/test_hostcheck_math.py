@@ -341,3 +341,23 @@ def test_slp_programs_match_oracle(hc):
         S = E2.add(E2.add(S, S), Cs[k])
     assert hc.hc_slp_run(2, blob, o) == 14
     assert ub12(o.raw[:576]) == miller_loop_fast(neg_g1, S)
+    # one-set Miller item (Montgomery lane-form in/out): a pair that takes part, and one that
+    # does not (P = (0, 0), use 0) contributing exactly 1
+    pk, Q = E1.mul(G1_GEN, 99), E2.mul(G2_GEN, 1234)
+    (qx, qy) = Q
+    assert hc.hc_slp_run(3, be(pk[0]) + be(pk[1]) + b2(qx) + b2(qy) + be(1), o) == 12
+    assert ub12(o.raw[:576]) == miller_loop_fast(pk, Q)
+    assert hc.hc_slp_run(3, be(0) + be(0) + b2(qx) + b2(qy) + be(0), o) == 12
+    assert ub12(o.raw[:576]) == F12_ONE
+
+
+def test_inv_gcd_matches_pow(hc):
+    """lsg_inv.hpp (divstep GCD inversion of the programs' INV operation) against pow(x, -1, p),
+    including 0 (-> 0), 1, p - 1 and values near 2^k"""
+    if hc.backend != "pair":
+        pytest.skip("pair backend only")
+    vals = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, 1 << 380, (1 << 200) + 1] + [rng.randrange(P) for _ in range(300)]
+    o = buf(48)
+    for x in vals:
+        hc.hc_inv_gcd(be(x), o)
+        assert int.from_bytes(o.raw, "big") == (pow(x, -1, P) if x else 0), x

@@ -54,7 +54,7 @@ MAX_TERMS = 7  # terms per operand form (A and B each)
 COEF_MIN, COEF_MAX = -32, 31
 SLOT_BITS = 10
 MAX_SLOTS = 1 << SLOT_BITS
-W_LAT = {"mul": 1.0, "loadmul": 1.0, "lin": 0.25}  # step costs relative to one product
+W_LAT = {"mul": 1.0, "loadmul": 1.0, "lin": 0.25, "inv": 20.0}  # step costs relative to one product
 COMBINE_TERMS = int(os.environ.get("LSG_SLP_COMBINE", "12"))  # a form built by +/- keeps up to this many terms
 COMBINE_KEEP = int(os.environ.get("LSG_SLP_KEEP", "7"))  # ... and is cut back to this many
 
@@ -87,6 +87,9 @@ class IntF:
 class IntEngine:
     def const(self, v):
         return IntF(v)
+
+    def inv(self, a):
+        return IntF(pow(a.v, -1, P) if a.v else 0)
 
     def zero(self):
         return IntF(0)
@@ -175,6 +178,10 @@ class Ctx:
 
     def input(self, j):
         """input Fp #j of the item in Montgomery form"""
+        if self.load_inputs == "mont":  # already Montgomery (lane-form values, < 2p)
+            raw = self._new(2, -1)
+            self.inputs.append(raw)
+            return Sym(self, {raw: 1})
         if self.load_inputs:
             v = self._new(2, len(self.ops), 1.0)
             self.ops.append(["loadmul", v, [], [(self._raw_const(R * R % P), 1)], j])
@@ -278,11 +285,24 @@ class Ctx:
         A = self.fit(a.t, MAX_TERMS, min(LIN_MAX, MUL_BB // max(1, self._fbound(B))))
         return self._mul_forms(A, B)
 
+    def inv(self, s):
+        """s^-1: the INV operation inverts a value in (-p, 2p) (a product output) and
+        multiplies the integer inverse by R^3 (Montgomery form of the inverse)"""
+        t = self.mul(s, Sym(self, {self.one: 1}))
+        (tv,) = t.t
+        A = [(tv, 1)]
+        B = [(self._raw_const(R * R * R % P), 1)]
+        d = self._new(2, len(self.ops), self.est[tv] + W_LAT["inv"])
+        self.ops.append(["inv", d, A, B, -1])
+        return Sym(self, {d: 1})
+
     def output(self, s):
         """an output Fp: converted out of Montgomery form (in (-p, 2p), canonicalised by the
         kernel)"""
         A = self.fit(s.t, MAX_TERMS, LIN_MAX) if s.t else [(self._raw_const(0), 1)]
-        B = [(self._raw_const(1), 1)]
+        # Montgomery-form outputs (lane-form consumers) are tamed below 2p; the others leave
+        # Montgomery form for the canonical blobs
+        B = [(self.one if self.load_inputs == "mont" else self._raw_const(1), 1)]
         d = self._new(2, len(self.ops))
         self.ops.append(["mul", d, A, B, -1])
         self.outputs.append(d)
@@ -371,7 +391,8 @@ def fp_pow(E, a, e):
 
 
 def fp_inv(E, a):
-    return fp_pow(E, a, P - 2)
+    """a^-1 (0 -> 0): one INV operation (divstep GCD, lsg_inv.hpp) in a program"""
+    return E.inv(a)
 
 
 def f2_inv(E, a):
@@ -703,11 +724,49 @@ def prog_horner_miller(E, inp):
     return flat12(ml_neg_g1(E, S)) + list(S[2])
 
 
+def miller_loop_masked(E, Pxy, Q, u):
+    """f_{|x|,Q}(P) conjugated for one pair of a Miller item (lsg_pairing.hpp:173), with the
+    pair's use flag u (Montgomery 1 or 0) folded into every line: a pair that does not take
+    part (P = (0, 0), u = 0) contributes the line (1, 0, 0) at every step, i.e. exactly 1 --
+    the same identity lines k_miller_fused uses for such pairs"""
+    xP, yP = Pxy
+    one = E.const(1)
+
+    def ev(L):
+        l00 = (u * (L[0][0] - one) + one, u * L[0][1])
+        return (l00, f2_mul_fp(L[1], xP), f2_mul_fp(L[2], yP))
+
+    T = (Q[0], Q[1], f2_one(E))
+    T, L = ml_dbl_step(T)
+    L = ev(L)
+    z = f2_zero(E)
+    f = ((L[0], L[1], z), (z, L[2], z))
+    T, L = ml_add_step(T, Q)
+    f = f12_mul_line(f, *ev(L))
+    for b in range(61, -1, -1):
+        f = f12_sqr(f)
+        T, L = ml_dbl_step(T)
+        f = f12_mul_line(f, *ev(L))
+        if (X_ABS >> b) & 1:
+            T, L = ml_add_step(T, Q)
+            f = f12_mul_line(f, *ev(L))
+    return f12_conj(f)
+
+
+def prog_miller_item1(E, inp):
+    """in (Montgomery lane-form values): P (x, y; 0 when the pair is unused), Q = H(m)
+    (x.c0, x.c1, y.c0, y.c1), u (1 or 0); out: the item's Miller value (12 Fp, Montgomery)"""
+    v = inp(7)
+    return flat12(miller_loop_masked(E, (v[0], v[1]), ((v[2], v[3]), (v[4], v[5])), v[6]))
+
+
 PROGRAMS = {
-    # name: (builder, n_inputs, inputs loaded by LOADMUL ops inside the program)
+    # name: (builder, n_inputs, inputs: False = canonical blob bytes, True = loaded by LOADMUL
+    #        ops inside the program, "mont" = Montgomery lane-form values, outputs likewise)
     "final_exp": (prog_final_exp, 12, False),
     "miller_neg_g1": (prog_miller_neg_g1, 6, False),
     "horner_miller": (prog_horner_miller, 384, True),
+    "miller_item1": (prog_miller_item1, 7, "mont"),
 }
 
 
@@ -886,6 +945,9 @@ def run_program(cx, steps, slot, n_slots, raw_inputs):
                 r = (form(A) + form(B)) % P
             elif kind == "mul":
                 r = form(A) * form(B) * RINV % P
+            elif kind == "inv":
+                x = form(A)
+                r = (pow(x, -1, P) if x else 0) * form(B) * RINV % P
             else:
                 r = raw_inputs[j] * form(B) * RINV % P
             res.append((slot[d], r))
@@ -920,13 +982,19 @@ def enc_term(sl, c):
 
 def encode(cx, steps, slot):
     """8 words per op: w0 = dst | kind << 10 | nA << 12 | nB << 16 | input << 20; w1..w7 = 14
-    16-bit terms (slot | coef << 10), the A terms at positions 0..6, the B terms at 7..13"""
-    kinds = {"lin": 0, "mul": 1, "loadmul": 2}
+    16-bit terms (slot | coef << 10), the A terms at positions 0..6, the B terms at 7..13
+    (unused terms are 0: slot 0 with coefficient 0).  Step descriptor: ops | max nA << 8 |
+    max nB << 11 | has LIN << 14 | has MUL/LOADMUL << 15 | first op << 16."""
+    kinds = {"lin": 0, "mul": 1, "loadmul": 2, "inv": 3}
     words = []
     desc = []
     for s in steps:
-        assert len(s) < 256
-        desc.append(len(words) // 8 << 8 | len(s))
+        assert len(s) < 256 and len(words) // 8 < 1 << 16
+        na = max(len(cx.ops[o][2]) for o in s)
+        nb = max(len(cx.ops[o][3]) for o in s)
+        has_lin = any(cx.ops[o][0] == "lin" for o in s)
+        has_mul = any(cx.ops[o][0] != "lin" for o in s)
+        desc.append(len(s) | na << 8 | nb << 11 | has_lin << 14 | has_mul << 15 | (len(words) // 8) << 16)
         for o in s:
             kind, d, A, B, j = cx.ops[o]
             assert len(A) <= MAX_TERMS and len(B) <= MAX_TERMS
@@ -938,6 +1006,7 @@ def encode(cx, steps, slot):
             words.append(w0)
             for k in range(7):
                 words.append(terms[2 * k] | terms[2 * k + 1] << 16)
+    desc.append(0)  # sentinel: the interpreter prefetches one step ahead
     return words, desc
 
 
@@ -968,8 +1037,11 @@ def emit(out_path, n_check=1, W=1, verbose=True):
         for _ in range(n_check):
             x = rand_inputs(name, rng)
             got = run_program(cx, steps, slot, n_slots, x)
-            want = reference(name, x)
-            want = [w * 1 % P for w in want]
+            if cx.load_inputs == "mont":  # Montgomery in and out
+                want = reference(name, [v * RINV % P for v in x])
+                got = [v * RINV % P for v in got]
+            else:
+                want = reference(name, x)
             if got != want:
                 raise SystemExit("gen_slp: program %s does not reproduce its algorithm" % name)
         words, desc = encode(cx, steps, slot)
