@@ -553,15 +553,7 @@ bool miller_fused() {
   return !(e && atoi(e) == 0);
 }
 
-// Packages of up to LSG_SLP_ITEMS sets (default 2048; 0: never) run one-set Miller items as
-// straight-line programs (lsg_slp.hip, one workgroup per set, ~0.8 ms) instead of the fused
-// kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
-size_t slp_items_max() {
-  const char* e = getenv("LSG_SLP_ITEMS");
-  const size_t v = e ? (size_t)atol(e) : (size_t)2048;
-  return lsg_serial_mode() == LSG_SERIAL_SLP ? v : 0;
-}
-
+size_t slp_items_max();
 int miller_k_for(size_t n_sets) {
   if (miller_fused()) return n_sets <= slp_items_max() ? 1 : 4;  // fused: four waves' lane pairs per item
   const char* e = getenv("LSG_MILLER_K");
@@ -770,11 +762,24 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
   return LSG_OK;
 }
 
+// Packages of up to LSG_SLP_ITEMS sets (default 2048; 0: never) run one-set Miller items as
+// straight-line programs (lsg_slp.hip, one workgroup per set, ~0.8 ms) instead of the fused
+// kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
+size_t slp_items_max() {
+  const char* e = getenv("LSG_SLP_ITEMS");
+  const size_t v = e ? (size_t)atol(e) : (size_t)2048;
+  return lsg_serial_mode() == LSG_SERIAL_SLP ? v : 0;
+}
+
 // hash_to_G2 of the slot's n expanded messages (d_ub) into d_H / d_hinf on the current stream
 int launch_hash(Slot* s, int n) {
   KL(s, "k_h2c_prep", lsgk::h2c_prep(S_(s), n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrm)));
   LSG_RC(batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)));
   KL(s, "k_h2c_map", lsgk::h2c_map(S_(s), n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp)));
+  if ((size_t)n <= slp_items_max()) {  // small packages: clearing + affine as one program per set
+    KL(s, "k_slp_h2c", lsg_slp_h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
+    return LSG_OK;
+  }
   KL(s, "k_h2c_clear",
      lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf)));
   LSG_RC(batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)));

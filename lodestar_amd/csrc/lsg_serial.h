@@ -37,6 +37,9 @@ LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out5
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict);
 hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576);
 hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576);
+// hash_to_G2's cofactor clearing and affine conversion: Hp (projective lane form, the SSWU
+// map's Q0 + Q1) -> H (affine lane form), hinf
+hipError_t lsg_slp_h2c_clear(hipStream_t st, int n, const uint32_t* Hp, uint32_t* H, uint8_t* hinf);
 // Miller items of one set each (lane-form P, pinf, hinf, err, H as for k_miller_fused):
 // f[item] = ML(P_i, H_i) of set item_first[item], 1 for a set that does not take part
 hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,

@@ -26,33 +26,36 @@ namespace {
 #include "lsg_slp_progs.h"
 #include "lsg_layout.h"
 // lane-form words per lane of one item (lsg_layout.h counts both lanes of the pair)
-constexpr size_t lsgl_w_g1a = lsgl::W_G1A / 2, lsgl_w_g2a = lsgl::W_G2A / 2, lsgl_w_f12 = lsgl::W_F12 / 2;
+constexpr size_t lsgl_w_g1a = lsgl::W_G1A / 2, lsgl_w_g2a = lsgl::W_G2A / 2, lsgl_w_g2p = lsgl::W_G2P / 2,
+                 lsgl_w_f12 = lsgl::W_F12 / 2;
 
 namespace {
 
-enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3 };
+enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3, SLP_H2C_CLEAR = 4 };
 
-template <int PROG>
+template <int PROG, int W>
 struct Prog;
-#define LSG_SLP_PROG(ID, NAME, UP)                                         \
-  template <>                                                              \
-  struct Prog<ID> {                                                        \
-    static constexpr int n_steps = LSG_SLP_##UP##_N_STEPS;                 \
-    static constexpr int n_slots = LSG_SLP_##UP##_N_SLOTS;                 \
-    static constexpr int n_consts = LSG_SLP_##UP##_N_CONSTS;               \
-    static constexpr int n_in = LSG_SLP_##UP##_N_IN;                       \
-    static constexpr int n_load = LSG_SLP_##UP##_N_LOAD;                   \
-    static constexpr int n_out = LSG_SLP_##UP##_N_OUT;                     \
-    static __device__ const uint32_t* ops() { return lsg_slp_##NAME##_ops; }     \
-    static __device__ const uint32_t* steps() { return lsg_slp_##NAME##_steps; } \
-    static __device__ const uint32_t* consts() { return lsg_slp_##NAME##_consts; } \
-    static __device__ const uint16_t* in() { return lsg_slp_##NAME##_in; }       \
-    static __device__ const uint16_t* out() { return lsg_slp_##NAME##_out; }     \
+#define LSG_SLP_PROG_W(ID, W, NAME, UP)                                                \
+  template <>                                                                          \
+  struct Prog<ID, W> {                                                                 \
+    static constexpr int n_steps = LSG_SLP_##UP##_W##W##_N_STEPS;                      \
+    static constexpr int n_slots = LSG_SLP_##UP##_W##W##_N_SLOTS;                      \
+    static constexpr int n_consts = LSG_SLP_##UP##_W##W##_N_CONSTS;                    \
+    static constexpr int n_in = LSG_SLP_##UP##_W##W##_N_IN;                            \
+    static constexpr int n_load = LSG_SLP_##UP##_W##W##_N_LOAD;                        \
+    static constexpr int n_out = LSG_SLP_##UP##_W##W##_N_OUT;                          \
+    static __device__ const uint32_t* ops() { return lsg_slp_##NAME##_w##W##_ops; }     \
+    static __device__ const uint32_t* steps() { return lsg_slp_##NAME##_w##W##_steps; } \
+    static __device__ const uint32_t* consts() { return lsg_slp_##NAME##_w##W##_consts; } \
+    static __device__ const uint16_t* in() { return lsg_slp_##NAME##_w##W##_in; }       \
+    static __device__ const uint16_t* out() { return lsg_slp_##NAME##_w##W##_out; }     \
   };
+#define LSG_SLP_PROG(ID, NAME, UP) LSG_SLP_PROG_W(ID, 1, NAME, UP) LSG_SLP_PROG_W(ID, 2, NAME, UP)
 LSG_SLP_PROG(SLP_FE, final_exp, FINAL_EXP)
 LSG_SLP_PROG(SLP_ML, miller_neg_g1, MILLER_NEG_G1)
 LSG_SLP_PROG(SLP_HORNER, horner_miller, HORNER_MILLER)
 LSG_SLP_PROG(SLP_ITEM1, miller_item1, MILLER_ITEM1)
+LSG_SLP_PROG(SLP_H2C_CLEAR, h2c_clear, H2C_CLEAR)
 
 // the program's steps (inputs and constants already in their slots): in every step lane pair
 // q executes operation q; the next step's descriptor and this lane pair's entry of it are in
@@ -103,7 +106,7 @@ __device__ __forceinline__ void slp_consts(uint32_t* lds, uint32_t q, uint32_t h
 template <int PROG, int W, int MODE>
 __global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __restrict__ in, uint32_t in_stride,
                                                 uint8_t* __restrict__ out, int32_t* __restrict__ verdict) {
-  using PR = Prog<PROG>;
+  using PR = Prog<PROG, W>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int item = blockIdx.x;
   if (item >= n_items) return;
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __re
   __syncthreads();
   slp_steps<PR>(lds, inp, q, h);
   // outputs: canonical values; lane pair j holds output j (n_out <= 32 W)
-  static_assert(PR::n_out <= 32, "one output per lane pair");
+  static_assert(PR::n_out <= 32, "one output per lane pair of the first wave");
   __shared__ uint32_t s_flag;
   fp_t c = fp_zero();
   bool nz = false;
@@ -164,16 +167,17 @@ __global__ void __launch_bounds__(64 * W) k_slp(int n_items, const uint8_t* __re
 // the pair (P_i, H(m_i)) of set item_first[item] -> that item's Miller value in lane form in
 // f (the layout k_miller_fused writes).  A set with an error or an infinite point takes part
 // as (0, 0) with use flag 0: its lines are the identity and it contributes 1.
-__global__ void __launch_bounds__(64) k_slp_items1(int n_items, const int32_t* __restrict__ item_first,
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_slp_items1(int n_items, const int32_t* __restrict__ item_first,
                                                    const uint32_t* __restrict__ P, const uint8_t* __restrict__ pinf,
                                                    const uint8_t* __restrict__ hinf, const int32_t* __restrict__ err,
                                                    const uint32_t* __restrict__ H, uint32_t* __restrict__ f) {
-  using PR = Prog<SLP_ITEM1>;
+  using PR = Prog<SLP_ITEM1, W>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int item = blockIdx.x;
   if (item >= n_items) return;
   const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
-  slp_consts<PR>(lds, q, h, 32);
+  slp_consts<PR>(lds, q, h, 32 * W);
   static_assert(PR::n_in == 7, "P.x, P.y, H.x.c0, H.x.c1, H.y.c0, H.y.c1, use");
   if (q < 7) {
     const size_t s = (size_t)item_first[item];
@@ -202,30 +206,98 @@ __global__ void __launch_bounds__(64) k_slp_items1(int n_items, const int32_t* _
   }
 }
 
+// hash_to_G2's last stages for small packages: Q = Q0 + Q1 (projective lane
+// form, k_h2c_map) -> H = clear_cofactor(Q) in affine lane form, hinf = (H = O); the same
+// outputs as k_h2c_clear + the batched inversion + k_h2c_affine
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_slp_h2c(int n, const uint32_t* __restrict__ Hp, uint32_t* __restrict__ H,
+                                                    uint8_t* __restrict__ hinf) {
+  using PR = Prog<SLP_H2C_CLEAR, W>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_nz;
+  const int item = blockIdx.x;
+  if (item >= n) return;
+  const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
+  slp_consts<PR>(lds, q, h, 32 * W);
+  static_assert(PR::n_in == 6 && PR::n_out == 6, "projective in, affine + Z out");
+  if (q < 6) {
+    const uint32_t* src = Hp + ((size_t)item * lsgl_w_g2p + 7 * q) * 2 + h;
+    fp_t v;
+#pragma unroll
+    for (int w = 0; w < 7; w++) v.l[w] = src[2 * w];
+    slot_store(lds, PR::in()[q], h, v);
+  }
+  if (tid == 0) s_nz = 0;
+  __syncthreads();
+  slp_steps<PR>(lds, nullptr, q, h);
+  fp_t v = fp_zero();
+  if (q < 6) v = slot_load(lds, PR::out()[q], h);
+  if (q == 4 || q == 5) {  // Z = 0: H is the point at infinity
+    const fp_t c = pair_canon_small(v);
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < 7; w++) x |= c.l[w];
+    x |= pswap(x);
+    if (x) s_nz = 1;  // benign race: every writer stores 1
+  }
+  __syncthreads();
+  const bool inf = s_nz == 0;
+  if (q < 4) {
+    if (inf) v = fp_zero();
+    uint32_t* dst = H + ((size_t)item * lsgl_w_g2a + 7 * q) * 2 + h;
+#pragma unroll
+    for (int w = 0; w < 7; w++) dst[2 * w] = v.l[w];
+  }
+  if (tid == 0) hinf[item] = inf ? 1 : 0;
+}
+
 template <int PROG, int W, int MODE>
 hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, uint8_t* out, int32_t* verdict) {
   if (n <= 0) return hipSuccess;
-  const size_t shm = (size_t)Prog<PROG>::n_slots * LSG_SLP_STRIDE * 4;
+  const size_t shm = (size_t)Prog<PROG, W>::n_slots * LSG_SLP_STRIDE * 4;
   hipLaunchKernelGGL((k_slp<PROG, W, MODE>), dim3(n), dim3(64 * W), shm, st, n, in, in_stride, out, verdict);
   return hipGetLastError();
 }
 
 }  // namespace
 
+// Two waves per item (steps of 64 operations, each wave on its own SIMD) while the items fit
+// the chip one wave per SIMD; one wave per item beyond (a fallback phase's thousands of
+// groups: throughput).  env LSG_SLP_W2_MAX (default 512).
+static int slp_waves(int n) {
+  const char* e = getenv("LSG_SLP_W2_MAX");
+  const int lim = e ? atoi(e) : 512;
+  return n <= lim ? 2 : 1;
+}
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
-  return launch<SLP_FE, 1, 0>(st, ng, F576, 576, nullptr, verdict);
+  return slp_waves(ng) == 2 ? launch<SLP_FE, 2, 0>(st, ng, F576, 576, nullptr, verdict)
+                            : launch<SLP_FE, 1, 0>(st, ng, F576, 576, nullptr, verdict);
 }
 hipError_t lsg_slp_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
-  return launch<SLP_ML, 1, 1>(st, ng, S288, 288, out576, nullptr);
+  return slp_waves(ng) == 2 ? launch<SLP_ML, 2, 1>(st, ng, S288, 288, out576, nullptr)
+                            : launch<SLP_ML, 1, 1>(st, ng, S288, 288, out576, nullptr);
 }
 hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
-  return launch<SLP_HORNER, 1, 1>(st, ng, C288, 288 * 64, out576, nullptr);
+  return slp_waves(ng) == 2 ? launch<SLP_HORNER, 2, 1>(st, ng, C288, 288 * 64, out576, nullptr)
+                            : launch<SLP_HORNER, 1, 1>(st, ng, C288, 288 * 64, out576, nullptr);
+}
+template <int W>
+static hipError_t items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P, const uint8_t* pinf,
+                         const uint8_t* hinf, const int32_t* err, const uint32_t* H, uint32_t* f) {
+  const size_t shm = (size_t)Prog<SLP_ITEM1, W>::n_slots * LSG_SLP_STRIDE * 4;
+  hipLaunchKernelGGL(k_slp_items1<W>, dim3(n_items), dim3(64 * W), shm, st, n_items, item_first, P, pinf, hinf, err, H, f);
+  return hipGetLastError();
 }
 hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,
                                  const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, const uint32_t* H,
                                  uint32_t* f) {
   if (n_items <= 0) return hipSuccess;
-  const size_t shm = (size_t)Prog<SLP_ITEM1>::n_slots * LSG_SLP_STRIDE * 4;
-  hipLaunchKernelGGL(k_slp_items1, dim3(n_items), dim3(64), shm, st, n_items, item_first, P, pinf, hinf, err, H, f);
+  return slp_waves(n_items) == 2 ? items1<2>(st, n_items, item_first, P, pinf, hinf, err, H, f)
+                                 : items1<1>(st, n_items, item_first, P, pinf, hinf, err, H, f);
+}
+hipError_t lsg_slp_h2c_clear(hipStream_t st, int n, const uint32_t* Hp, uint32_t* H, uint8_t* hinf) {
+  if (n <= 0) return hipSuccess;
+  const size_t shm = (size_t)Prog<SLP_H2C_CLEAR, 1>::n_slots * LSG_SLP_STRIDE * 4;
+  hipLaunchKernelGGL(k_slp_h2c<1>, dim3(n), dim3(64), shm, st, n, Hp, H, hinf);
   return hipGetLastError();
 }

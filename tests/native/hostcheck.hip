@@ -352,17 +352,22 @@ struct HcProg {
   int n_steps, n_slots, n_consts, n_in, n_out;
 };
 #define HC_PROG(NAME, UP)                                                                                  \
-  HcProg{lsg_slp_##NAME##_ops, lsg_slp_##NAME##_steps, lsg_slp_##NAME##_consts, lsg_slp_##NAME##_in,       \
-         lsg_slp_##NAME##_out, LSG_SLP_##UP##_N_STEPS, LSG_SLP_##UP##_N_SLOTS, LSG_SLP_##UP##_N_CONSTS,      \
-         LSG_SLP_##UP##_N_IN, LSG_SLP_##UP##_N_OUT}
+  HcProg{lsg_slp_##NAME##_w1_ops, lsg_slp_##NAME##_w1_steps, lsg_slp_##NAME##_w1_consts, lsg_slp_##NAME##_w1_in,  \
+         lsg_slp_##NAME##_w1_out, LSG_SLP_##UP##_W1_N_STEPS, LSG_SLP_##UP##_W1_N_SLOTS,                           \
+         LSG_SLP_##UP##_W1_N_CONSTS, LSG_SLP_##UP##_W1_N_IN, LSG_SLP_##UP##_W1_N_OUT},                           \
+  HcProg{lsg_slp_##NAME##_w2_ops, lsg_slp_##NAME##_w2_steps, lsg_slp_##NAME##_w2_consts, lsg_slp_##NAME##_w2_in,  \
+         lsg_slp_##NAME##_w2_out, LSG_SLP_##UP##_W2_N_STEPS, LSG_SLP_##UP##_W2_N_SLOTS,                           \
+         LSG_SLP_##UP##_W2_N_CONSTS, LSG_SLP_##UP##_W2_N_IN, LSG_SLP_##UP##_W2_N_OUT}
 extern "C" {
-// prog: 0 final_exp, 1 miller_neg_g1, 2 horner_miller, 3 miller_item1 (whose lane-form
+// prog: 2 k + (W - 1) for k = 0 final_exp, 1 miller_neg_g1, 2 horner_miller, 3 miller_item1,
+// 4 h2c_clear (the last two with lane-form
 // Montgomery inputs/outputs are converted here); in: the item's inputs as canonical 48-byte
 // values; out: the canonical outputs (48 bytes each).  Returns the output count.
 int hc_slp_run(int prog, const uint8_t* in, uint8_t* out) {
-  const HcProg P[4] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
-                       HC_PROG(horner_miller, HORNER_MILLER), HC_PROG(miller_item1, MILLER_ITEM1)};
-  const bool mont = prog == 3;  // Montgomery-form inputs and outputs (lane-form programs)
+  const HcProg P[10] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
+                        HC_PROG(horner_miller, HORNER_MILLER), HC_PROG(miller_item1, MILLER_ITEM1),
+                        HC_PROG(h2c_clear, H2C_CLEAR)};
+  const bool mont = prog / 2 >= 3;  // Montgomery-form inputs and outputs (lane-form programs)
   const fp_t r2 = fp_t(FP_R2), one = fp_t(FP_ONE_CANON);
   const HcProg& p = P[prog];
   std::vector<uint32_t> lds((size_t)p.n_slots * 16, 0xdeadbeefu);

@@ -308,10 +308,11 @@ def _g2_proj_blob(Q, z):
     return b2(f2_mul(x, z)) + b2(f2_mul(y, z)) + b2(z)
 
 
-def test_slp_programs_match_oracle(hc):
+@pytest.mark.parametrize("waves", [1, 2])
+def test_slp_programs_match_oracle(hc, waves):
     """The straight-line programs of the serial stages (tools/gen_slp.py), run op by op with
     the gfx950 interpreter's own operation code (lsg_slp_exec.hpp) in the host build of the
-    pair backend: final exponentiation, ML(-G1, S) and Horner + ML(-G1, S) against the
+    pair backend, scheduled for one and two waves per item: final exponentiation, ML(-G1, S) and Horner + ML(-G1, S) against the
     oracle (oracle/pairing.py final_exp_fast, miller_loop_fast)."""
     if hc.backend != "pair":
         pytest.skip("programs run on the pair backend")
@@ -323,14 +324,14 @@ def test_slp_programs_match_oracle(hc):
     Q = E2.mul(G2_GEN, 31337)
     prod = f12_mul(miller_loop_fast(pk, Q), miller_loop_fast(neg_g1, E2.mul(Q, 4242)))
     for f in (rf12(), prod):
-        assert hc.hc_slp_run(0, b12(f), o) == 12
+        assert hc.hc_slp_run(0 + waves - 1, b12(f), o) == 12
         assert ub12(o.raw[:576]) == final_exp_fast(f)
     assert final_exp_fast(prod) == F12_ONE
     # ML(-G1, S) of a projective S, and S.Z
     for k in (1, 77, 123456789):
         S = E2.mul(G2_GEN, k)
         z = rf2()
-        assert hc.hc_slp_run(1, _g2_proj_blob(S, z), o) == 14
+        assert hc.hc_slp_run(2 + waves - 1, _g2_proj_blob(S, z), o) == 14
         assert ub12(o.raw[:576]) == miller_loop_fast(neg_g1, S)
         assert ub2(o.raw[576:672]) == z
     # Horner over 64 per-bit sums (some at infinity), then ML(-G1, S)
@@ -339,16 +340,25 @@ def test_slp_programs_match_oracle(hc):
     S = None
     for k in range(63, -1, -1):
         S = E2.add(E2.add(S, S), Cs[k])
-    assert hc.hc_slp_run(2, blob, o) == 14
+    assert hc.hc_slp_run(4 + waves - 1, blob, o) == 14
     assert ub12(o.raw[:576]) == miller_loop_fast(neg_g1, S)
     # one-set Miller item (Montgomery lane-form in/out): a pair that takes part, and one that
     # does not (P = (0, 0), use 0) contributing exactly 1
     pk, Q = E1.mul(G1_GEN, 99), E2.mul(G2_GEN, 1234)
     (qx, qy) = Q
-    assert hc.hc_slp_run(3, be(pk[0]) + be(pk[1]) + b2(qx) + b2(qy) + be(1), o) == 12
+    assert hc.hc_slp_run(6 + waves - 1, be(pk[0]) + be(pk[1]) + b2(qx) + b2(qy) + be(1), o) == 12
     assert ub12(o.raw[:576]) == miller_loop_fast(pk, Q)
-    assert hc.hc_slp_run(3, be(0) + be(0) + b2(qx) + b2(qy) + be(0), o) == 12
+    assert hc.hc_slp_run(6 + waves - 1, be(0) + be(0) + b2(qx) + b2(qy) + be(0), o) == 12
     assert ub12(o.raw[:576]) == F12_ONE
+    # cofactor clearing + affine of an SSWU-map sum (a point of E2 outside G2), projective in
+    for k in range(2):
+        u = (rng.randrange(P), rng.randrange(P))
+        Qm = h2c.iso_map(h2c.map_to_curve_sswu(u))
+        z = rf2()
+        assert hc.hc_slp_run(8 + waves - 1, _g2_proj_blob(Qm, z), o) == 6
+        Hc = h2c.clear_cofactor(Qm)
+        assert (ub2(o.raw[:96]), ub2(o.raw[96:192])) == Hc
+        assert ub2(o.raw[192:288]) != (0, 0)
 
 
 def test_inv_gcd_matches_pow(hc):

@@ -760,6 +760,87 @@ def prog_miller_item1(E, inp):
     return flat12(miller_loop_masked(E, (v[0], v[1]), ((v[2], v[3]), (v[4], v[5])), v[6]))
 
 
+def _f2inv_int(a):
+    n = pow((a[0] * a[0] + a[1] * a[1]) % P, -1, P)
+    return (a[0] * n % P, -a[1] * n % P)
+
+
+def _f2mul_int(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+PSI_CX = _f2inv_int(_f2pow(XI, (P - 1) // 3))  # psi(x, y) = (conj(x) cx, conj(y) cy)
+PSI_CY = _f2inv_int(_f2pow(XI, (P - 1) // 2))
+PSI2_CX = _f2mul_int(PSI_CX, (PSI_CX[0], -PSI_CX[1] % P))[0]  # psi^2 = psi o psi: the norms
+PSI2_CY = _f2mul_int(PSI_CY, (PSI_CY[0], -PSI_CY[1] % P))[0]
+
+
+def g2_psi(E, p):
+    return (f2_mul(f2_conj(p[0]), f2_const(E, PSI_CX)), f2_mul(f2_conj(p[1]), f2_const(E, PSI_CY)), f2_conj(p[2]))
+
+
+def g2_psi2(E, p):
+    return (f2_mul_fp(p[0], E.const(PSI2_CX)), f2_mul_fp(p[1], E.const(PSI2_CY)), p[2])
+
+
+def g2_neg(p):
+    return (p[0], f2_neg(p[1]), p[2])
+
+
+def jac_dbl(p):
+    """Jacobian doubling, a = 0 (lsg_curve.hpp jac_dbl_t)"""
+    X, Y, Z = p
+    A = f2_sqr(X)
+    B = f2_sqr(Y)
+    C = f2_sqr(B)
+    D = f2_muls(f2_sub(f2_sqr(f2_add(X, B)), f2_add(A, C)), 2)
+    Ee = f2_muls(A, 3)
+    X3 = f2_sub(f2_sqr(Ee), f2_muls(D, 2))
+    Y3 = f2_sub(f2_mul(Ee, f2_sub(D, X3)), f2_muls(C, 8))
+    Z3 = f2_muls(f2_mul(Y, Z), 2)
+    return (X3, Y3, Z3)
+
+
+def jac_from_proj(p):
+    """homogeneous (X:Y:Z) -> Jacobian (XZ : YZ^2 : Z) (lsg_curve.hpp; the infinity select of
+    the kernels is left out: a hashed point at infinity has probability < 2^-380)"""
+    return (f2_mul(p[0], p[2]), f2_mul(p[1], f2_sqr(p[2])), p[2])
+
+
+def jac_to_proj(p):
+    return (f2_mul(p[0], p[2]), p[1], f2_mul(f2_sqr(p[2]), p[2]))
+
+
+def proj_mul_xabs(p):
+    """[|x|]P: 63 Jacobian doublings, 5 complete additions (lsg_curve.hpp proj_mul_xabs)"""
+    acc = jac_from_proj(p)
+    for b in range(62, -1, -1):
+        acc = jac_dbl(acc)
+        if (X_ABS >> b) & 1:
+            acc = jac_from_proj(g2_add(jac_to_proj(acc), p))
+    return jac_to_proj(acc)
+
+
+def clear_cofactor(E, p):
+    """h_eff P = c + [x]([x]P + psi(P)), c = psi^2(2P) - psi(P) - P - [x]P (lsg_h2c.hpp:228)"""
+    u = g2_psi(E, p)
+    c = g2_add(g2_psi2(E, g2_dbl(p)), g2_neg(u))
+    c = g2_add(c, g2_neg(p))
+    t1 = g2_neg(proj_mul_xabs(p))
+    c = g2_add(c, g2_neg(t1))
+    t2 = g2_neg(proj_mul_xabs(g2_add(t1, u)))
+    return g2_add(c, t2)
+
+
+def prog_h2c_clear(E, inp):
+    """in (Montgomery lane form): Q0 + Q1 of the SSWU map, projective (6 Fp); out: H = h_eff Q
+    affine (4 Fp, Montgomery) and its projective Z (2 Fp: the H = O test)"""
+    v = inp(6)
+    q = clear_cofactor(E, g2p_from(v))
+    zi = f2_inv(E, q[2])
+    return list(f2_mul(q[0], zi)) + list(f2_mul(q[1], zi)) + list(q[2])
+
+
 PROGRAMS = {
     # name: (builder, n_inputs, inputs: False = canonical blob bytes, True = loaded by LOADMUL
     #        ops inside the program, "mont" = Montgomery lane-form values, outputs likewise)
@@ -767,6 +848,7 @@ PROGRAMS = {
     "miller_neg_g1": (prog_miller_neg_g1, 6, False),
     "horner_miller": (prog_horner_miller, 384, True),
     "miller_item1": (prog_miller_item1, 7, "mont"),
+    "h2c_clear": (prog_h2c_clear, 6, "mont"),
 }
 
 
@@ -1026,55 +1108,62 @@ def build(name, W):
     return cx, steps, slot, n_slots
 
 
-def emit(out_path, n_check=1, W=1, verbose=True):
+WAVES = (1, 2)  # programs are scheduled for one and for two waves per item
+
+
+def emit(out_path, n_check=1, verbose=True):
     rng = random.Random(20261017)
     lines = ["// GENERATED by tools/gen_slp.py -- do not edit.",
-             "// Straight-line programs of the per-group serial stages (lsg_slp.hip).",
+             "// Straight-line programs of the per-group serial stages (lsg_slp.hip), each scheduled",
+             "// for W = 1 and 2 waves per item (steps of <= 32 W operations): lsg_slp_<name>_w<W>.",
              "#pragma once", "#include <stdint.h>",
              "#ifndef LSG_SLP_ARRAY", "#define LSG_SLP_ARRAY static const", "#endif", ""]
     for name in PROGRAMS:
-        cx, steps, slot, n_slots = build(name, W)
-        for _ in range(n_check):
-            x = rand_inputs(name, rng)
-            got = run_program(cx, steps, slot, n_slots, x)
-            if cx.load_inputs == "mont":  # Montgomery in and out
-                want = reference(name, [v * RINV % P for v in x])
-                got = [v * RINV % P for v in got]
-            else:
-                want = reference(name, x)
-            if got != want:
-                raise SystemExit("gen_slp: program %s does not reproduce its algorithm" % name)
-        words, desc = encode(cx, steps, slot)
-        nm, nl, ns, sm, cost = stats(cx, steps)
-        if verbose:
-            print("[gen_slp] %-14s W=%d ops %6d (mul %6d lin %5d) steps %5d (with mul %5d) cost %.0f slots %d" %
-                  (name, W, nm + nl, nm, nl, ns, sm, cost, n_slots), flush=True)
-        cn = "lsg_slp_%s" % name
-        lines.append("// %s: %d ops (%d products), %d steps, %d LDS slots" % (name, nm + nl, nm, ns, n_slots))
-        lines.append("LSG_SLP_ARRAY uint32_t %s_ops[%d] __attribute__((aligned(32))) = {" % (cn, len(words)))
-        for i in range(0, len(words), 8):
-            lines.append("  " + ", ".join("0x%08xu" % w for w in words[i:i + 8]) + ",")
-        lines.append("};")
-        lines.append("LSG_SLP_ARRAY uint32_t %s_steps[%d] = {" % (cn, len(desc)))
-        for i in range(0, len(desc), 12):
-            lines.append("  " + ", ".join("0x%08xu" % w for w in desc[i:i + 12]) + ",")
-        lines.append("};")
-        consts = [c for _, c in cx.const_list]
-        lines.append("LSG_SLP_ARRAY uint32_t %s_consts[%d] = {" % (cn, 14 * len(consts)))
-        for c in consts:
-            lines.append("  " + ", ".join("0x%08xu" % w for w in limbs29(c)) + ",")
-        lines.append("};")
-        ins = [slot[v] for v in cx.inputs] or [0]
-        outs = [slot[v] for v in cx.outputs]
-        lines.append("LSG_SLP_ARRAY uint16_t %s_in[%d] = {%s};" % (cn, len(ins), ", ".join(map(str, ins))))
-        lines.append("LSG_SLP_ARRAY uint16_t %s_out[%d] = {%s};" % (cn, len(outs), ", ".join(map(str, outs))))
-        lines.append("#define %s_N_STEPS %d" % (cn.upper(), ns))
-        lines.append("#define %s_N_SLOTS %d" % (cn.upper(), n_slots))
-        lines.append("#define %s_N_CONSTS %d" % (cn.upper(), len(consts)))
-        lines.append("#define %s_N_IN %d" % (cn.upper(), len(cx.inputs)))
-        lines.append("#define %s_N_LOAD %d" % (cn.upper(), cx.n_inputs if cx.load_inputs else 0))
-        lines.append("#define %s_N_OUT %d" % (cn.upper(), len(outs)))
-        lines.append("")
+        cx = trace(name)
+        for W in WAVES:
+            steps = schedule_loads(cx, W)
+            slot, n_slots = allocate(cx, steps)
+            for _ in range(n_check):
+                x = rand_inputs(name, rng)
+                got = run_program(cx, steps, slot, n_slots, x)
+                if cx.load_inputs == "mont":  # Montgomery in and out
+                    want = reference(name, [v * RINV % P for v in x])
+                    got = [v * RINV % P for v in got]
+                else:
+                    want = reference(name, x)
+                if got != want:
+                    raise SystemExit("gen_slp: program %s (W=%d) does not reproduce its algorithm" % (name, W))
+            words, desc = encode(cx, steps, slot)
+            nm, nl, ns, sm, cost = stats(cx, steps)
+            if verbose:
+                print("[gen_slp] %-14s W=%d ops %6d (mul %6d lin %5d) steps %5d (with mul %5d) cost %.0f slots %d" %
+                      (name, W, nm + nl, nm, nl, ns, sm, cost, n_slots), flush=True)
+            cn = "lsg_slp_%s_w%d" % (name, W)
+            lines.append("// %s: %d ops (%d products), %d steps, %d LDS slots" % (cn, nm + nl, nm, ns, n_slots))
+            lines.append("LSG_SLP_ARRAY uint32_t %s_ops[%d] __attribute__((aligned(32))) = {" % (cn, len(words)))
+            for i in range(0, len(words), 8):
+                lines.append("  " + ", ".join("0x%08xu" % w for w in words[i:i + 8]) + ",")
+            lines.append("};")
+            lines.append("LSG_SLP_ARRAY uint32_t %s_steps[%d] = {" % (cn, len(desc)))
+            for i in range(0, len(desc), 12):
+                lines.append("  " + ", ".join("0x%08xu" % w for w in desc[i:i + 12]) + ",")
+            lines.append("};")
+            consts = [c for _, c in cx.const_list]
+            lines.append("LSG_SLP_ARRAY uint32_t %s_consts[%d] = {" % (cn, 14 * len(consts)))
+            for c in consts:
+                lines.append("  " + ", ".join("0x%08xu" % w for w in limbs29(c)) + ",")
+            lines.append("};")
+            ins = [slot[v] for v in cx.inputs] or [0]
+            outs = [slot[v] for v in cx.outputs]
+            lines.append("LSG_SLP_ARRAY uint16_t %s_in[%d] = {%s};" % (cn, len(ins), ", ".join(map(str, ins))))
+            lines.append("LSG_SLP_ARRAY uint16_t %s_out[%d] = {%s};" % (cn, len(outs), ", ".join(map(str, outs))))
+            lines.append("#define %s_N_STEPS %d" % (cn.upper(), ns))
+            lines.append("#define %s_N_SLOTS %d" % (cn.upper(), n_slots))
+            lines.append("#define %s_N_CONSTS %d" % (cn.upper(), len(consts)))
+            lines.append("#define %s_N_IN %d" % (cn.upper(), len(cx.inputs)))
+            lines.append("#define %s_N_LOAD %d" % (cn.upper(), cx.n_inputs if cx.load_inputs else 0))
+            lines.append("#define %s_N_OUT %d" % (cn.upper(), len(outs)))
+            lines.append("")
     tmp = out_path + ".tmp"
     with open(tmp, "w") as f:
         f.write("\n".join(lines) + "\n")
