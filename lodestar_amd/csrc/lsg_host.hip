@@ -790,7 +790,8 @@ int launch_hash(Slot* s, int n) {
 
 // ---- staging: the package's sets into the slot's pinned arena (order given by `order`),
 // randomizers drawn here (seed == 0: OS CSPRNG; else deterministic, for tests)
-int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale) {
+int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale,
+               const std::vector<uint8_t>* noscale = nullptr) {
   size_t npk = 0, msg_total = 0;
   bool all_index = true;  // every key names a table row: 4-byte key slots (a block body's
                           // ~3.7M signers cross PCIe as 15 MB instead of 355 MB)
@@ -881,6 +882,11 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   } else if (n) {
     memset(rnd, 0, 8 * n);
   }
+  // sets that form a group of their own are verified as they are (maybeBatch.ts:34-38: one
+  // set is a plain verify): r_i = 0 means "not scaled" to k_pk_scale and k_sig_scale
+  if (scale && noscale)
+    for (size_t i = 0; i < n; i++)
+      if ((*noscale)[i]) rnd[i] = 0;
   memcpy(s->rnd.data(), rnd, 8 * n);
   hipStream_t S = s->st[0];
   struct {
@@ -1264,7 +1270,23 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   s->nb_sets = 0;
   for (size_t k : s->batch_order) s->nb_sets += s->jobs[k].count;
   s->K = miller_k_for(flat.size());
-  LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true));
+  // sets alone in their phase-A group (and so in every later group): no RLC scaling
+  std::vector<uint8_t> noscale(flat.size(), 0);
+  if (package_group_mode()) {
+    if (s->nb_sets == 1) noscale[0] = 1;
+  } else {
+    const auto ch = chunkify(s->batch_order.size(), 16);
+    for (auto& c : ch) {
+      size_t len = 0;
+      for (size_t q = c.first; q < c.second; q++) len += s->jobs[s->batch_order[q]].count;
+      if (len == 1)
+        for (size_t q = c.first; q < c.second; q++)
+          if (s->jobs[s->batch_order[q]].count == 1) noscale[s->jobs[s->batch_order[q]].first] = 1;
+    }
+  }
+  for (size_t k : nonb)
+    if (s->jobs[k].count == 1) noscale[s->jobs[k].first] = 1;
+  LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true, &noscale));
   // phase-A groups, MSM groups first: the package group, then one per non-batchable job
   PhasePlan& A = s->phA;
   A = PhasePlan();

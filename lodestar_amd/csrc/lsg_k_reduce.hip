@@ -13,6 +13,9 @@
 // chunk results (lsg_host.hip plan_seg), so a reduction is one or two launches instead of
 // one launch per tree level.
 #include "lsg_kcommon.hpp"
+namespace {
+#include "lsg_inv.hpp"
+}  // namespace
 
 template <class T>
 LSG_DEVI T shfl_xor_t(const T& v, int lane_mask) {
@@ -106,10 +109,13 @@ __global__ void LSG_KERNEL_ATTR k_binv_fold(int n, int zero_to_one, const uint32
   }
   lane_store(tot, item, acc);
 }
+// the one inversion of a batched inversion: the divstep GCD (lsg_inv.hpp, ~30 us) instead of
+// the ~455-product Fermat chain (~0.4 ms of dependent products on one lane pair)
 __global__ void LSG_KERNEL_ATTR k_binv_root(const uint32_t* __restrict__ top, uint32_t* __restrict__ inv) {
   LANE_ITEM(1);
   (void)lead;
-  lane_store(inv, 0, fp_inv(lane_load<fp_t>(top, 0)));
+  const fp_t d = pair_inv_gcd(pair_canon(lane_load<fp_t>(top, 0)));  // (x R)^-1 as an integer, 0 -> 0
+  lane_store(inv, 0, pair_mont_mul(d, fp_t(FP_RCUBE)));              // x^-1 R
 }
 // out[k] = 1 / in[k] from the chunk's inverse product tinv[chunk] and the prefix products
 __global__ void LSG_KERNEL_ATTR k_binv_unfold(int n, int zero_to_one, const uint32_t* __restrict__ in,

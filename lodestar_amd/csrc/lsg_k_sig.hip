@@ -62,7 +62,10 @@ __global__ void LSG_KERNEL_ATTR k_sig_scale(int n, const uint32_t* __restrict__ 
   (void)lead;
   if (mode && !mode[item]) return;  // a set of an MSM group: k_sig_proj wrote its point
   g2p_t r = proj_inf<fp2_t>();
-  if (sig_usable(item, inf, err, pinf)) r = proj_mul_u64(proj_from_aff(lane_load<g2a_t>(sig_aff, item)), rnd[item]);
+  if (sig_usable(item, inf, err, pinf)) {
+    r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
+    if (rnd[item] != 0) r = proj_mul_u64(r, rnd[item]);  // r_i = 0: a set verified alone, not scaled
+  }
   lane_store(out, item, r);
 }
 

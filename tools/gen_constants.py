@@ -140,6 +140,7 @@ def main(out, bits=32):
     s.append(fp_decl("FP_ONE", 1))
     s.append(fp_decl("FP_R2", RM % P))  # mont(R) = R^2
     s.append(fp_decl("FP_R3", (1 << 384) * RM % P))  # mont(2^384 R) (= R^3 for R = 2^384)
+    s.append(fp_decl("FP_RCUBE", RM * RM % P))  # R^3: mont(y, R^3) = y R^2 (an integer inverse to Montgomery)
     s.append(fp_decl("FP_R2_SHL256", (1 << 256) * RM % P))  # mont(2^256 R) = 2^256 R^2 mod p
     s.append(f"LSG_CONST fpc_t FP_ONE_CANON = {{{arrl(1)}}};  // plain 1 (for from_mont)\n")
     if BITS != 32:  # plain multipliers between this layout and the 12 x 32-bit (R = 2^384) one
