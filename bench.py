@@ -333,6 +333,9 @@ def main():
                     help="node workload: node/V8 flags -- the reference's production heap setting (Dockerfile:45 "
                          "NODE_OPTIONS=--max-old-space-size=4096) plus a 64 MB young generation for the verifier's "
                          "per-call promises (INTEGRATION.md)")
+    ap.add_argument("--coalesce", type=int, default=None,
+                    help="lsg_set_coalesce max sets per package (default: 4096 for gossip / sync, else 0 = off)")
+    ap.add_argument("--coalesce-inflight", type=int, default=2, help="launches on the device before packages are held")
     ap.add_argument("--devices", type=int, default=0,
                     help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
                          "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")
@@ -340,7 +343,9 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 6, "gossip": 8, "single": 1}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 16, "gossip": 16, "single": 1}[args.workload]
+    if args.coalesce is None:
+        args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
         args.packages = 2 if args.workload == "block" else args.depth + 1
 
@@ -366,7 +371,11 @@ def main():
     prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
     n_sets = wl.sets_per_package
     max_pks = int(n_sets * wl.pks_per_set) + 1
-    ctx.reserve(n_sets, max_pks, 32 * n_sets, n_slots=args.depth + 1)
+    # coalesced launches hold up to `depth` packages: slots sized for that
+    co = args.depth if args.coalesce and n_sets <= args.coalesce else 1
+    ctx.reserve(n_sets * co, max_pks * co, 32 * n_sets * co, n_slots=args.depth + 1)
+    if args.coalesce:
+        ctx.set_coalesce(args.coalesce, args.coalesce_inflight)
 
     import numpy as np
 
@@ -586,6 +595,7 @@ def main():
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
             "pipeline_depth": args.depth, "distinct_packages": len(prepared),
+            "coalesce": {"max_sets": args.coalesce, "inflight": args.coalesce_inflight} if args.coalesce else None,
             "allocations_in_timed_region": allocs, "timed_window_monotonic_ns": [w0, w1],
             "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
             "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),

@@ -180,6 +180,19 @@ int lsg_jobs_partial(lsg_ctx* ctx, lsg_ticket ticket, uint8_t* out576, int32_t* 
 int lsg_jobs_partial_device(lsg_ctx* ctx, lsg_ticket ticket, void* dev_out576, int32_t* has_batch);
 int lsg_wait_jobs_node(lsg_ctx* ctx, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results,
                        lsg_stats* stats);
+/* Coalescing of small packages (single-device contexts; off by default).  From this call on,
+ * a package of at most max_sets sets submitted with lsg_submit_jobs is copied (the caller's
+ * buffers are free on return) and, while max_inflight launches are on the device, held back;
+ * the held packages go out together as ONE launch when the device has room (a wait frees a
+ * slot) or when one of them is waited on.  Every package keeps the reference's semantics on
+ * its own (multithread/index.ts:335 one package per worker; worker.ts:30-106): its
+ * batchable jobs in 16-job chunks each checked as one RLC batch, per-job retry, the
+ * deserializeSet rule over its jobs, its own counters (n_final_exps counts the whole launch).
+ * Such tickets have no node protocol: lsg_jobs_partial* and lsg_wait_jobs_node with
+ * node_valid != -1 reject them.  This fills the GPU with many small packages (gossip-sized)
+ * without one launch -- and one chain of dependent kernels -- per package.  max_sets = 0 turns
+ * coalescing off (held packages are launched first). */
+int lsg_set_coalesce(lsg_ctx* ctx, uint32_t max_sets, int32_t max_inflight);
 /* Whole-job assignment of lsg_init_devices (host only, no device needed): owner[j] = device of
  * job j = floor(sets before j * n_devices / total sets). */
 int lsg_assign_jobs(const uint32_t* job_sets, size_t n_jobs, int32_t n_devices, int32_t* owner);

@@ -99,6 +99,7 @@ EXPORTS = [
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
     "lsg_signing_roots", "lsg_attestation_signing_roots", "lsg_jobs_partial_device", "lsg_final_submit_device",
+    "lsg_set_coalesce",
 ]
 
 
@@ -156,6 +157,7 @@ def load_library(path=LIB_PATH):
         lib.lsg_final_submit.argtypes = [vp, ctypes.c_char_p, sz, pu64]
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
         lib.lsg_pipeline_slots.argtypes = [vp, pi32]
+        lib.lsg_set_coalesce.argtypes = [vp, u32, i32]
         lib.lsg_probe_mad_peak.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         for name in EXPORTS:
             if name != "lsg_last_error":
@@ -296,6 +298,11 @@ class Context:
         max_pks = max_sets if max_pks is None else max_pks
         max_msg_bytes = 32 * max_sets if max_msg_bytes is None else max_msg_bytes
         self._check(self.lib.lsg_reserve(self.h, max_sets, max_pks, max_msg_bytes, n_slots), "lsg_reserve")
+
+    def set_coalesce(self, max_sets, max_inflight=2):
+        """lsg_set_coalesce: packages of <= max_sets sets are held while max_inflight launches
+        are on the device and go out together (0 turns it off)"""
+        self._check(self.lib.lsg_set_coalesce(self.h, int(max_sets), int(max_inflight)), "lsg_set_coalesce")
 
     def allocation_count(self):
         v = ctypes.c_uint64()

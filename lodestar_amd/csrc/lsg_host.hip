@@ -32,7 +32,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -117,6 +119,7 @@ std::vector<std::pair<size_t, size_t>> chunkify(size_t len, size_t min_per_chunk
   for (size_t i = 0; i < len; i += per) out.push_back({i, std::min(len, i + per)});
   return out;
 }
+
 
 // ---- segmented-reduction plans (lsgk::seg_reduce): int32 words appended to a slot's plan
 // arena, uploaded once per phase
@@ -228,7 +231,21 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
 // ---------------------------------------------------------------------------- state
 namespace {
 
-enum SlotKind { SLOT_FREE = 0, SLOT_JOBS = 1, SLOT_FINAL = 3 };
+enum SlotKind { SLOT_FREE = 0, SLOT_JOBS = 1, SLOT_FINAL = 3, SLOT_MERGE = 4 /* tickets of coalesced packages */ };
+
+// a small package held for a coalesced launch (lsg_set_coalesce): the caller's jobs, sets
+// and bytes copied, so the caller's buffers are free once lsg_submit_jobs returns
+struct PendingPkg {
+  uint64_t serial = 0, seed = 0;
+  size_t n_sets = 0;
+  std::vector<lsg_job> jobs;
+  std::vector<lsg_set> sets;
+  std::vector<uint8_t> data;
+};
+struct MergeTicket {
+  int slot = -1;  // -1: not launched yet
+  int sub = -1;
+};
 
 struct Dev;
 
@@ -325,6 +342,18 @@ struct Slot {
   lsg_stats stats;
   bool has_node = false;  // this slot computed the node check (device 0 of a multi-device ticket)
   size_t n_jobs = 0;      // device 0: the ticket's job count
+  // coalesced launch (lsg_set_coalesce): n_sub caller packages in one slot.  sub_first: their
+  // job-index bounds in the merged job list; bpos_first: their bounds in batch_order.  Each
+  // one keeps its own 16-job chunks, deserialisation rule and counters; the slot is freed
+  // when every sub-package's ticket has been waited on.
+  int n_sub = 0;
+  std::vector<size_t> sub_first, bpos_first;
+  std::vector<uint64_t> sub_serial;
+  std::vector<lsg_stats> sub_stats;
+  std::vector<int32_t> sub_pkfail;
+  std::vector<uint8_t> sub_done;
+  bool resolved = false, resolving = false;
+  int resolve_rc = LSG_OK;
 };
 
 struct Dev {
@@ -348,7 +377,16 @@ struct Dev {
 
 struct lsg_ctx {
   std::mutex mu;
+  std::condition_variable cv;  // waiters of a coalesced slot being resolved by another thread
   std::string err;
+  // coalescing (lsg_set_coalesce): packages of <= co_max_sets sets wait in `pending` while
+  // co_inflight launches are on the device, then go out as one launch
+  uint32_t co_max_sets = 0;
+  int co_inflight = 2;
+  size_t co_max_pending = 16384;
+  std::vector<PendingPkg> pending;
+  size_t pending_sets = 0;
+  std::unordered_map<uint64_t, MergeTicket> merged;
   int n_dev = 0;
   Dev* dev[LSG_MAX_DEVICES] = {};
   bool rccl = false;  // several distinct devices: the partials are all-gathered over RCCL
@@ -540,6 +578,28 @@ int slot_ready(Dev* d, Slot* s, int index) {
   const int rc = slot_create(d, s, index, nullptr);
   if (rc) slot_destroy(s);
   return rc;
+}
+
+// the 16-job chunks (worker.ts:51) of the slot's batchable jobs as batch_order positions:
+// over the whole package, or per sub-package of a coalesced launch (never across two)
+std::vector<std::pair<size_t, size_t>> slot_chunks(const Slot* s) {
+  if (s->n_sub == 0) return chunkify(s->batch_order.size(), 16);
+  std::vector<std::pair<size_t, size_t>> out;
+  for (int k = 0; k < s->n_sub; k++) {
+    const size_t a = s->bpos_first[k], b = s->bpos_first[k + 1];
+    if (b == a) continue;
+    for (auto& c : chunkify(b - a, 16)) out.push_back({a + c.first, a + c.second});
+  }
+  return out;
+}
+// sub-package of a batch_order position / of a job (coalesced launches; 0 otherwise)
+int sub_of_pos(const Slot* s, size_t q) {
+  if (s->n_sub == 0) return 0;
+  return (int)(std::upper_bound(s->bpos_first.begin(), s->bpos_first.end(), q) - s->bpos_first.begin()) - 1;
+}
+int sub_of_job(const Slot* s, size_t j) {
+  if (s->n_sub == 0) return 0;
+  return (int)(std::upper_bound(s->sub_first.begin(), s->sub_first.end(), j) - s->sub_first.begin()) - 1;
 }
 
 // ---- sizes
@@ -1239,7 +1299,8 @@ int launch_sig_prep(Slot* s, bool scale, const std::vector<uint8_t>* mode, uint3
 // first), plan and launch every per-set stage and group stage up to the canonical products
 // (ev_part).  n_node > 0: this slot also reduces the all-gathered partials of n_node devices
 // (its plan holds that product's chunk list).
-int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint64_t seed, int n_node) {
+int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint64_t seed, int n_node,
+              const std::vector<size_t>* subs = nullptr) {
   timer_reset(s);
   s->plan.clear();
   memset(&s->stats, 0, sizeof(s->stats));
@@ -1269,13 +1330,31 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     }
   s->nb_sets = 0;
   for (size_t k : s->batch_order) s->nb_sets += s->jobs[k].count;
+  // a coalesced launch: sub-package bounds (jobs and batch_order positions), per-sub state
+  s->n_sub = subs ? (int)subs->size() - 1 : 0;
+  s->resolved = s->resolving = false;
+  s->resolve_rc = LSG_OK;
+  if (subs) {
+    s->sub_first = *subs;
+    s->bpos_first.assign(1, 0);
+    size_t q = 0;
+    for (int k = 0; k < s->n_sub; k++) {
+      while (q < s->batch_order.size() && s->batch_order[q] < (*subs)[k + 1]) q++;
+      s->bpos_first.push_back(q);
+    }
+    lsg_stats z;
+    memset(&z, 0, sizeof(z));
+    s->sub_stats.assign(s->n_sub, z);
+    s->sub_pkfail.assign(s->n_sub, 0);
+    s->sub_done.assign(s->n_sub, 0);
+  }
   s->K = miller_k_for(flat.size());
   // sets alone in their phase-A group (and so in every later group): no RLC scaling
   std::vector<uint8_t> noscale(flat.size(), 0);
-  if (package_group_mode()) {
+  if (package_group_mode() && !subs) {
     if (s->nb_sets == 1) noscale[0] = 1;
   } else {
-    const auto ch = chunkify(s->batch_order.size(), 16);
+    const auto ch = slot_chunks(s);
     for (auto& c : ch) {
       size_t len = 0;
       for (size_t q = c.first; q < c.second; q++) len += s->jobs[s->batch_order[q]].count;
@@ -1300,11 +1379,11 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     (g.msm ? gm : gs).push_back(g);
     (g.msm ? om : os).push_back(owner);
   };
-  s->chunk_mode = !package_group_mode();
+  s->chunk_mode = !package_group_mode() || subs;  // a coalesced launch checks every chunk on its own
   s->chunk_group.clear();
   std::vector<std::pair<size_t, size_t>> chunks;
   if (s->chunk_mode) {
-    chunks = chunkify(s->batch_order.size(), 16);
+    chunks = slot_chunks(s);
     for (size_t c = 0; c < chunks.size(); c++) {
       size_t len = 0;
       for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
@@ -1327,7 +1406,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   // check (phase B) reuses them instead of re-running the Miller accumulation
   std::vector<size_t> chunk_sub;  // chunks with sets, in order
   if (!s->chunk_mode && s->nb_sets) {
-    chunks = chunkify(s->batch_order.size(), 16);
+    chunks = slot_chunks(s);
     A.sub.assign(om.size(), {});
     for (size_t g = 0; g < om.size(); g++) {
       if (om[g] != -2) continue;
@@ -1532,10 +1611,41 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     for (size_t j = 0; j < nj; j++) s->results[j] = {LSG_ERROR, pkfail};
     return LSG_OK;
   }
+  // counters of the chunk at batch_order position q: the slot's, and its sub-package's
+  auto retry_inc = [&](size_t q) {
+    s->stats.batch_retries++;
+    if (s->n_sub) s->sub_stats[(size_t)sub_of_pos(s, q)].batch_retries++;
+  };
+  auto succ_add = [&](size_t q, size_t len) {
+    s->stats.batch_sigs_success += (uint32_t)len;
+    if (s->n_sub) s->sub_stats[(size_t)sub_of_pos(s, q)].batch_sigs_success += (uint32_t)len;
+  };
+  // a coalesced launch: the deserializeSet rule per sub-package (worker.ts:41-43)
+  std::vector<uint8_t> job_dead(nj, 0);
+  for (int k = 0; k < s->n_sub; k++) {
+    const int32_t* pkerr = H_<int32_t>(s->h_pkerr);
+    int32_t e = 0;
+    size_t ej = 0;
+    for (size_t j = s->sub_first[k]; j < s->sub_first[k + 1] && !e; j++)
+      for (size_t i = s->jobs[j].first; i < s->jobs[j].first + s->jobs[j].count && !e; i++)
+        for (uint32_t q = 0; q < s->pk_cnt[i] && !e; q++)
+          if (pkerr[s->pk_first[i] + q]) {
+            e = pkerr[s->pk_first[i] + q];
+            ej = j - s->sub_first[k];
+          }
+    s->sub_pkfail[k] = e;
+    s->sub_stats[k].key_error = e;
+    s->sub_stats[k].key_error_job = e ? (uint32_t)ej : 0;
+    if (e)
+      for (size_t j = s->sub_first[k]; j < s->sub_first[k + 1]; j++) {
+        s->results[j] = {LSG_ERROR, e};
+        job_dead[j] = 1;
+      }
+  }
   // non-batchable jobs: their own group (worker.ts:88-96)
   for (size_t j = 0; j < nj; j++) {
     const int g = s->job_group[j];
-    if (g < 0) continue;
+    if (g < 0 || job_dead[j]) continue;
     const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
     s->results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{vA[(size_t)g] ? LSG_VALID : LSG_INVALID, 0};
   }
@@ -1547,7 +1657,7 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
   // accepting the package.
   (void)node_valid;
   const bool big_ok = s->big_g < 0 || vA[(size_t)s->big_g] != 0;
-  auto chunks = chunkify(s->batch_order.size(), 16);
+  auto chunks = slot_chunks(s);
   std::vector<size_t> retry;  // jobs verified individually (phase C)
   std::vector<Grp> chk;       // chunks checked on their own (phase B)
   std::vector<std::pair<size_t, size_t>> chk_jobs;
@@ -1566,11 +1676,12 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     any_err_chunk = any_err_chunk || chunk_err[c];
   }
   for (size_t c = 0; c < chunks.size(); c++) {
+    if (job_dead[s->batch_order[chunks[c].first]]) continue;  // its sub-package has a bad key
     const size_t first = s->jobs[s->batch_order[chunks[c].first]].first;
     size_t len = 0;
     for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
     if (len == 0) {  // maybeBatch([]) throws: retried, and every job throws again
-      s->stats.batch_retries++;
+      retry_inc(chunks[c].first);
       for (size_t q = chunks[c].first; q < chunks[c].second; q++)
         s->results[s->batch_order[q]] = {LSG_ERROR, LSG_ERR_EMPTY_SET};
       continue;
@@ -1578,18 +1689,18 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     if (!chunk_err[c] && s->chunk_mode) {  // the chunk's own phase-A group decides
       if (vA[(size_t)s->chunk_group[c]]) {
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
-        s->stats.batch_sigs_success += (uint32_t)len;
+        succ_add(chunks[c].first, len);
       } else {
-        s->stats.batch_retries++;
+        retry_inc(chunks[c].first);
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
       }
     } else if (!chunk_err[c]) {
       if (big_ok) {
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
-        s->stats.batch_sigs_success += (uint32_t)len;
+        succ_add(chunks[c].first, len);
       } else if (chunks.size() == 1 && !any_err_chunk) {
         // the package group is exactly this chunk: its verdict is the chunk's
-        s->stats.batch_retries++;
+        retry_inc(chunks[c].first);
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
       } else {
         Grp g;
@@ -1600,7 +1711,7 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         chk_items.push_back(c < s->chunk_items.size() ? s->chunk_items[c] : std::make_pair(-1, -1));
       }
     } else {  // the chunk throws (worker.ts:79-85): every job is verified on its own
-      s->stats.batch_retries++;
+      retry_inc(chunks[c].first);
       for (size_t q = chunks[c].first; q < chunks[c].second; q++) {
         const size_t j = s->batch_order[q];
         const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
@@ -1622,9 +1733,9 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     for (size_t c = 0; c < chk.size(); c++) {
       if (v[c]) {
         for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
-        s->stats.batch_sigs_success += (uint32_t)chk[c].len;
+        succ_add(chk_jobs[c].first, chk[c].len);
       } else {
-        s->stats.batch_retries++;
+        retry_inc(chk_jobs[c].first);
         if (reuse) {
           fail_chunks.push_back(c);
         } else {
@@ -1884,6 +1995,169 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
     keep_times(s);
   }
   (void)hipSetDevice(c->dev[0]->device);
+  return rc;
+}
+
+// ---- coalesced launches (lsg_set_coalesce)
+PendingPkg copy_pkg(const lsg_job* jobs, size_t n_jobs, uint64_t seed) {
+  PendingPkg pk;
+  pk.seed = seed;
+  size_t ns = 0, nb = 0;
+  for (size_t j = 0; j < n_jobs; j++)
+    for (uint32_t q = 0; q < jobs[j].n_sets; q++) {
+      const lsg_set& t = jobs[j].sets[q];
+      ns++;
+      nb += (t.pks ? (size_t)t.n_pks * (t.pk_len == LSG_PK_INDEX ? 4 : t.pk_len) : 0) + (t.msg ? t.msg_len : 0) +
+            (t.sig ? t.sig_len : 0);
+    }
+  pk.n_sets = ns;
+  pk.sets.resize(ns);
+  pk.data.resize(std::max(nb, (size_t)1));
+  pk.jobs.assign(jobs, jobs + n_jobs);
+  size_t si = 0, off = 0;
+  auto put = [&](const uint8_t* src, size_t len) -> const uint8_t* {
+    if (!src) return nullptr;
+    uint8_t* d = pk.data.data() + off;
+    if (len) memcpy(d, src, len);
+    off += len;
+    return d;
+  };
+  for (size_t j = 0; j < n_jobs; j++) {
+    pk.jobs[j].sets = pk.sets.data() + si;
+    for (uint32_t q = 0; q < jobs[j].n_sets; q++, si++) {
+      lsg_set t = jobs[j].sets[q];
+      t.pks = put(t.pks, t.pks ? (size_t)t.n_pks * (t.pk_len == LSG_PK_INDEX ? 4 : t.pk_len) : 0);
+      t.msg = put(t.msg, t.msg ? t.msg_len : 0);
+      t.sig = put(t.sig, t.sig ? t.sig_len : 0);
+      pk.sets[si] = t;
+    }
+  }
+  return pk;
+}
+
+int launches_in_flight(lsg_ctx* c) {
+  int n = 0;
+  for (int i = 0; i < LSG_SLOTS; i++) n += c->dev[0]->slots[i].kind == SLOT_JOBS ? 1 : 0;
+  return n;
+}
+
+// the pending packages as one launch: one slot, each package a sub-package with its own
+// chunks, deserialisation rule and counters (context lock held)
+int flush_pending(lsg_ctx* c) {
+  if (c->pending.empty()) return LSG_OK;
+  int p = -1;
+  for (int i = 0; i < LSG_SLOTS && p < 0; i++)
+    if (c->dev[0]->slots[i].kind == SLOT_FREE) p = i;
+  if (p < 0) {
+    c->err = "all pipeline slots are busy (wait on an outstanding ticket first)";
+    return LSG_ERR_BUSY;
+  }
+  Slot* s = &c->dev[0]->slots[p];
+  LSG_RC(slot_ready(c->dev[0], s, p));
+  std::vector<lsg_job> all;
+  std::vector<size_t> subs{0};
+  uint64_t seed = c->pending[0].seed;
+  for (auto& pk : c->pending) {
+    all.insert(all.end(), pk.jobs.begin(), pk.jobs.end());
+    subs.push_back(all.size());
+    if (!pk.seed) seed = 0;  // any package asking for OS randomness gets it for all
+  }
+  std::vector<size_t> ids(all.size());
+  for (size_t j = 0; j < ids.size(); j++) ids[j] = j;
+  int rc = pkg_part1(s, all.data(), ids, seed, 0, &subs);
+  if (!rc) rc = pkg_part2(s);
+  if (rc) {
+    sync_slot(s);
+    for (auto& pk : c->pending) c->merged.erase(pk.serial);  // their waits report the error
+    c->pending.clear();
+    c->pending_sets = 0;
+    return rc;
+  }
+  uint64_t serial;
+  (void)make_ticket(c, SLOT_JOBS, p, &serial);
+  s->kind = SLOT_JOBS;
+  s->serial = serial;
+  s->n_jobs = all.size();
+  s->sub_serial.clear();
+  for (size_t k = 0; k < c->pending.size(); k++) {
+    s->sub_serial.push_back(c->pending[k].serial);
+    c->merged[c->pending[k].serial] = MergeTicket{p, (int)k};
+  }
+  s->stats.submit_us = (uint32_t)((now_ns() - s->stats.start_ns) / 1000);
+  c->pending.clear();
+  c->pending_sets = 0;
+  return LSG_OK;
+}
+
+// launch what is pending when the device has room (after a wait freed a slot)
+void maybe_flush(lsg_ctx* c) {
+  if (!c->pending.empty() && launches_in_flight(c) < c->co_inflight) (void)flush_pending(c);
+}
+
+int submit_merged(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, size_t n_sets, lsg_ticket* ticket) {
+  if (c->pending_sets + n_sets > c->co_max_pending) LSG_RC(flush_pending(c));
+  PendingPkg pk = copy_pkg(jobs, n_jobs, seed);
+  uint64_t serial;
+  *ticket = make_ticket(c, SLOT_MERGE, 0, &serial);
+  pk.serial = serial;
+  c->merged[serial] = MergeTicket{};
+  c->pending.push_back(std::move(pk));
+  c->pending_sets += n_sets;
+  if (launches_in_flight(c) < c->co_inflight) {
+    const int rc = flush_pending(c);
+    if (rc && rc != LSG_ERR_BUSY) return rc;  // (busy: it stays pending, a later wait launches it)
+  }
+  return LSG_OK;
+}
+
+int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* stats) {
+  const uint64_t serial = t >> 16;
+  int p, k;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
+    auto it = c->merged.find(serial);
+    if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+    if (it->second.slot < 0) LSG_RC(flush_pending(c));  // the waiter wants it now
+    it = c->merged.find(serial);
+    if (it == c->merged.end() || it->second.slot < 0) return LSG_ERR_INVALID_ARG;
+    p = it->second.slot;
+    k = it->second.sub;
+    ev = c->dev[0]->slots[p].ev_done;
+  }
+  if (hipEventSynchronize(ev) != hipSuccess) return fail_c(c, "hipEventSynchronize", hipGetLastError());
+  CtxLock lk(c->mu);
+  LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
+  Slot* s = &c->dev[0]->slots[p];
+  c->cv.wait(lk, [&] { return !s->resolving; });
+  if (!s->resolved) {  // the first waiter resolves every sub-package (fallback phases included)
+    s->resolving = true;
+    s->resolve_rc = pkg_resolve(s, &lk, -1, 0);
+    s->resolved = true;
+    s->resolving = false;
+    c->cv.notify_all();
+  }
+  const int rc = s->resolve_rc;
+  for (size_t j = s->sub_first[k]; j < s->sub_first[k + 1]; j++) results[j - s->sub_first[k]] = s->results[j];
+  if (stats) {
+    *stats = s->sub_stats[k];
+    stats->start_ns = s->stats.start_ns;
+    stats->submit_us = s->stats.submit_us;
+    stats->n_final_exps = s->stats.n_final_exps;  // (the whole coalesced launch)
+    stats->end_ns = now_ns();
+  }
+  c->merged.erase(serial);
+  s->sub_done[k] = 1;
+  bool all = true;
+  for (uint8_t d : s->sub_done) all = all && d;
+  if (all) {
+    if (rc) sync_slot(s);
+    s->kind = SLOT_FREE;
+    s->n_sub = 0;
+    keep_times(s);
+    maybe_flush(c);
+  }
   return rc;
 }
 
@@ -2189,11 +2463,33 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
   for (size_t j = 0; j < n_jobs; j++)
     if (jobs[j].n_sets && !jobs[j].sets) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
+  if (c->co_max_sets && c->n_dev == 1) {
+    size_t ns = 0;
+    for (size_t j = 0; j < n_jobs; j++) ns += jobs[j].n_sets;
+    if (ns <= c->co_max_sets) return submit_merged(c, jobs, n_jobs, seed, ns, ticket);
+  }
   return submit_pkg(c, jobs, n_jobs, seed, ticket);
+}
+
+int lsg_set_coalesce(lsg_ctx* c, uint32_t max_sets, int32_t max_inflight) {
+  if (!c || max_inflight < 1) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  LSG_RC(flush_pending(c));
+  c->co_max_sets = max_sets;
+  c->co_inflight = max_inflight;
+  return LSG_OK;
 }
 
 int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_job_result* results, lsg_stats* stats) {
   if (!c) return LSG_ERR_INVALID_ARG;
+  if (((ticket >> 8) & 255) == SLOT_MERGE) {
+    if (node_valid != -1) {
+      c->err = "lsg_wait_jobs_node: a coalesced package has no node check of its own";
+      return LSG_ERR_INVALID_ARG;
+    }
+    if (!results) return LSG_ERR_INVALID_ARG;
+    return wait_merged(c, ticket, results, stats);
+  }
   if (int prc = presync_pkg(c, ticket, false)) return prc;
   CtxLock lk(c->mu);
   LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
@@ -2205,7 +2501,9 @@ int lsg_wait_jobs_node(lsg_ctx* c, lsg_ticket ticket, int32_t node_valid, lsg_jo
     c->err = "lsg_wait_jobs_node: a multi-device context runs its own node check";
     return LSG_ERR_INVALID_ARG;
   }
-  return wait_pkg(c, &lk, p, node_valid == -1 ? -2 : (node_valid ? 1 : 0), results, stats);
+  const int rc = wait_pkg(c, &lk, p, node_valid == -1 ? -2 : (node_valid ? 1 : 0), results, stats);
+  maybe_flush(c);
+  return rc;
 }
 
 int lsg_wait_jobs(lsg_ctx* c, lsg_ticket ticket, lsg_job_result* results, lsg_stats* stats) {
@@ -2284,6 +2582,18 @@ int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
   std::vector<hipEvent_t> evs;
   if (Slot* f = ticket_final(c, ticket)) {
     evs.push_back(f->ev_done);
+  } else if (((ticket >> 8) & 255) == SLOT_MERGE) {
+    auto it = c->merged.find(ticket >> 16);
+    if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+    if (it->second.slot < 0) {  // not launched: launch when the device has room
+      maybe_flush(c);
+      it = c->merged.find(ticket >> 16);
+      if (it == c->merged.end() || it->second.slot < 0) {
+        *done = 0;
+        return LSG_OK;
+      }
+    }
+    evs.push_back(c->dev[0]->slots[it->second.slot].ev_done);
   } else {
     const int p = ticket_pkg(c, ticket);
     if (p < 0) return LSG_ERR_INVALID_ARG;

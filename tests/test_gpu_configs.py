@@ -391,3 +391,54 @@ def test_node_mode_partials_device_resident(ctx, keys):
         assert ctx.final_wait(ctx.final_submit_device(dev[576:].data_ptr(), 2)) == ok
         got, _ = ctx.wait_jobs_node(t, 1 if ok else 0)
         assert [g[0] for g in got] == [0 if (not ok and i == 77) else 1 for i in range(200)]
+
+
+# ---- coalesced launches (lsg_set_coalesce): many small packages in one launch, each with the
+# reference's per-package semantics (multithread/index.ts:335 one package per worker,
+# worker.ts:30-106 chunks, retries and the deserializeSet rule)
+def test_coalesced_packages_match_separate_launches(keys):
+    from lodestar_amd._native import Context
+    c, ref = Context(0), Context(0)
+    try:
+        sets = single_sets(c, keys, b"coalesce", 260)
+        bad, _ = corrupt(c, keys, sets, 0.03, 11)
+        pk = bytearray(bad[200][0][0])
+        pk[95] ^= 1  # off the curve: rejects every job of ITS package only
+        badkey = ([bytes(pk)], bad[200][1], bad[200][2])
+        pkgs = [
+            [([s], 1) for s in bad[0:40]],                                  # gossip-like, some bad
+            [(bad[40 + 5 * k:45 + 5 * k], 0) for k in range(3)],            # non-batchable jobs
+            [([s], 1) for s in sets[60:80]],                                # all valid
+            [([s], 1) for s in bad[180:200]] + [([badkey], 1)],             # a bad key
+            [(sets[80:81], 1)],                                             # one set
+            [(bad[81:114], 1), (sets[114:118], 0), ([], 1)],                # multi-set, mixed, empty
+            [([s], 1) for s in bad[120:180]],                               # 60 jobs: 3 chunks
+            [],                                                             # no jobs
+        ]
+        c.set_coalesce(4096, 1)  # one launch in flight: the rest wait and go out together
+        tickets = [c.submit_jobs(p, seed=0) for p in pkgs]
+        assert all(t is not None for t in tickets)
+        got = {}
+        for i in (3, 0, 7, 5, 1, 6, 2, 4):  # waits in any order
+            got[i] = c.wait_jobs(tickets[i])
+        for i, p in enumerate(pkgs):
+            exp, est = ref.verify_jobs(p)
+            res, st = got[i]
+            assert res == exp, (i, res, exp)
+            for k in ("batch_retries", "batch_sigs_success", "key_error", "key_error_job"):
+                assert st[k] == est[k], (i, k, st[k], est[k])
+        assert got[3][0] == [(2, 2)] * len(pkgs[3])
+        # the oracle decides the packages without a bad key
+        for i in (0, 2, 6):
+            flat = [s for js, _ in pkgs[i] for s in js]
+            exp, retries, success = co.expected_jobs([[k] for k in range(len(flat))], [True] * len(flat), oracle_each(flat))
+            res, st = got[i]
+            assert [(g[0], g[1] if g[0] == 2 else 0) for g in res] == exp
+            assert (st["batch_retries"], st["batch_sigs_success"]) == (retries, success)
+        # off again: later packages launch on their own
+        c.set_coalesce(0, 1)
+        t = c.submit_jobs(pkgs[2])
+        assert t[0] >> 8 & 255 == 1 and c.wait_jobs(t)[0] == [(1, 0)] * 20
+    finally:
+        c.close()
+        ref.close()
