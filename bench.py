@@ -335,7 +335,7 @@ def main():
                          "per-call promises (INTEGRATION.md)")
     ap.add_argument("--coalesce", type=int, default=None,
                     help="lsg_set_coalesce max sets per package (default: 4096 for gossip / sync, else 0 = off)")
-    ap.add_argument("--coalesce-inflight", type=int, default=2, help="launches on the device before packages are held")
+    ap.add_argument("--coalesce-inflight", type=int, default=4, help="launches on the device before packages are held")
     ap.add_argument("--devices", type=int, default=0,
                     help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
                          "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")
@@ -343,7 +343,7 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 16, "gossip": 16, "single": 1}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 32, "single": 1}[args.workload]
     if args.coalesce is None:
         args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)

@@ -29,6 +29,7 @@ for step in "$@"; do
     bench-short) run bench_short 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench-*) w=${step#bench-}; run "bench_$w" 400 python -u bench.py --workload "$w" --no-cpu-baseline ;;
     depth-*) a=${step#depth-}; w=${a%%:*}; d=${a#*:}; run "bench_${w}_d$d" 400 python -u bench.py --workload "$w" --depth "$d" --no-cpu-baseline ;;
+    co-*) a=${step#co-}; w=${a%%:*}; r=${a#*:}; d=${r%%:*}; f=${r#*:}; run "bench_${w}_d${d}_f$f" 400 python -u bench.py --workload "$w" --depth "$d" --coalesce-inflight "$f" --no-cpu-baseline ;;
     devices1) run bench_devices1 400 python -u bench.py --devices 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
     node-semi128) run bench_node_semi128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" ;;
