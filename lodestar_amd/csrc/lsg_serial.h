@@ -40,6 +40,11 @@ hipError_t lsg_slp_horner_miller(hipStream_t st, int ng, const uint8_t* C288, ui
 // hash_to_G2's cofactor clearing and affine conversion: Hp (projective lane form, the SSWU
 // map's Q0 + Q1) -> H (affine lane form), hinf
 hipError_t lsg_slp_h2c_clear(hipStream_t st, int n, const uint32_t* Hp, uint32_t* H, uint8_t* hinf);
+// signature side of small packages: G2 membership (k_sig_subgroup's contract) and [r_i] sig_i
+// (k_sig_scale's: mode selects the sets, r_i = 0 leaves a point unscaled)
+hipError_t lsg_slp_g2_subgroup(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, int32_t* err);
+hipError_t lsg_slp_g2_scale(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                            const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out);
 // Miller items of one set each (lane-form P, pinf, hinf, err, H as for k_miller_fused):
 // f[item] = ML(P_i, H_i) of set item_first[item], 1 for a set that does not take part
 hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,

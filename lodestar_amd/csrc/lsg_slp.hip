@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "lsg_serial.h"
+#include "../../include/lodestar_bls.h"
 
 namespace {
 #include "lsg_fp_pair.hpp"
@@ -31,7 +32,7 @@ constexpr size_t lsgl_w_g1a = lsgl::W_G1A / 2, lsgl_w_g2a = lsgl::W_G2A / 2, lsg
 
 namespace {
 
-enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3, SLP_H2C_CLEAR = 4 };
+enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3, SLP_H2C_CLEAR = 4, SLP_G2_SUBGROUP = 5, SLP_G2_SCALE = 6 };
 
 template <int PROG, int W>
 struct Prog;
@@ -56,6 +57,8 @@ LSG_SLP_PROG(SLP_ML, miller_neg_g1, MILLER_NEG_G1)
 LSG_SLP_PROG(SLP_HORNER, horner_miller, HORNER_MILLER)
 LSG_SLP_PROG(SLP_ITEM1, miller_item1, MILLER_ITEM1)
 LSG_SLP_PROG(SLP_H2C_CLEAR, h2c_clear, H2C_CLEAR)
+LSG_SLP_PROG(SLP_G2_SUBGROUP, g2_subgroup, G2_SUBGROUP)
+LSG_SLP_PROG(SLP_G2_SCALE, g2_scale, G2_SCALE)
 
 // the program's steps (inputs and constants already in their slots): in every step lane pair
 // q executes operation q; the next step's descriptor and this lane pair's entry of it are in
@@ -251,6 +254,88 @@ __global__ void __launch_bounds__(64 * W) k_slp_h2c(int n, const uint32_t* __res
   if (tid == 0) hinf[item] = inf ? 1 : 0;
 }
 
+// lane-form component c (7 words per lane) of item i in an array of W-word-per-lane items
+__device__ __forceinline__ fp_t lane_comp(const uint32_t* mem, size_t i, size_t wlane, uint32_t c, uint32_t h) {
+  const uint32_t* src = mem + (i * wlane + 7 * c) * 2 + h;
+  fp_t v;
+#pragma unroll
+  for (int w = 0; w < 7; w++) v.l[w] = src[2 * w];
+  return v;
+}
+__device__ __forceinline__ void lane_comp_store(uint32_t* mem, size_t i, size_t wlane, uint32_t c, uint32_t h,
+                                                const fp_t& v) {
+  uint32_t* dst = mem + (i * wlane + 7 * c) * 2 + h;
+#pragma unroll
+  for (int w = 0; w < 7; w++) dst[2 * w] = v.l[w];
+}
+
+// G2 membership of decoded signatures for small packages (k_sig_subgroup's contract, SURVEY
+// 8a M2: Signature.fromBytes(validate)): psi(P) == [x]P with complete formulas
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_slp_g2_subgroup(int n, const uint32_t* __restrict__ sig_aff,
+                                                            const uint8_t* __restrict__ inf, int32_t* __restrict__ err) {
+  using PR = Prog<SLP_G2_SUBGROUP, W>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_nz;
+  const int item = blockIdx.x;
+  if (item >= n || err[item] != 0 || inf[item]) return;  // (uniform over the workgroup)
+  const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
+  slp_consts<PR>(lds, q, h, 32 * W);
+  if (q < 4) slot_store(lds, PR::in()[q], h, lane_comp(sig_aff, (size_t)item, lsgl_w_g2a, q, h));
+  if (tid == 0) s_nz = 0;
+  __syncthreads();
+  slp_steps<PR>(lds, nullptr, q, h);
+  if (q < 4) {
+    const fp_t c = pair_canon_small(slot_load(lds, PR::out()[q], h));
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < 7; w++) x |= c.l[w];
+    x |= pswap(x);
+    if (x) s_nz = 1;  // benign race: every writer stores 1
+  }
+  __syncthreads();
+  if (tid == 0 && s_nz) err[item] = LSG_BLST_POINT_NOT_IN_GROUP;
+}
+
+// [r_i] sig_i for the RLC of small packages (k_sig_scale's contract): mode (optional) selects
+// the sets; unusable sets get O, r_i = 0 (a set verified alone) its point unscaled
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_slp_g2_scale(int n, const uint32_t* __restrict__ sig_aff,
+                                                         const uint8_t* __restrict__ inf, const int32_t* __restrict__ err,
+                                                         const uint8_t* __restrict__ pinf, const uint64_t* __restrict__ rnd,
+                                                         const uint8_t* __restrict__ mode, uint32_t* __restrict__ out) {
+  using PR = Prog<SLP_G2_SCALE, W>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int item = blockIdx.x;
+  if (item >= n || (mode && !mode[item])) return;
+  const uint32_t tid = threadIdx.x, h = tid & 1u, q = tid >> 1;
+  const bool usable = err[item] == 0 && !inf[item] && !(pinf && pinf[item]);
+  const uint64_t r = rnd[item];
+  if (!usable || r == 0) {  // O = (0 : 1 : 0), or (x : y : 1)
+    if (q < 6) {
+      fp_t v = fp_zero();
+      if (q == 2 && !usable) v = fp_t(FP_ONE);
+      if (q == 4 && usable) v = fp_t(FP_ONE);
+      if (usable && q < 4) v = lane_comp(sig_aff, (size_t)item, lsgl_w_g2a, q, h);
+      lane_comp_store(out, (size_t)item, lsgl_w_g2p, q, h, v);
+    }
+    return;
+  }
+  slp_consts<PR>(lds, q, h, 32 * W);
+  static_assert(PR::n_in == 68 && PR::n_out == 6, "point + 64 bits in, projective out");
+  for (uint32_t j = q; j < 68; j += 32 * W) {
+    fp_t v = fp_zero();
+    if (j < 4)
+      v = lane_comp(sig_aff, (size_t)item, lsgl_w_g2a, j, h);
+    else if ((r >> (j - 4)) & 1u)
+      v = fp_t(FP_ONE);
+    slot_store(lds, PR::in()[j], h, v);
+  }
+  __syncthreads();
+  slp_steps<PR>(lds, nullptr, q, h);
+  if (q < 6) lane_comp_store(out, (size_t)item, lsgl_w_g2p, q, h, slot_load(lds, PR::out()[q], h));
+}
+
 template <int PROG, int W, int MODE>
 hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, uint8_t* out, int32_t* verdict) {
   if (n <= 0) return hipSuccess;
@@ -285,7 +370,7 @@ template <int W>
 static hipError_t items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P, const uint8_t* pinf,
                          const uint8_t* hinf, const int32_t* err, const uint32_t* H, uint32_t* f) {
   const size_t shm = (size_t)Prog<SLP_ITEM1, W>::n_slots * LSG_SLP_STRIDE * 4;
-  hipLaunchKernelGGL(k_slp_items1<W>, dim3(n_items), dim3(64 * W), shm, st, n_items, item_first, P, pinf, hinf, err, H, f);
+  hipLaunchKernelGGL((k_slp_items1<W>), dim3(n_items), dim3(64 * W), shm, st, n_items, item_first, P, pinf, hinf, err, H, f);
   return hipGetLastError();
 }
 hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,
@@ -298,6 +383,29 @@ hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* ite
 hipError_t lsg_slp_h2c_clear(hipStream_t st, int n, const uint32_t* Hp, uint32_t* H, uint8_t* hinf) {
   if (n <= 0) return hipSuccess;
   const size_t shm = (size_t)Prog<SLP_H2C_CLEAR, 1>::n_slots * LSG_SLP_STRIDE * 4;
-  hipLaunchKernelGGL(k_slp_h2c<1>, dim3(n), dim3(64), shm, st, n, Hp, H, hinf);
+  hipLaunchKernelGGL((k_slp_h2c<1>), dim3(n), dim3(64), shm, st, n, Hp, H, hinf);
   return hipGetLastError();
+}
+template <int W>
+static hipError_t g2_subgroup_w(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, int32_t* err) {
+  const size_t shm = (size_t)Prog<SLP_G2_SUBGROUP, W>::n_slots * LSG_SLP_STRIDE * 4;
+  hipLaunchKernelGGL((k_slp_g2_subgroup<W>), dim3(n), dim3(64 * W), shm, st, n, sig_aff, inf, err);
+  return hipGetLastError();
+}
+template <int W>
+static hipError_t g2_scale_w(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                             const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out) {
+  const size_t shm = (size_t)Prog<SLP_G2_SCALE, W>::n_slots * LSG_SLP_STRIDE * 4;
+  hipLaunchKernelGGL((k_slp_g2_scale<W>), dim3(n), dim3(64 * W), shm, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
+  return hipGetLastError();
+}
+hipError_t lsg_slp_g2_subgroup(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, int32_t* err) {
+  if (n <= 0) return hipSuccess;
+  return slp_waves(n) == 2 ? g2_subgroup_w<2>(st, n, sig_aff, inf, err) : g2_subgroup_w<1>(st, n, sig_aff, inf, err);
+}
+hipError_t lsg_slp_g2_scale(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
+                            const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out) {
+  if (n <= 0) return hipSuccess;
+  return slp_waves(n) == 2 ? g2_scale_w<2>(st, n, sig_aff, inf, err, pinf, rnd, mode, out)
+                           : g2_scale_w<1>(st, n, sig_aff, inf, err, pinf, rnd, mode, out);
 }

@@ -360,13 +360,14 @@ struct HcProg {
          LSG_SLP_##UP##_W2_N_CONSTS, LSG_SLP_##UP##_W2_N_IN, LSG_SLP_##UP##_W2_N_OUT}
 extern "C" {
 // prog: 2 k + (W - 1) for k = 0 final_exp, 1 miller_neg_g1, 2 horner_miller, 3 miller_item1,
-// 4 h2c_clear (the last two with lane-form
+// 4 h2c_clear, 5 g2_subgroup, 6 g2_scale (the last four with lane-form
 // Montgomery inputs/outputs are converted here); in: the item's inputs as canonical 48-byte
 // values; out: the canonical outputs (48 bytes each).  Returns the output count.
 int hc_slp_run(int prog, const uint8_t* in, uint8_t* out) {
-  const HcProg P[10] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
+  const HcProg P[14] = {HC_PROG(final_exp, FINAL_EXP), HC_PROG(miller_neg_g1, MILLER_NEG_G1),
                         HC_PROG(horner_miller, HORNER_MILLER), HC_PROG(miller_item1, MILLER_ITEM1),
-                        HC_PROG(h2c_clear, H2C_CLEAR)};
+                        HC_PROG(h2c_clear, H2C_CLEAR), HC_PROG(g2_subgroup, G2_SUBGROUP),
+                        HC_PROG(g2_scale, G2_SCALE)};
   const bool mont = prog / 2 >= 3;  // Montgomery-form inputs and outputs (lane-form programs)
   const fp_t r2 = fp_t(FP_R2), one = fp_t(FP_ONE_CANON);
   const HcProg& p = P[prog];

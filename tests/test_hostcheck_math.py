@@ -359,6 +359,33 @@ def test_slp_programs_match_oracle(hc, waves):
         Hc = h2c.clear_cofactor(Qm)
         assert (ub2(o.raw[:96]), ub2(o.raw[96:192])) == Hc
         assert ub2(o.raw[192:288]) != (0, 0)
+    # G2 membership: a subgroup point passes, an E2 point outside G2 (the map's raw output)
+    # and a small-order point fail
+    Sg = E2.mul(G2_GEN, 4321)
+    R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    H2 = 0x5D543A95414E7F1091D50792876A202CD91DE4547085ABAA68A205B2E5A7DDFA628F1CB4D9E82EF21537E293A6691AE1616EC6E786F0C70CF1C38E31C7238E5
+    small = None  # a point of small prime order l | h2 (the complete formulas meet O on the way)
+    for t in range(20):
+        Qt = h2c.iso_map(h2c.map_to_curve_sswu((7 + t, 11 * t)))
+        for l in (13, 23, 2713):
+            cand = E2.mul(Qt, R_ORDER * (H2 // l))
+            if cand is not None:
+                small, order = cand, l
+                break
+        if small is not None:
+            break
+    assert small is not None and E2.mul(small, order) is None
+    for pt, member in ((Sg, True), (Qm, False), (small, False)):
+        assert hc.hc_slp_run(10 + waves - 1, b2(pt[0]) + b2(pt[1]), o) == 4
+        zero = all(ub2(o.raw[96 * i:96 * i + 96]) == (0, 0) for i in range(2))
+        assert zero == member
+    # [r] P for a 64-bit r, bits least significant first (0 / 1 in Montgomery form)
+    for r in (1, 2, 3, 0xDEADBEEFCAFEF00D, (1 << 64) - 1):
+        bits = b"".join(be((r >> k) & 1) for k in range(64))
+        assert hc.hc_slp_run(12 + waves - 1, b2(Sg[0]) + b2(Sg[1]) + bits, o) == 6
+        X, Y, Z = ub2(o.raw[:96]), ub2(o.raw[96:192]), ub2(o.raw[192:288])
+        zi = f2_inv(Z)
+        assert (f2_mul(X, zi), f2_mul(Y, zi)) == E2.mul(Sg, r)
 
 
 def test_inv_gcd_matches_pow(hc):

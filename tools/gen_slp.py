@@ -841,6 +841,61 @@ def prog_h2c_clear(E, inp):
     return list(f2_mul(q[0], zi)) + list(f2_mul(q[1], zi)) + list(q[2])
 
 
+def g2_mul_xabs_complete(p):
+    """[|x|]P with the complete formulas only (RCB doubling and addition): exact for every
+    point of E2, small-order ones included -- the subgroup check's inputs are adversarial"""
+    acc = p
+    for b in range(62, -1, -1):
+        acc = g2_dbl(acc)
+        if (X_ABS >> b) & 1:
+            acc = g2_add(acc, p)
+    return acc
+
+
+def prog_g2_subgroup(E, inp):
+    """Scott's test psi(P) == [x]P (x < 0; lsg_curve.hpp g2_in_group) for an affine signature
+    point (4 Fp, Montgomery lane form); out: X1 Z2 - X2 Z1, Y1 Z2 - Y2 Z1 of psi(P) and -[|x|]P
+    (4 Fp): both zero iff P is in G2 (the kernel reads them)"""
+    v = inp(4)
+    P = ((v[0], v[1]), (v[2], v[3]), f2_one(E))
+    X1, Y1, Z1 = g2_psi(E, P)
+    X2, Y2, Z2 = g2_neg(g2_mul_xabs_complete(P))
+    return list(f2_sub(f2_mul(X1, Z2), f2_mul(X2, Z1))) + list(f2_sub(f2_mul(Y1, Z2), f2_mul(Y2, Z1)))
+
+
+def prog_g2_scale(E, inp):
+    """[r] sig for the RLC (lsg_k_sig.hip k_sig_scale): in the affine point (4 Fp, Montgomery
+    lane form) and the 64 bits of r as 0 / 1 (Montgomery) values, least significant first; out:
+    [r] P projective (6 Fp).  2-bit windows: the window's point (O, P, 2P or 3P) is a linear
+    combination of the precomputed multiples with the window's indicator values -- selected
+    off the critical path -- added with the complete formulas (exact for O)"""
+    v = inp(4 + 64)
+    one = E.const(1)
+    P = ((v[0], v[1]), (v[2], v[3]), f2_one(E))
+    bits = v[4:]
+    P2 = g2_dbl(P)
+    P3 = g2_add(P2, P)
+    T = None
+    for w in range(31, -1, -1):
+        b1, b0 = bits[2 * w + 1], bits[2 * w]
+        c3 = b1 * b0
+        c2 = b1 - c3
+        c1 = b0 - c3
+        pick = []
+        for k in range(3):  # X, Y, Z
+            comp = []
+            for i in range(2):
+                t = c1 * P[k][i] if not (k == 2) else (c1 if i == 0 else E.zero())
+                t = t + c2 * P2[k][i] + c3 * P3[k][i]
+                if k == 1 and i == 0:
+                    t = t + (one - c1 - c2 - c3)  # O = (0 : 1 : 0)
+                comp.append(t)
+            pick.append(tuple(comp))
+        D = tuple(pick)
+        T = D if T is None else g2_add(g2_dbl(g2_dbl(T)), D)
+    return [c for pt in T for c in pt]
+
+
 PROGRAMS = {
     # name: (builder, n_inputs, inputs: False = canonical blob bytes, True = loaded by LOADMUL
     #        ops inside the program, "mont" = Montgomery lane-form values, outputs likewise)
@@ -849,6 +904,8 @@ PROGRAMS = {
     "horner_miller": (prog_horner_miller, 384, True),
     "miller_item1": (prog_miller_item1, 7, "mont"),
     "h2c_clear": (prog_h2c_clear, 6, "mont"),
+    "g2_subgroup": (prog_g2_subgroup, 4, "mont"),
+    "g2_scale": (prog_g2_scale, 68, "mont"),
 }
 
 
@@ -938,25 +995,37 @@ def schedule(cx, W, earliest=None):
     return [s for s in steps if s]
 
 
-def schedule_loads(cx, W):
-    """LOADMUL inputs: schedule once, then hold each load back to a few steps before its
-    first consumer (otherwise the loads run first and all 384 inputs sit in LDS)"""
-    steps = schedule(cx, W)
-    if not cx.load_inputs:
-        return steps
-    step_of = {}
-    for t, s in enumerate(steps):
-        for o in s:
-            step_of[o] = t
+def _hold_back(cx, steps, pred, lead):
+    """earliest steps holding every op selected by pred back to `lead` steps before its first
+    consumer in `steps` (ops scheduled early only because capacity was free hold their results
+    in LDS for nothing)"""
     first_use = {}
-    for t, s in enumerate(steps):
-        for o in s:
+    for t, st in enumerate(steps):
+        for o in st:
             for v, _ in cx.ops[o][2] + cx.ops[o][3]:
                 p = cx.prod[v]
-                if p >= 0 and cx.ops[p][0] == "loadmul":
+                if p >= 0 and pred(p):
                     first_use[p] = min(first_use.get(p, 1 << 30), t)
-    earliest = {p: max(0, u - 3) for p, u in first_use.items()}
-    return schedule(cx, W, earliest)
+    return {p: max(0, u - lead) for p, u in first_use.items()}
+
+
+def schedule_loads(cx, W, passes=3, lead=4):
+    """list schedule, then hold LOADMUL inputs and off-critical-path work back towards their
+    consumers: a few passes, each kept only if it does not lengthen the program"""
+    steps = schedule(cx, W)
+    if cx.load_inputs is True:
+        steps = schedule(cx, W, _hold_back(cx, steps, lambda p: cx.ops[p][0] == "loadmul", 3))
+    best = steps
+    _, best_slots = allocate(cx, best)
+    for _ in range(passes):
+        cand = schedule(cx, W, _hold_back(cx, steps, lambda p: True, lead))
+        if len(cand) > len(best) * 1.01:
+            break
+        _, ns = allocate(cx, cand)
+        steps = cand
+        if ns < best_slots:
+            best, best_slots = cand, ns
+    return best
 
 
 def allocate(cx, steps):
