@@ -343,7 +343,7 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 32, "single": 1}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 64, "single": 1}[args.workload]
     if args.coalesce is None:
         args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
