@@ -398,15 +398,22 @@ LSG_INL proj_t<F> proj_mul_u64_s3(const proj_t<F>& p, uint64_t k) {
 
 // [|x|]P for the BLS parameter |x| = 0xd201000000010000 (public, uniform branch):
 // 63 Jacobian doublings, 5 complete additions
-template <class F>
-LSG_INL proj_t<F> proj_mul_xabs(const proj_t<F>& p) {
+// The base point comes from get() at each addition: a per-set kernel keeps it in LDS
+// (lsg_kcommon.hpp lds_park) so that the doubling chain holds one point in registers.
+template <class F, class G>
+LSG_INL proj_t<F> proj_mul_xabs_get(const G& get) {
   const uint64_t xa = ((uint64_t)LSG_X_ABS_HI << 32) | LSG_X_ABS_LO;
-  jac_t<F> acc = jac_from_proj(p);
+  jac_t<F> acc = jac_from_proj(get());
+#pragma unroll 1
   for (int b = 62; b >= 0; b--) {
     acc = jac_dbl(acc);
-    if ((xa >> b) & 1u) acc = jac_add_proj(acc, p);
+    if ((xa >> b) & 1u) acc = jac_add_proj(acc, get());
   }
   return jac_to_proj(acc);
+}
+template <class F>
+LSG_INL proj_t<F> proj_mul_xabs(const proj_t<F>& p) {
+  return proj_mul_xabs_get<F>([&]() { return p; });
 }
 
 template <class F>
@@ -442,10 +449,14 @@ LSG_INL g2p_t g2_psi2(const g2p_t& p) {
 }
 
 // Scott's G2 membership test: psi(P) == [x]P (x < 0)
+template <class G>
+LSG_INL bool g2_in_group_get(const G& get) {
+  if (proj_is_inf(get())) return true;
+  g2p_t xp = proj_neg(proj_mul_xabs_get<fp2_t>(get));
+  return proj_eq(g2_psi(get()), xp);
+}
 LSG_BIGFN bool g2_in_group(g2p_t p) {
-  if (proj_is_inf(p)) return true;
-  g2p_t xp = proj_neg(proj_mul_xabs(p));
-  return proj_eq(g2_psi(p), xp);
+  return g2_in_group_get([&]() { return p; });
 }
 
 // G1 membership by definition, [r]P == O: double-and-add over the 255-bit group order

@@ -234,3 +234,23 @@ LSG_BIGFN g2p_t clear_cofactor_g2(g2p_t p) {
   const g2p_t t2 = proj_neg(proj_mul_xabs(g2_add(t1, u)));  // [x]([x]P + psi(P))
   return g2_add(c, t2);
 }
+// The same sum for a per-set kernel with one parked point (get/put: a per-lane LDS slot
+// holding P on entry) and one point parked in the caller's global slot (cput/cget): the [x]
+// chains run with their base in LDS and only the accumulator in registers, and no step in
+// between holds more than two points.
+template <class G, class P, class CP, class CG>
+LSG_INL g2p_t clear_cofactor_g2_parked(const G& get, const P& put, const CP& cput, const CG& cget) {
+  cput(proj_neg(proj_mul_xabs_get<fp2_t>(get)));  // t1 = [x]P
+  g2p_t c;
+  {
+    const g2p_t p = get();
+    c = g2_add(g2_psi2(g2_dbl(p)), proj_neg(p));
+    put(g2_psi(p));  // u = psi(P)
+  }
+  c = g2_add(c, proj_neg(get()));
+  const g2p_t t1 = cget();
+  cput(g2_add(c, proj_neg(t1)));  // c = psi^2(2P) - P - psi(P) - [x]P
+  put(g2_add(t1, get()));         // [x]P + psi(P)
+  const g2p_t t2 = proj_neg(proj_mul_xabs_get<fp2_t>(get));  // [x]([x]P + psi(P))
+  return g2_add(cget(), t2);
+}

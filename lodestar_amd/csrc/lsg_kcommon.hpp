@@ -39,6 +39,28 @@ static_assert(ML_STEPS == lsgl::ML_STEPS, "layout: Miller steps");
 #define LSG_KERNEL_ATTR_W(w) __launch_bounds__(LSG_TPB) __attribute__((amdgpu_waves_per_eu(w)))
 #define LSG_ITEMS_PER_BLOCK (LSG_TPB / LSG_GROUP)
 
+// A value parked in LDS for the thread's own use: word k of thread t at l[k * LSG_TPB + t]
+// (consecutive lanes, consecutive banks).  Long-lived points of the per-set kernels wait here
+// across the leaf calls instead of spilling to scratch.
+template <class T>
+static __device__ __forceinline__ void lds_park(uint32_t* l, const T& v) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < W; k++) l[k * LSG_TPB + threadIdx.x] = w[k];
+}
+template <class T>
+static __device__ __forceinline__ T lds_unpark(const uint32_t* l) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = l[k * LSG_TPB + threadIdx.x];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 #define LANE_ITEM(n)                        \
   lsg_lane_setup();                         \
