@@ -304,7 +304,7 @@ struct Slot {
   // per-set state
   DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_rs2, d_fall,
       d_fall2;
-  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Q, d_Hp, d_zN, d_zNi;
+  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi;
   DevBuf binv_lv[2], binv_iv[2];
   DevBuf d_lines;
   bool rs2_ready = false;
@@ -549,7 +549,7 @@ void slot_destroy(Slot* s) {
                     &s->d_rnd,  &s->d_mode,   &s->d_dst,  &s->d_ub,     &s->d_sigaff, &s->d_siginf, &s->d_seterr,
                     &s->d_pkp,  &s->d_pkerr,  &s->d_agg,  &s->d_P,      &s->d_pinf,   &s->d_H,     &s->d_hinf,
                     &s->d_rs,   &s->d_rs2,    &s->d_fall, &s->d_fall2,  &s->d_Pp,     &s->d_zP,    &s->d_zPi,
-                    &s->d_U,    &s->d_nrm,    &s->d_nrmi, &s->d_Q, &s->d_Hp,     &s->d_zN,     &s->d_zNi,   &s->binv_lv[0],
+                    &s->d_U,    &s->d_nrm,    &s->d_nrmi, &s->d_Hp,     &s->d_zN,     &s->d_zNi,   &s->binv_lv[0],
                     &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
                     &s->d_nodeF, &s->d_nodeV, &s->d_plan};
@@ -698,7 +698,6 @@ int size_state(Slot* s, size_t n, size_t np, size_t ng, size_t n_msm, int pkg = 
              {&s->d_U, 4 * W_H2CU * nn},
              {&s->d_nrm, 4 * W_FP * 2 * nn},
              {&s->d_nrmi, 4 * W_FP * 2 * nn},
-             {&s->d_Q, 4 * W_G2P * 2 * nn},
              {&s->d_Hp, 4 * W_G2P * nn},
              {&s->d_zN, 4 * W_FP * nn},
              {&s->d_zNi, 4 * W_FP * nn},
@@ -836,14 +835,13 @@ size_t slp_items_max() {
 int launch_hash(Slot* s, int n) {
   KL(s, "k_h2c_prep", lsgk::h2c_prep(S_(s), n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrm)));
   LSG_RC(batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)));
-  KL(s, "k_h2c_map", lsgk::h2c_map(S_(s), n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Q)));
+  KL(s, "k_h2c_map", lsgk::h2c_map(S_(s), n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp)));
   if ((size_t)n <= slp_items_max()) {  // small packages: clearing + affine as one program per set
-    KL(s, "k_h2c_add", lsgk::h2c_add(S_(s), n, P_<uint32_t>(s->d_Q), P_<uint32_t>(s->d_Hp)));
     KL(s, "k_slp_h2c", lsg_slp_h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
     return LSG_OK;
   }
-  KL(s, "k_h2c_clear", lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Q), P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN),
-                                       P_<uint8_t>(s->d_hinf)));
+  KL(s, "k_h2c_clear",
+     lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf)));
   LSG_RC(batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)));
   KL(s, "k_h2c_affine", lsgk::h2c_affine(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi),
                                          P_<uint8_t>(s->d_hinf), P_<uint32_t>(s->d_H)));

@@ -5,8 +5,8 @@
 //
 //   k_expand_msg   expand_message_xmd(msg_i, DST, 256), one thread per set (SHA-256)
 //   k_h2c_prep     hash_to_field -> u0, u1; norms N(tv1(u0)), N(tv1(u1)) for one batched inversion
-//   k_h2c_map      SSWU (shared-norm square root) -> 3-isogeny, one per field element
-//   k_h2c_clear    Q0 + Q1, clear_cofactor (psi form); N(Z) for the second batched inversion
+//   k_h2c_map      SSWU (shared-norm square root) -> 3-isogeny, one per field element; Q0 + Q1
+//   k_h2c_clear    clear_cofactor (psi form); N(Z) for the second batched inversion
 //   k_h2c_affine   (X, Y) * conj(Z) / N(Z)
 #include "lsg_kcommon.hpp"
 
@@ -55,23 +55,38 @@ __global__ void LSG_KERNEL_ATTR k_h2c_prep(int n, const uint8_t* __restrict__ ub
 }
 
 // stage 2: SSWU -> 3-isogeny for one field element per item (2n items: u0 and u1 of set i
-// are items 2i, 2i + 1), projective Q_j.  One map per item holds no second point while the
-// other is computed (both in one item spilled 1.2 KB per lane).
+// are items 2i, 2i + 1, adjacent lane pairs of one quad), then P_i = Q_2i + Q_2i+1 by the even
+// item with its neighbour's point moved over by a DPP quad permutation.  One map per item
+// holds no second point while the other is computed (both in one item spilled 1.2 KB per
+// lane).
+template <class T>
+LSG_DEVI T quad_swap_pairs(const T& v) {  // lanes 4i, 4i + 1 <-> 4i + 2, 4i + 3
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = pdpp<0x4E>(w[k]);  // quad_perm [2, 3, 0, 1]
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
 __global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_map(int n2, const uint32_t* __restrict__ U, const uint32_t* __restrict__ ninv,
-                                          uint32_t* __restrict__ Q) {
-  LANE_ITEM(n2);
+                                          uint32_t* __restrict__ Hp) {
+  LANE_ITEM(n2);  // n2 is even: both items of a set are live or neither is
   (void)lead;
-  lane_store(Q, item, iso_map3(map_to_curve_sswu_ni(lane_load<fp2_t>(U, item), lane_load<fp_t>(ninv, item))));
+  const g2p_t q = iso_map3(map_to_curve_sswu_ni(lane_load<fp2_t>(U, item), lane_load<fp_t>(ninv, item)));
+  const g2p_t o = quad_swap_pairs(q);
+  if ((item & 1) == 0) lane_store(Hp, item >> 1, g2_add(q, o));
 }
 
-// stage 2b: P = Q_2i + Q_2i+1, clear_cofactor; zN_i = N(Z) (0 at infinity) for the batched
-// inversion.  The [x] chains take their base point from an LDS slot per lane and the partial
-// sum waits in the item's output slot, so the chains hold only their accumulator.
-__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, const uint32_t* __restrict__ Q, uint32_t* __restrict__ Hp,
-                                            uint32_t* __restrict__ zN, uint8_t* __restrict__ hinf) {
+// stage 2b: clear_cofactor in place; zN_i = N(Z) (0 at infinity) for the batched inversion.
+// The [x] chains take their base point from an LDS slot per lane and the partial sum waits in
+// the item's own slot of Hp, so the chains hold only their accumulator.
+__global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, uint32_t* __restrict__ Hp, uint32_t* __restrict__ zN,
+                                            uint8_t* __restrict__ hinf) {
   __shared__ uint32_t park[sizeof(g2p_t) / 4 * LSG_TPB];
   LANE_ITEM(n);
-  lds_park(park, g2_add(lane_load<g2p_t>(Q, 2 * item), lane_load<g2p_t>(Q, 2 * item + 1)));
+  lds_park(park, lane_load<g2p_t>(Hp, item));
   g2p_t q = clear_cofactor_g2_parked([&]() { return lds_unpark<g2p_t>(park); },
                                      [&](const g2p_t& v) { lds_park(park, v); },
                                      [&](const g2p_t& v) { lane_store(Hp, item, v); },
@@ -80,13 +95,6 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, const uint32
   lane_store(Hp, item, q);
   lane_store(zN, item, is_inf ? fp_zero() : fp2_norm(q.Z));
   if (lead) hinf[item] = is_inf ? 1 : 0;
-}
-
-// P = Q_2i + Q_2i+1 only (packages whose clearing runs as a straight-line program)
-__global__ void LSG_KERNEL_ATTR k_h2c_add(int n, const uint32_t* __restrict__ Q, uint32_t* __restrict__ Hp) {
-  LANE_ITEM(n);
-  (void)lead;
-  lane_store(Hp, item, g2_add(lane_load<g2p_t>(Q, 2 * item), lane_load<g2p_t>(Q, 2 * item + 1)));
 }
 
 // stage 3: H affine = (X, Y) * conj(Z) / N(Z)   (= proj_to_aff, 1/Z = conj(Z) / N(Z))
@@ -193,14 +201,11 @@ hipError_t expand_msg(hipStream_t st, int n, const uint8_t* msg, const uint32_t*
 hipError_t h2c_prep(hipStream_t st, int n, const uint8_t* ub, uint32_t* U, uint32_t* norms) {
   LSG_LAUNCH_ITEMS(k_h2c_prep, n, st, n, ub, U, norms);
 }
-hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* ninv, uint32_t* Q) {
-  LSG_LAUNCH_ITEMS(k_h2c_map, 2 * n, st, 2 * n, U, ninv, Q);
+hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* ninv, uint32_t* Hp) {
+  LSG_LAUNCH_ITEMS(k_h2c_map, 2 * n, st, 2 * n, U, ninv, Hp);
 }
-hipError_t h2c_clear(hipStream_t st, int n, const uint32_t* Q, uint32_t* Hp, uint32_t* zN, uint8_t* hinf) {
-  LSG_LAUNCH_ITEMS(k_h2c_clear, n, st, n, Q, Hp, zN, hinf);
-}
-hipError_t h2c_add(hipStream_t st, int n, const uint32_t* Q, uint32_t* Hp) {
-  LSG_LAUNCH_ITEMS(k_h2c_add, n, st, n, Q, Hp);
+hipError_t h2c_clear(hipStream_t st, int n, uint32_t* Hp, uint32_t* zN, uint8_t* hinf) {
+  LSG_LAUNCH_ITEMS(k_h2c_clear, n, st, n, Hp, zN, hinf);
 }
 hipError_t h2c_affine(hipStream_t st, int n, const uint32_t* Hp, const uint32_t* ninv, const uint8_t* hinf,
                       uint32_t* H) {
