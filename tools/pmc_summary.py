@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kname(s):
+    s = s.replace("(anonymous namespace)::", "")
     return re.split(r"[(]", s)[0].replace("void ", "").strip()
 
 
