@@ -23,6 +23,10 @@ Workloads:
   adversarial  config E: the jobs workload with 1% of the sets corrupted over the five kinds
                (wrong message, flipped x bit, truncated, non-subgroup point, infinity); every
                verdict is checked against its expected value
+  committees   config D mainnet-shaped: the jobs package with the messages a slot's attesters
+               actually sign -- 64 distinct AttestationData (one per committee of 512, before
+               EIP-7549 moved the committee index out of it), arrivals interleaved over the
+               committees; every set has its own key (no duplicate sets)
 Keys: interop keys sk_{v mod 1024} (state-transition/src/util/interop.ts:19-22); messages
 sha256(b"lodestar-mi355x" || workload || i); signatures made on the GPU before timing.
 
@@ -71,18 +75,23 @@ class Workload:
         pks = ctx.sk_to_pk(sks)
         self.packages = []
         tag = name.encode()
-        if name in ("jobs", "adversarial", "gossip", "single"):
+        self.msgs_per_set = 1.0
+        if name in ("jobs", "adversarial", "gossip", "single", "committees"):
             n = 128 if name == "gossip" else (1 if name == "single" else sets_per_step)
             for p in range(n_packages):
                 base = (rank * n_packages + p) * n
-                msgs = [msg(tag, base + i) for i in range(n)]
+                if name == "committees":  # set i: key i mod 1024, committee (i + i // 1024) mod 64
+                    msgs = [msg(tag, (rank * n_packages + p) * 64 + (i + i // N_KEYS) % 64) for i in range(n)]
+                    self.msgs_per_set = min(64, n) / n
+                else:
+                    msgs = [msg(tag, base + i) for i in range(n)]
                 sigs = ctx.sign([sks[(base + i) % N_KEYS] for i in range(n)], msgs)
                 sets = [([pks[(base + i) % N_KEYS]], msgs[i], sigs[i]) for i in range(n)]
                 if name == "gossip":
                     self.packages.append(([(sets, 1)], None))
                 elif name == "single":  # verifyOnMainThread / BlsSingleThreadVerifier: one set, one verify
                     self.packages.append(([(sets, 0)], None))
-                elif name == "jobs":
+                elif name in ("jobs", "committees"):
                     self.packages.append(([([s], 1) for s in sets], None))
                 else:
                     self.packages.append(self._corrupt(ctx, sets, seed=base))
@@ -320,7 +329,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30, help="timed packages per GPU")
     ap.add_argument("--warmup", type=int, default=5, help="untimed packages per GPU (at least --depth are run)")
-    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node", "single"], default="jobs")
+    ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node", "single", "committees"],
+                    default="jobs")
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
@@ -343,7 +353,8 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 64, "single": 1}[args.workload]
+        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 64, "single": 1,
+                      "committees": 6}[args.workload]
     if args.coalesce is None:
         args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
@@ -546,7 +557,8 @@ def main():
     # whole-path work per set: the per-set stages with the bucket-MSM signature sum (groups of
     # >= 256 sets) plus the package group's share of its per-group stages, plus one G1
     # addition per extra signer of an aggregate set
-    group = n_sets if args.workload in ("jobs", "adversarial") else (128 if args.workload in ("block", "gossip") else 1)
+    group = n_sets if args.workload in ("jobs", "adversarial", "committees") else \
+        (128 if args.workload in ("block", "gossip") else 1)
     if group >= 256:
         per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / group
     else:
@@ -556,11 +568,12 @@ def main():
     per_set_muls += (sf["miller_fused_per_set"] if fused else sf["miller_lines"] + sf[accum_key]) \
         - sf["miller_multi2_per_set"]
     per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
+    per_set_muls -= (1.0 - wl.msgs_per_set) * sf["hash_map"]  # hash_to_G2 once per distinct message
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            if args.workload in ("jobs", "adversarial", "gossip", "single"):
+            if args.workload in ("jobs", "adversarial", "gossip", "single", "committees"):
                 sets = [s for job, _ in wl.packages[0][0] for s in job]
                 if args.workload == "adversarial":
                     sets = [s for (job, _), e in zip(wl.packages[0][0], wl.packages[0][1]) if e == (1, 0) for s in job]
@@ -582,6 +595,9 @@ def main():
             "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
             "single": "one set per call (verifyOnMainThread / BlsSingleThreadVerifier, maybeBatch.ts:34-38 verify): "
                       "latency of a lone verification",
+            "committees": "firehose, mainnet-shaped messages (SURVEY 8d config D): one slot of unaggregated "
+                          "attestations per GPU signing 64 distinct AttestationData (committees of 512, interleaved), "
+                          "one batchable job per set, hash_to_G2 once per distinct message",
         }[args.workload]
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "sets/s", "n_gpus": world * n_dev, "steps": args.steps,

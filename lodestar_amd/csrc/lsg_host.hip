@@ -299,12 +299,18 @@ struct Slot {
   size_t n_sets = 0, n_pks = 0;
   std::vector<uint32_t> pk_cnt, pk_first;
   std::vector<uint64_t> rnd;
+  // distinct messages of the staged package: set i hashes message msg_id[i] (n_msgs of them);
+  // msg_dedup when some sets share one (a committee's attestations sign one AttestationData)
+  size_t n_msgs = 0;
+  bool msg_dedup = false;
+  std::vector<uint32_t> mtab, mfirst;
+  std::vector<uint64_t> mkey;
   bool single_keys = false;  // every set has exactly one key (key i is set i's)
   uint32_t pk_stride = 96;   // bytes per key slot in d_pk: 4 when every key is a table index
   // per-set state
   DevBuf d_ub, d_sigaff, d_siginf, d_seterr, d_pkp, d_pkerr, d_agg, d_P, d_pinf, d_H, d_hinf, d_rs, d_rs2, d_fall,
       d_fall2;
-  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi;
+  DevBuf d_Pp, d_zP, d_zPi, d_U, d_nrm, d_nrmi, d_Hp, d_zN, d_zNi, d_mid, d_Hm, d_hinfm;
   DevBuf binv_lv[2], binv_iv[2];
   DevBuf d_lines;
   bool rs2_ready = false;
@@ -552,7 +558,7 @@ void slot_destroy(Slot* s) {
                     &s->d_U,    &s->d_nrm,    &s->d_nrmi, &s->d_Hp,     &s->d_zN,     &s->d_zNi,   &s->binv_lv[0],
                     &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
-                    &s->d_nodeF, &s->d_nodeV, &s->d_plan};
+                    &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm};
   for (DevBuf* b : bufs) free_dev(*b);
   for (auto& u : s->seg_tmp)
     for (DevBuf& b : u) free_dev(b);
@@ -656,7 +662,7 @@ size_t binv_iv_words(size_t n) {
 int size_inputs(Slot* s, size_t n, size_t np, size_t mb) {
   const size_t nn = std::max(n, (size_t)1), pp = std::max(np, (size_t)1);
   auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
-  const size_t arena = al(192 * nn) + al(4 * nn) * 3 + al(4 * pp) + al(8 * nn) + al(96 * pp) + al(std::max(mb, (size_t)1)) + nn;
+  const size_t arena = al(192 * nn) + al(4 * nn) * 4 + al(4 * pp) + al(8 * nn) + al(96 * pp) + al(std::max(mb, (size_t)1)) + nn;
   LSG_RC(ensure_host(s, s->h_arena, arena));
   LSG_RC(ensure(s, s->d_sig, 192 * nn));
   LSG_RC(ensure(s, s->d_siglen, 4 * nn));
@@ -667,6 +673,7 @@ int size_inputs(Slot* s, size_t n, size_t np, size_t mb) {
   LSG_RC(ensure(s, s->d_pklen, 4 * pp));
   LSG_RC(ensure(s, s->d_rnd, 8 * nn));
   LSG_RC(ensure(s, s->d_mode, nn));
+  LSG_RC(ensure(s, s->d_mid, 4 * nn));
   return LSG_OK;
 }
 
@@ -831,27 +838,39 @@ size_t slp_items_max() {
   return lsg_serial_mode() == LSG_SERIAL_SLP ? v : 0;
 }
 
-// hash_to_G2 of the slot's n expanded messages (d_ub) into d_H / d_hinf on the current stream
-int launch_hash(Slot* s, int n) {
+// hash_to_G2 of the slot's n expanded messages (d_ub) into H / hinf on the current stream
+int launch_hash(Slot* s, int n, uint32_t* H, uint8_t* hinf) {
   KL(s, "k_h2c_prep", lsgk::h2c_prep(S_(s), n, P_<uint8_t>(s->d_ub), P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrm)));
   LSG_RC(batch_inv(s, 0, "binv_sswu", P_<uint32_t>(s->d_nrm), 2 * (size_t)n, P_<uint32_t>(s->d_nrmi)));
   KL(s, "k_h2c_map", lsgk::h2c_map(S_(s), n, P_<uint32_t>(s->d_U), P_<uint32_t>(s->d_nrmi), P_<uint32_t>(s->d_Hp)));
   if ((size_t)n <= slp_items_max()) {  // small packages: clearing + affine as one program per set
-    KL(s, "k_slp_h2c", lsg_slp_h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
+    KL(s, "k_slp_h2c", lsg_slp_h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), H, hinf));
     return LSG_OK;
   }
-  KL(s, "k_h2c_clear",
-     lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), P_<uint8_t>(s->d_hinf)));
+  KL(s, "k_h2c_clear", lsgk::h2c_clear(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zN), hinf));
   LSG_RC(batch_inv(s, 0, "binv_hash", P_<uint32_t>(s->d_zN), (size_t)n, P_<uint32_t>(s->d_zNi)));
-  KL(s, "k_h2c_affine", lsgk::h2c_affine(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi),
-                                         P_<uint8_t>(s->d_hinf), P_<uint32_t>(s->d_H)));
+  KL(s, "k_h2c_affine", lsgk::h2c_affine(S_(s), n, P_<uint32_t>(s->d_Hp), P_<uint32_t>(s->d_zNi), hinf, H));
   return LSG_OK;
 }
 
 // ---- staging: the package's sets into the slot's pinned arena (order given by `order`),
 // randomizers drawn here (seed == 0: OS CSPRNG; else deterministic, for tests)
+// 64-bit mix of a message (its length and 8-byte words; signing roots are SHA-256 outputs)
+static uint64_t msg_key(const uint8_t* m, uint32_t len) {
+  uint64_t h = 0x9e3779b97f4a7c15ull ^ len;
+  uint32_t k = 0;
+  for (; k + 8 <= len; k += 8) {
+    uint64_t w;
+    memcpy(&w, m + k, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  for (; k < len; k++) h = (h ^ m[k]) * 0x100000001b3ull;
+  return h ^ (h >> 29);
+}
+
 int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, bool scale,
-               const std::vector<uint8_t>* noscale = nullptr) {
+               const std::vector<uint8_t>* noscale = nullptr, bool dedup = false) {
   size_t npk = 0, msg_total = 0;
   bool all_index = true;  // every key names a table row: 4-byte key slots (a block body's
                           // ~3.7M signers cross PCIe as 15 MB instead of 355 MB)
@@ -868,12 +887,13 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   const size_t nn = std::max(n, (size_t)1), np = std::max(npk, (size_t)1);
   auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
   const size_t o_sig = 0, o_siglen = al(o_sig + 192 * nn), o_msgoff = al(o_siglen + 4 * nn),
-               o_msglen = al(o_msgoff + 4 * nn), o_pklen = al(o_msglen + 4 * nn), o_rnd = al(o_pklen + 4 * np),
-               o_pk = al(o_rnd + 8 * nn), o_msg = al(o_pk + ks * np);
+               o_msglen = al(o_msgoff + 4 * nn), o_mid = al(o_msglen + 4 * nn), o_pklen = al(o_mid + 4 * nn),
+               o_rnd = al(o_pklen + 4 * np), o_pk = al(o_rnd + 8 * nn), o_msg = al(o_pk + ks * np);
   uint8_t* A = H_<uint8_t>(s->h_arena);
   uint32_t* siglen = (uint32_t*)(A + o_siglen);
   uint32_t* msgoff = (uint32_t*)(A + o_msgoff);
   uint32_t* msglen = (uint32_t*)(A + o_msglen);
+  uint32_t* mid = (uint32_t*)(A + o_mid);
   uint32_t* pklen = (uint32_t*)(A + o_pklen);
   uint64_t* rnd = (uint64_t*)(A + o_rnd);
   siglen[0] = msgoff[0] = msglen[0] = pklen[0] = 0;
@@ -881,8 +901,43 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   s->pk_cnt.resize(n);
   s->pk_first.resize(n);
   s->rnd.resize(n);
-  size_t mo = 0, po = 0;
+  size_t mo = 0, po = 0, nm = 0;
   bool single = npk == n;
+  // open-addressing table over the messages: slot -> distinct message id (mfirst: its set),
+  // with the message's 64-bit key beside it so that a probe compares bytes only on a key match
+  size_t cap = 0;
+  static const bool dedup_on = [] {
+    const char* e = getenv("LSG_MSG_DEDUP");
+    return !(e && e[0] == '0');
+  }();
+  // a package whose sample of 256 evenly spaced sets shows no repeated message is taken as all
+  // distinct and staged without the table (the firehose of distinct gossip messages pays ~5 us,
+  // not the table's ~1 ms under the context lock); committee-shaped packages repeat at once
+  auto sample_repeats = [&]() {
+    const size_t k = std::min(n, (size_t)256), step = n / k;
+    uint64_t seen[512];
+    bool used[512] = {false};
+    for (size_t j = 0; j < k; j++) {
+      const lsg_set* q = sets[j * step];
+      const uint64_t key = msg_key(q->msg, q->msg_len);
+      for (size_t h = (size_t)key & 511;; h = (h + 1) & 511) {
+        if (!used[h]) {
+          used[h] = true;
+          seen[h] = key;
+          break;
+        }
+        if (seen[h] == key) return true;
+      }
+    }
+    return false;
+  };
+  if (dedup && dedup_on && n > 1 && sample_repeats()) {
+    cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    s->mtab.assign(cap, UINT32_MAX);
+    s->mkey.resize(cap);
+    s->mfirst.resize(n);
+  }
   for (size_t i = 0; i < n; i++) {
     const lsg_set* q = sets[i];
     siglen[i] = q->sig_len;
@@ -891,10 +946,33 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
       memcpy(sg, q->sig, q->sig_len);
     else
       memset(sg, 0, 96);
-    msgoff[i] = (uint32_t)mo;
-    msglen[i] = q->msg_len;
-    if (q->msg_len) memcpy(A + o_msg + mo, q->msg, q->msg_len);
-    mo += q->msg_len;
+    uint32_t id = (uint32_t)nm;
+    if (cap) {
+      const uint64_t key = msg_key(q->msg, q->msg_len);
+      for (size_t h = (size_t)key & (cap - 1);; h = (h + 1) & (cap - 1)) {
+        const uint32_t e = s->mtab[h];
+        if (e == UINT32_MAX) {
+          s->mtab[h] = id;
+          s->mkey[h] = key;
+          s->mfirst[id] = (uint32_t)i;
+          break;
+        }
+        if (s->mkey[h] != key) continue;
+        const lsg_set* r = sets[s->mfirst[e]];
+        if (r->msg_len == q->msg_len && (q->msg_len == 0 || memcmp(r->msg, q->msg, q->msg_len) == 0)) {
+          id = e;
+          break;
+        }
+      }
+    }
+    mid[i] = id;
+    if (id == nm) {  // a new message: staged once
+      msgoff[nm] = (uint32_t)mo;
+      msglen[nm] = q->msg_len;
+      if (q->msg_len) memcpy(A + o_msg + mo, q->msg, q->msg_len);
+      mo += q->msg_len;
+      nm++;
+    }
     s->pk_cnt[i] = q->n_pks;
     s->pk_first[i] = (uint32_t)po;
     if (q->n_pks != 1) single = false;
@@ -918,6 +996,8 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
     }
   }
   s->single_keys = single && n > 0;
+  s->n_msgs = nm;
+  s->msg_dedup = nm < n;
   if (scale && n) {
     if (seed == 0) {
       if (!os_random(rnd, 8 * n)) {
@@ -956,6 +1036,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
             {&s->d_msgoff, o_msgoff, 4 * nn}, {&s->d_msglen, o_msglen, 4 * nn}, {&s->d_pk, o_pk, ks * np},
             {&s->d_pklen, o_pklen, 4 * np},   {&s->d_rnd, o_rnd, 8 * nn}};
   for (auto& x : cp) LSG_HIP(s, hipMemcpyAsync(x.d->p, A + x.off, x.len, hipMemcpyHostToDevice, S));
+  if (s->msg_dedup) LSG_HIP(s, hipMemcpyAsync(s->d_mid.p, A + o_mid, 4 * n, hipMemcpyHostToDevice, S));
   return LSG_OK;
 }
 
@@ -1193,10 +1274,20 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item
                                                P_<int32_t>(s->d_seterr)));
   LSG_HIP(s, hipEventRecord(s->ev_sig, s->st[1]));
   s->cur = 0;
-  KL(s, "k_expand_msg", lsgk::expand_msg(S_(s), n, P_<uint8_t>(s->d_msg), P_<uint32_t>(s->d_msgoff),
+  // hash_to_G2 once per distinct message, then each set's point gathered from its message's
+  const int nm = (int)s->n_msgs;
+  KL(s, "k_expand_msg", lsgk::expand_msg(S_(s), nm, P_<uint8_t>(s->d_msg), P_<uint32_t>(s->d_msgoff),
                                          P_<uint32_t>(s->d_msglen), P_<uint8_t>(s->d_dst), DST_POP_LEN,
                                          P_<uint8_t>(s->d_ub)));
-  LSG_RC(launch_hash(s, n));
+  if (s->msg_dedup) {
+    LSG_RC(ensure(s, s->d_Hm, 4 * W_G2A * (size_t)nm));
+    LSG_RC(ensure(s, s->d_hinfm, (size_t)nm));
+    LSG_RC(launch_hash(s, nm, P_<uint32_t>(s->d_Hm), P_<uint8_t>(s->d_hinfm)));
+    KL(s, "k_h2c_gather", lsgk::h2c_gather(S_(s), n, P_<uint32_t>(s->d_mid), P_<uint32_t>(s->d_Hm),
+                                           P_<uint8_t>(s->d_hinfm), P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
+  } else {
+    LSG_RC(launch_hash(s, n, P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
+  }
   if (!miller_fused())
     KL(s, "k_miller_lines", lsgk::miller_lines(S_(s), n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
@@ -1379,7 +1470,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   }
   for (size_t k : nonb)
     if (s->jobs[k].count == 1) noscale[s->jobs[k].first] = 1;
-  LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true, &noscale));
+  LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true, &noscale, true));
   // phase-A groups, MSM groups first: the package group, then one per non-batchable job
   PhasePlan& A = s->phA;
   A = PhasePlan();
@@ -2263,7 +2354,7 @@ int util_hash(Slot* s, const uint8_t* msgs, uint32_t msg_len, size_t n, const ui
   const int nn = (int)n;
   KL(s, "k_expand_msg", lsgk::expand_msg(S_(s), nn, P_<uint8_t>(s->d_msg), P_<uint32_t>(s->d_msgoff),
                                          P_<uint32_t>(s->d_msglen), P_<uint8_t>(s->d_dst), dst_len, P_<uint8_t>(s->d_ub)));
-  LSG_RC(launch_hash(s, nn));
+  LSG_RC(launch_hash(s, nn, P_<uint32_t>(s->d_H), P_<uint8_t>(s->d_hinf)));
   // the utility slot's DST is restored for the next caller
   LSG_HIP(s, hipMemcpyAsync(s->d_dst.p, DST_POP, DST_POP_LEN, hipMemcpyHostToDevice, s->st[0]));
   return LSG_OK;

@@ -97,6 +97,17 @@ __global__ void LSG_KERNEL_ATTR_W(LSG_H2C_WAVES) k_h2c_clear(int n, uint32_t* __
   if (lead) hinf[item] = is_inf ? 1 : 0;
 }
 
+// each set's hashed point from its message's (packages whose sets share messages hash every
+// distinct message once)
+__global__ void LSG_KERNEL_ATTR k_h2c_gather(int n, const uint32_t* __restrict__ mid, const uint32_t* __restrict__ Hm,
+                                             const uint8_t* __restrict__ hinfm, uint32_t* __restrict__ H,
+                                             uint8_t* __restrict__ hinf) {
+  LANE_ITEM(n);
+  const uint32_t m = mid[item];
+  lane_store(H, item, lane_load<g2a_t>(Hm, m));
+  if (lead) hinf[item] = hinfm[m];
+}
+
 // stage 3: H affine = (X, Y) * conj(Z) / N(Z)   (= proj_to_aff, 1/Z = conj(Z) / N(Z))
 __global__ void LSG_KERNEL_ATTR k_h2c_affine(int n, const uint32_t* __restrict__ Hp, const uint32_t* __restrict__ ninv,
                                              const uint8_t* __restrict__ hinf, uint32_t* __restrict__ H) {
@@ -206,6 +217,10 @@ hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* nin
 }
 hipError_t h2c_clear(hipStream_t st, int n, uint32_t* Hp, uint32_t* zN, uint8_t* hinf) {
   LSG_LAUNCH_ITEMS(k_h2c_clear, n, st, n, Hp, zN, hinf);
+}
+hipError_t h2c_gather(hipStream_t st, int n, const uint32_t* mid, const uint32_t* Hm, const uint8_t* hinfm, uint32_t* H,
+                      uint8_t* hinf) {
+  LSG_LAUNCH_ITEMS(k_h2c_gather, n, st, n, mid, Hm, hinfm, H, hinf);
 }
 hipError_t h2c_affine(hipStream_t st, int n, const uint32_t* Hp, const uint32_t* ninv, const uint8_t* hinf,
                       uint32_t* H) {

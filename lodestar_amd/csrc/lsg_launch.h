@@ -16,6 +16,8 @@ hipError_t expand_msg(hipStream_t st, int n, const uint8_t* msg, const uint32_t*
 hipError_t h2c_prep(hipStream_t st, int n, const uint8_t* ub, uint32_t* U, uint32_t* norms);
 hipError_t h2c_map(hipStream_t st, int n, const uint32_t* U, const uint32_t* ninv, uint32_t* Hp);
 hipError_t h2c_clear(hipStream_t st, int n, uint32_t* Hp, uint32_t* zN, uint8_t* hinf);
+hipError_t h2c_gather(hipStream_t st, int n, const uint32_t* mid, const uint32_t* Hm, const uint8_t* hinfm, uint32_t* H,
+                      uint8_t* hinf);
 hipError_t h2c_affine(hipStream_t st, int n, const uint32_t* Hp, const uint32_t* ninv, const uint8_t* hinf,
                       uint32_t* H);
 hipError_t signing_root(hipStream_t st, int n, const uint8_t* roots, const uint8_t* domains, uint32_t dstride,

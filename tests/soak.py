@@ -2,7 +2,9 @@
 """Verdict soak on the GPU (north_star: "zero verdict mismatches over 10^7 valid plus
 adversarially corrupted sets").  Test infrastructure (tests/).
 
-Every set is distinct: each package draws fresh messages (a global counter), signs them on the
+Every set is distinct: each package draws fresh messages (a global counter; every
+--committee-every-th package signs 64 committee messages shared by its sets, so hash_to_G2
+runs once per message), signs them on the
 GPU with the interop keys sk_{v mod 1024}, corrupts --bad-rate of them (default 1%) split
 evenly over the config E kinds, cuts them into worker jobs of mixed sizes (gossip singles,
 2-16-set batches, 128-set chunks; 90% batchable) and streams the packages through the
@@ -46,6 +48,9 @@ def main():
     ap.add_argument("--package", type=int, default=32768, help="sets per package (lsg_submit_jobs call)")
     ap.add_argument("--depth", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--committee-every", type=int, default=2,
+                    help="every K-th package signs committee messages: 64 distinct messages, set i of the "
+                         "package in committee (i + i // 1024) mod 64 (hash_to_G2 once per message); 0: never")
     args = ap.parse_args()
     rng = random.Random(args.seed)
     import numpy as np
@@ -57,14 +62,22 @@ def main():
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sig_decode.json")))
     non_subgroup = [bytes.fromhex(c["sig"]) for c in gold["cases"] if c["err"] == 3 and len(c["sig"]) == 192]
     counter = 0
+    n_pkg = 0
 
     def make_package():
         nonlocal counter
+        nonlocal n_pkg
         n = args.package
         base = counter
         counter += n
-        msgs = [hashlib.sha256(b"lodestar-mi355x" + b"soak" + (base + i).to_bytes(8, "little")).digest()
-                for i in range(n)]
+        n_pkg += 1
+        if args.committee_every and n_pkg % args.committee_every == 0:
+            # base + c: distinct from every other package's messages (bases step by n >= 64)
+            msgs = [hashlib.sha256(b"lodestar-mi355x" + b"soak" + (base + (i + i // 1024) % 64).to_bytes(8, "little"))
+                    .digest() for i in range(n)]
+        else:
+            msgs = [hashlib.sha256(b"lodestar-mi355x" + b"soak" + (base + i).to_bytes(8, "little")).digest()
+                    for i in range(n)]
         keys = [(base + i) % 1024 for i in range(n)]
         sigs = ctx.sign([sks[k] for k in keys], msgs)
         sets = [([pks[keys[i]]], msgs[i], sigs[i]) for i in range(n)]
@@ -149,7 +162,8 @@ def main():
             print(f"{done_sets} sets / {done_jobs} jobs verified, {mismatches} mismatches, {n_false} false, "
                   f"{n_err} rejected, {retries} batch retries ({el:.0f} s, generation included)", flush=True)
     el = time.time() - t_start
-    print(json.dumps({"sets": done_sets, "distinct_sets": done_sets, "jobs": done_jobs, "mismatches": mismatches,
+    print(json.dumps({"sets": done_sets, "distinct_sets": done_sets, "committee_every": args.committee_every,
+                      "jobs": done_jobs, "mismatches": mismatches,
                       "jobs_false": n_false, "jobs_rejected": n_err, "batch_retries": retries,
                       "bad_rate": args.bad_rate, "seconds_incl_generation": round(el, 1),
                       "path": "lsg_submit_jobs/lsg_wait_jobs (one RLC group per package + worker.ts fallback)",

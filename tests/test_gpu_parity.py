@@ -170,6 +170,39 @@ def test_adversarial_jobs_match_oracle(ctx):
     check_jobs(ctx, jobs, seed=99)
 
 
+def test_shared_messages_match_oracle(ctx):
+    """Sets that sign one message (a committee's attestations) share one hash_to_G2 per
+    package (stage_sets message table, k_h2c_gather): verdicts, errors and counters stay the
+    oracle's, with corrupted sets inside the shared groups and sets whose corruption gives
+    them a message of their own."""
+    import random
+    rng = random.Random(5)
+    msgs = [bd.msg("committee", c) for c in range(3)]
+    sets = []
+    for c, m in enumerate(msgs):
+        for k in range(6):
+            key = 300 + 6 * c + k
+            sets.append(([bd.pk_bytes(key)], m, g2_serialize_compressed(bd.sig_point((key,), m))))
+    jobs = [([s], 1) for s in sets]
+    check_jobs(ctx, jobs, seed=21)
+    bad = list(sets)
+    bad[1] = bd.corrupt_wrong_message(bad[1])       # leaves its group: a message of its own
+    bad[7] = bd.corrupt_infinity(bad[7])            # stays in its group
+    bad[8] = (bad[8][0], bad[8][1], bad[9][2])      # another signer's signature of the same message
+    bad[14] = bd.corrupt_not_in_group(bad[14])
+    bad[15] = bd.corrupt_truncate(bad[15])
+    jobs = [([s], 1 if rng.random() < 0.8 else 0) for s in bad]
+    jobs.append((bad[12:18], 1))                    # a multi-set job inside one shared group
+    check_jobs(ctx, jobs, seed=22)
+    assert ctx.verify_sets(sets, seed=23) == (1, 0)
+    assert ctx.verify_sets([sets[0], sets[1], bad[8]], seed=23) == (0, 0)
+
+
+def g2_serialize_compressed(pt):
+    from oracle.curves import g2_compress
+    return g2_compress(pt)
+
+
 def test_batch_partial_and_final_verify(ctx):
     sets = [bd.single_set(200 + i) for i in range(10)]
     p1, e1, a1 = ctx.batch_partial(sets[:5], seed=1)

@@ -17,11 +17,13 @@ run() {  # name seconds command...
 }
 for step in "$@"; do
   # row:<step> / pair:<step> run <step> with the row / pair serial kernels (A/B against the
-  # straight-line-program default); w4:<step> with the 4-bit-window signature scaling kernel
+  # straight-line-program default); w4:<step> with the 4-bit-window signature scaling kernel;
+  # nodedup:<step> hashing every set's message (no per-package message table)
   if [ "${step#pair:}" != "$step" ]; then export LSG_SERIAL=pair TAG=${LSG_TAG:-r03}_pair; step=${step#pair:};
   elif [ "${step#row:}" != "$step" ]; then export LSG_SERIAL=row TAG=${LSG_TAG:-r03}_row; step=${step#row:};
   elif [ "${step#w4:}" != "$step" ]; then export LSG_SIG_SCALE=4 TAG=${LSG_TAG:-r03}_w4; step=${step#w4:};
-  else unset LSG_SERIAL LSG_SIG_SCALE; TAG=${LSG_TAG:-r03}; fi
+  elif [ "${step#nodedup:}" != "$step" ]; then export LSG_MSG_DEDUP=0 TAG=${LSG_TAG:-r03}_nodedup; step=${step#nodedup:};
+  else unset LSG_SERIAL LSG_SIG_SCALE LSG_MSG_DEDUP; TAG=${LSG_TAG:-r03}; fi
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ;;
     test-*) run "pytest_${step#test-}" 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "${step#test-}" ;;
