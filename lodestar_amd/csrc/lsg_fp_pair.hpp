@@ -54,9 +54,18 @@ LSG_PFN uint32_t pdown(uint32_t x) {                           // lane 0 <- lane
   const uint32_t v = pdpp<0xF5>(x);
   return pair_h() ? 0u : v;
 }
-LSG_PFN uint32_t pup(uint32_t x) {  // lane 1 <- lane 0, lane 0 <- 0
-  const uint32_t v = pdpp<0xA0>(x);
-  return pair_h() ? v : 0u;
+LSG_PFN uint32_t pup(uint32_t x) {  // lane 1 <- lane 0, lane 0 <- 0: one v_and_b32 with a DPP source
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xf, 0xf, true) & (0u - pair_h());
+}
+// pdown(x & M29) and pbcast<0>(x) & M29 as ONE v_and_b32 each: the DPP move folds into the and
+// (GCNDPPCombine) when the mask is a register operand -- lmask = M29 on lane 0 and 0 on lane 1
+// also does pdown's zeroing of lane 1, so the retire step loses an and and a cndmask and the m
+// broadcast an and
+LSG_PFN uint32_t pdown_and(uint32_t x, uint32_t lmask) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xF5, 0xf, 0xf, true) & lmask;
+}
+LSG_PFN uint32_t pbcast0_and(uint32_t x, uint32_t m29) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xf, 0xf, true) & m29;
 }
 #else
 #define LSG_PFN LSG_INL
@@ -69,6 +78,8 @@ LSG_PFN uint32_t pbcast(uint32_t x) {
 LSG_PFN uint32_t pswap(uint32_t x) { return x; }
 LSG_PFN uint32_t pdown(uint32_t) { return 0u; }
 LSG_PFN uint32_t pup(uint32_t) { return 0u; }
+LSG_PFN uint32_t pdown_and(uint32_t, uint32_t) { return 0u; }
+LSG_PFN uint32_t pbcast0_and(uint32_t x, uint32_t m29) { return x & m29; }
 #endif
 LSG_PFN bool pair_top() { return pair_h() == (uint32_t)(LSG_GROUP - 1); }
 // this lane's k-th limb of a 14-limb literal
@@ -161,6 +172,10 @@ LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
   for (int n = 0; n < N; n++)
 #pragma unroll
     for (int j = 0; j < LSG_PL; j++) t[n][j] = 0;
+  uint32_t m29 = LSG_M29, lmask = top ? 0u : LSG_M29;
+#if LSG_PAIR_G == 2
+  asm volatile("" : "+v"(m29), "+v"(lmask));  // register operands: the DPP moves fold into the ands
+#endif
 #pragma unroll
   for (int i = 0; i < 14; i++) {
 #pragma unroll
@@ -172,7 +187,7 @@ LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
     }
 #pragma unroll
     for (int n = 0; n < N; n++) {
-      const uint32_t m = pbcast<0>(((uint32_t)t[n][0] * LSG_N0P) & LSG_M29);
+      const uint32_t m = pbcast0_and((uint32_t)t[n][0] * LSG_N0P, m29);
 #pragma unroll
       for (int j = 0; j < LSG_PL; j++) t[n][j] += (int64_t)(int32_t)m * (int32_t)p[j];
     }
@@ -181,7 +196,7 @@ LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
       // retire limb 0 (its low 29 bits are zero on lane 0): the high part carries into the
       // next accumulator of the same lane, lane 1's low 29 bits move down to lane 0's top
       const int64_t c = t[n][0] >> 29;
-      const uint32_t mv = pdown((uint32_t)t[n][0] & LSG_M29);
+      const uint32_t mv = pdown_and((uint32_t)t[n][0], lmask);
 #pragma unroll
       for (int j = 0; j < LSG_PL - 1; j++) t[n][j] = t[n][j + 1];
       t[n][0] += c;
