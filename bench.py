@@ -285,7 +285,9 @@ def run_node_workload(args):
     # at least 150 timed steps (~2.5 s): over a 30-step window (~0.6 s) the JIT, the heap
     # growth and single collections moved the rate by +-25 % between runs
     args.steps = max(args.steps, 150)
-    args.warmup = max(args.warmup, 10)
+    # 40 untimed steps: the first Node process on a fresh box ran its first ~10-20 packages
+    # 20-30 % slower (1.35-1.53M against 1.86-1.97M for a second run in the same call)
+    args.warmup = max(args.warmup, 40)
     cmd = ["node"] + args.node_flags.split() + [os.path.join(ROOT, "bench", "bench_node.js"), "--steps", str(args.steps), "--warmup",
            str(args.warmup), "--sets-per-step", str(args.sets_per_step), "--max-sigs-per-package",
            str(args.node_max_sigs), "--device", str(local), "--max-pending-sigs", str(args.node_max_pending)]

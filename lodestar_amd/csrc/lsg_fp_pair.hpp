@@ -218,19 +218,29 @@ LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
     const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
     if (!top) t[n][LSG_PL - 1] &= (int64_t)LSG_M29;
     t[n][0] += (int64_t)(((uint64_t)chi << 32) | clo);
+    // second pass: only limb 0 (lane 1's, plus lane 0's carry of < 2^35) can exceed 32 bits;
+    // limbs 1.. are < 2^29 (the top limb small and signed) and the carries from limb 1 on are
+    // a few units, so the rest runs on 32-bit words (same value, same unique limbs)
+    int32_t c = (int32_t)(t[n][0] >> 29);
+    r[n].l[0] = (uint32_t)t[n][0] & LSG_M29;
 #pragma unroll
-    for (int j = 0; j < LSG_PL - 1; j++) {
-      t[n][j + 1] += t[n][j] >> 29;
-      t[n][j] &= (int64_t)LSG_M29;
+    for (int j = 1; j < LSG_PL; j++) {
+      const int32_t v = (int32_t)(uint32_t)t[n][j] + c;
+      if (j < LSG_PL - 1) {
+        c = v >> 29;
+        r[n].l[j] = (uint32_t)v & LSG_M29;
+      } else {
+        r[n].l[j] = (uint32_t)v;
+      }
     }
   }
 #else
   (void)top;
-#endif
 #pragma unroll
   for (int n = 0; n < N; n++)
 #pragma unroll
     for (int j = 0; j < LSG_PL; j++) r[n].l[j] = (uint32_t)t[n][j];
+#endif
 }
 LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
   LSG_COUNT_MUL();
