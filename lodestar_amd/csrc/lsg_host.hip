@@ -278,6 +278,10 @@ struct PhasePlan {
   // host copy of the items (first set, set count): phase C's item-aligned job groups
   std::vector<int32_t> it_first, it_cnt;
   bool single_items = false;  // every item is one set: the list form of the Miller loop runs
+  // one Miller pair per distinct message for group agg_g (>= 0): its items are the n_magg
+  // message items (plan arena at magg_off) after the n_set_items per-set items
+  int agg_g = -1;
+  size_t n_magg = 0, magg_off = 0, n_set_items = 0;
 };
 
 struct JobRec {
@@ -305,6 +309,9 @@ struct Slot {
   bool msg_dedup = false;
   std::vector<uint32_t> mtab, mfirst;
   std::vector<uint64_t> mkey;
+  std::vector<uint32_t> msg_id;  // host copy of the set -> message map (msg_dedup)
+  SegPlan msum;                  // msg_agg: per message, the masked scaled keys of the package group
+  DevBuf d_mmask, d_PmP, d_Pm, d_pinfm, d_errm;
   bool single_keys = false;  // every set has exactly one key (key i is set i's)
   uint32_t pk_stride = 96;   // bytes per key slot in d_pk: 4 when every key is a table index
   // per-set state
@@ -558,7 +565,8 @@ void slot_destroy(Slot* s) {
                     &s->d_U,    &s->d_nrm,    &s->d_nrmi, &s->d_Hp,     &s->d_zN,     &s->d_zNi,   &s->binv_lv[0],
                     &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
-                    &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm};
+                    &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm,
+                    &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm};
   for (DevBuf* b : bufs) free_dev(*b);
   for (auto& u : s->seg_tmp)
     for (DevBuf& b : u) free_dev(b);
@@ -832,6 +840,15 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
 // Packages of up to LSG_SLP_ITEMS sets (default 2048; 0: never) run one-set Miller items as
 // straight-line programs (lsg_slp.hip, one workgroup per set, ~0.8 ms) instead of the fused
 // kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
+// one Miller pair per distinct message in the package group (LSG_MSG_AGG=1; default: per set)
+static bool msg_agg_on() {
+  static const bool on = [] {
+    const char* e = getenv("LSG_MSG_AGG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 size_t slp_items_max() {
   const char* e = getenv("LSG_SLP_ITEMS");
   const size_t v = e ? (size_t)atol(e) : (size_t)2048;
@@ -998,6 +1015,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   s->single_keys = single && n > 0;
   s->n_msgs = nm;
   s->msg_dedup = nm < n;
+  if (s->msg_dedup) s->msg_id.assign(mid, mid + n);
   if (scale && n) {
     if (seed == 0) {
       if (!os_random(rnd, 8 * n)) {
@@ -1133,7 +1151,9 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
     std::vector<std::pair<size_t, size_t>> ranges;
     std::vector<size_t> nsub(ng, 1);
     for (size_t g = 0; g < ng; g++) {
-      if (g < Ph.sub.size() && !Ph.sub[g].empty()) {
+      if ((int)g == Ph.agg_g) {  // message items instead (below)
+        nsub[g] = 0;
+      } else if (g < Ph.sub.size() && !Ph.sub[g].empty()) {
         ranges.insert(ranges.end(), Ph.sub[g].begin(), Ph.sub[g].end());
         nsub[g] = Ph.sub[g].size();
       } else {
@@ -1144,9 +1164,20 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
     Ph.n_items = plan_items(s, ranges, &Ph.item_off, nullptr, &Ph.sub_items, &Ph.it_first, &Ph.it_cnt);
     Ph.single_items = true;
     for (int32_t c : Ph.it_cnt) Ph.single_items = Ph.single_items && c == 1;
+    Ph.n_set_items = Ph.n_items;
+    if (Ph.agg_g >= 0) {  // item n_set_items + j = message j (one pair)
+      Ph.magg_off = A.size();
+      for (size_t j = 0; j < Ph.n_magg; j++) A.push_back((int32_t)j);
+      for (size_t j = 0; j < Ph.n_magg; j++) A.push_back(1);
+      Ph.n_items += Ph.n_magg;
+    }
     Ph.term_base = Ph.n_items;
     size_t r = 0;
     for (size_t g = 0; g < ng; g++) {
+      if ((int)g == Ph.agg_g) {
+        gi.push_back({(int32_t)Ph.n_set_items, (int32_t)Ph.n_items});
+        continue;
+      }
       gi.push_back({Ph.sub_items[r].first, Ph.sub_items[r + nsub[g] - 1].second});
       r += nsub[g];
     }
@@ -1245,7 +1276,8 @@ int launch_fe(Slot* s, size_t ng) {
 // Per-set stages of the slot's package (no host synchronisation):
 //   side: pubkeys -> aggregation -> [r_i] scaling -> signature decode -> subgroup check (ev_sig)
 //   main: expand_message -> hash_to_G2 [-> lines] -> wait ev_sig -> Miller items f (fall)
-int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item_off, uint32_t* fall) {
+int launch_set_stages(Slot* s, const SegPlan* pkagg, const PhasePlan& Ph, uint32_t* fall) {
+  const size_t n_items = Ph.agg_g >= 0 ? Ph.n_set_items : Ph.n_items, item_off = Ph.item_off;
   const int n = (int)s->n_sets, np = (int)s->n_pks;
   if (n == 0) return LSG_OK;
   Dev* d = s->d;
@@ -1272,6 +1304,21 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item
   else
     KL(s, "k_sig_subgroup", lsgk::sig_subgroup(S_(s), n, P_<uint32_t>(s->d_sigaff), P_<uint8_t>(s->d_siginf),
                                                P_<int32_t>(s->d_seterr)));
+  if (Ph.agg_g >= 0) {  // per message: sum of the package group's usable r_i pk_i, affine
+    const Grp& g = Ph.groups[(size_t)Ph.agg_g];
+    const size_t nm = Ph.n_magg;
+    LSG_RC(ensure(s, s->d_mmask, 4 * W_G1P * std::max(g.first + g.len, (size_t)1)));
+    LSG_RC(ensure(s, s->d_PmP, 4 * W_G1P * nm));
+    LSG_RC(ensure(s, s->d_Pm, 4 * W_G1A * nm));
+    LSG_RC(ensure(s, s->d_pinfm, nm));
+    LSG_RC(ensure(s, s->d_errm, 4 * nm));
+    KL(s, "k_pk_mask", lsgk::pk_mask(S_(s), (int)(g.first + g.len), P_<uint32_t>(s->d_Pp), P_<int32_t>(s->d_seterr),
+                                     P_<uint8_t>(s->d_pinf), P_<uint32_t>(s->d_mmask)));
+    LSG_RC(run_seg(s, 0, "msg_pk_sums", s->msum, P_<uint32_t>(s->d_mmask), P_<uint32_t>(s->d_PmP)));
+    KL(s, "k_g1p_affine_inv", lsgk::g1p_affine_inv(S_(s), (int)nm, P_<uint32_t>(s->d_PmP), P_<uint32_t>(s->d_Pm),
+                                                   P_<uint8_t>(s->d_pinfm)));
+    LSG_HIP(s, hipMemsetAsync(s->d_errm.p, 0, 4 * nm, s->st[1]));
+  }
   LSG_HIP(s, hipEventRecord(s->ev_sig, s->st[1]));
   s->cur = 0;
   // hash_to_G2 once per distinct message, then each set's point gathered from its message's
@@ -1292,6 +1339,11 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, size_t n_items, size_t item
     KL(s, "k_miller_lines", lsgk::miller_lines(S_(s), n, P_<uint32_t>(s->d_H), P_<uint32_t>(s->d_lines)));
   LSG_HIP(s, hipStreamWaitEvent(s->st[0], s->ev_sig, 0));
   if (n_items) LSG_RC(launch_accum(s, n_items, item_off, fall));
+  if (Ph.agg_g >= 0)  // one pair per message: (sum of r_i pk_i, H(m)), one program each
+    KL(s, "k_slp_items_msg",
+       lsg_slp_miller_items1(S_(s), (int)Ph.n_magg, PL(s, Ph.magg_off), P_<uint32_t>(s->d_Pm), P_<uint8_t>(s->d_pinfm),
+                             P_<uint8_t>(s->d_hinfm), P_<int32_t>(s->d_errm), P_<uint32_t>(s->d_Hm),
+                             fall + (size_t)lsgl::W_F12 * Ph.n_set_items));
   return LSG_OK;
 }
 
@@ -1536,9 +1588,31 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   }
   LSG_RC(size_state(s, s->n_sets, s->n_pks, A.groups.size(), gm.size(), 1));
   if (!s->single_keys) s->pkagg = plan_pk_agg(s);
+  // sets of the package group that share a message share one Miller pair: Π e(r_i pk_i, H(m))
+  // = e(Σ r_i pk_i, H(m)) exactly.  Its per-set items are then never computed, so a failing
+  // package group's chunks (phase B) run their own items and phase C goes per job.
+  A.agg_g = -1;
+  if (s->msg_dedup && !s->chunk_mode && s->big_g >= 0 && msg_agg_on() && s->n_msgs <= (size_t)8192 &&
+      slp_items_max() > 0) {
+    const Grp& g = A.groups[(size_t)s->big_g];
+    std::vector<int32_t> cnt(s->n_msgs, 0), off(s->n_msgs), fill;
+    for (size_t i = g.first; i < g.first + g.len; i++) cnt[s->msg_id[i]]++;
+    int32_t tot = 0;
+    for (size_t j = 0; j < s->n_msgs; j++) {
+      off[j] = tot;
+      tot += cnt[j];
+    }
+    fill = off;
+    const size_t idx_off = s->plan.size();
+    s->plan.resize(idx_off + (size_t)tot);
+    for (size_t i = g.first; i < g.first + g.len; i++) s->plan[idx_off + (size_t)fill[s->msg_id[i]]++] = (int32_t)i;
+    s->msum = plan_seg(s->plan, 0, off, cnt, true, idx_off, 0);
+    A.agg_g = s->big_g;
+    A.n_magg = s->n_msgs;
+  }
   LSG_RC(plan_phase(s, A));
   s->chunk_items.assign(chunks.size(), {-1, -1});
-  if (!chunk_sub.empty()) {  // sub_items of the package group, in chunk order
+  if (!chunk_sub.empty() && A.agg_g < 0) {  // sub_items of the package group, in chunk order
     size_t r = 0;
     for (size_t g = 0; g < om.size(); g++) {
       const size_t ns = g < A.sub.size() && !A.sub[g].empty() ? A.sub[g].size() : 1;
@@ -1553,7 +1627,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     node = plan_seg(s->plan, 2, off, len, false, 0, 0);
   }
   LSG_RC(upload_plan(s));
-  LSG_RC(launch_set_stages(s, &s->pkagg, A.n_items, A.item_off, P_<uint32_t>(s->d_fall)));
+  LSG_RC(launch_set_stages(s, &s->pkagg, A, P_<uint32_t>(s->d_fall)));
   // signature points: unscaled for MSM groups, [r_i] sig_i for the rest
   if (!A.groups.empty()) {
     const bool any_small = A.n_msm < A.groups.size();

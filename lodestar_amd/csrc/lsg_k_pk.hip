@@ -3,6 +3,9 @@
 // KeyValidate (8f(2), block/processDeposit.ts:57-65), the RLC scaling [r_i] aggPK_i of blst
 // mul_n_aggregate (8a M4) and G1 serialisation.
 #include "lsg_kcommon.hpp"
+namespace {
+#include "lsg_inv.hpp"
+}  // namespace
 
 // pubkey -> projective G1 (infinity and undecodable keys become (0:1:0)).  A key given by
 // index (len == LSG_PK_INDEX: the slot's first 4 bytes) is gathered from the resident table
@@ -78,6 +81,31 @@ __global__ void LSG_KERNEL_ATTR k_pk_affine(int n, const uint32_t* __restrict__ 
   lane_store(P, item, a);
 }
 
+// One Miller pair per distinct message (lsg_host.hip msg_agg): the package group's scaled keys
+// r_i pk_i, each masked to the identity when its set cannot contribute (the rule of the Miller
+// kernels: a decode error or an infinite key), are summed per message by the segmented
+// reduction; the sums go affine with one divstep inversion each (a few dozen messages).
+__global__ void LSG_KERNEL_ATTR k_pk_mask(int n, const uint32_t* __restrict__ Pp, const int32_t* __restrict__ err,
+                                          const uint8_t* __restrict__ pinf, uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  (void)lead;
+  g1p_t p = proj_inf<fp_t>();
+  if (err[item] == 0 && !pinf[item]) p = lane_load<g1p_t>(Pp, item);
+  lane_store(out, item, p);
+}
+__global__ void LSG_KERNEL_ATTR k_g1p_affine_inv(int n, const uint32_t* __restrict__ Pp, uint32_t* __restrict__ P,
+                                                 uint8_t* __restrict__ pinf) {
+  LANE_ITEM(n);
+  const g1p_t p = lane_load<g1p_t>(Pp, item);
+  const bool is_inf = proj_is_inf(p);
+  const fp_t d = pair_inv_gcd(pair_canon(is_inf ? fp_one() : p.Z));  // (Z R)^-1 as an integer
+  const fp_t zi = pair_mont_mul(d, fp_t(FP_RCUBE));                   // Z^-1 R
+  g1a_t a;
+  fp_mul2(a.x, a.y, p.X, zi, p.Y, zi);
+  lane_store(P, item, a);
+  if (lead) pinf[item] = is_inf ? 1 : 0;
+}
+
 __global__ void LSG_KERNEL_ATTR k_g1p_to_bytes(int n, const uint32_t* __restrict__ pts, uint8_t* __restrict__ out) {
   LANE_ITEM(n);
   (void)lead;
@@ -139,6 +167,12 @@ hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* 
 }
 hipError_t pk_affine(hipStream_t st, int n, const uint32_t* Pp, const uint32_t* zinv, uint32_t* P) {
   LSG_LAUNCH_ITEMS(k_pk_affine, n, st, n, Pp, zinv, P);
+}
+hipError_t pk_mask(hipStream_t st, int n, const uint32_t* Pp, const int32_t* err, const uint8_t* pinf, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_pk_mask, n, st, n, Pp, err, pinf, out);
+}
+hipError_t g1p_affine_inv(hipStream_t st, int n, const uint32_t* Pp, uint32_t* P, uint8_t* pinf) {
+  LSG_LAUNCH_ITEMS(k_g1p_affine_inv, n, st, n, Pp, P, pinf);
 }
 hipError_t g1p_to_bytes(hipStream_t st, int n, const uint32_t* pts, uint8_t* out96) {
   LSG_LAUNCH_ITEMS(k_g1p_to_bytes, n, st, n, pts, out96);

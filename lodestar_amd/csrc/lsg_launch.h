@@ -52,6 +52,8 @@ hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, u
 hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* rnd, uint32_t* Pp, uint32_t* zP,
                     uint8_t* pinf);
 hipError_t pk_affine(hipStream_t st, int n, const uint32_t* Pp, const uint32_t* zinv, uint32_t* P);
+hipError_t pk_mask(hipStream_t st, int n, const uint32_t* Pp, const int32_t* err, const uint8_t* pinf, uint32_t* out);
+hipError_t g1p_affine_inv(hipStream_t st, int n, const uint32_t* Pp, uint32_t* P, uint8_t* pinf);
 hipError_t g1p_to_bytes(hipStream_t st, int n, const uint32_t* pts, uint8_t* out96);
 hipError_t sk_to_pk(hipStream_t st, int n, const uint8_t* sks, uint8_t* out96);
 

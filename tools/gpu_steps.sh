@@ -18,12 +18,15 @@ run() {  # name seconds command...
 for step in "$@"; do
   # row:<step> / pair:<step> run <step> with the row / pair serial kernels (A/B against the
   # straight-line-program default); w4:<step> with the 4-bit-window signature scaling kernel;
-  # nodedup:<step> hashing every set's message (no per-package message table)
+  # nodedup:<step> hashing every set's message (no per-package message table); noagg:<step>
+  # one Miller pair per set even when sets share a message; agg:<step> one pair per message
   if [ "${step#pair:}" != "$step" ]; then export LSG_SERIAL=pair TAG=${LSG_TAG:-r03}_pair; step=${step#pair:};
   elif [ "${step#row:}" != "$step" ]; then export LSG_SERIAL=row TAG=${LSG_TAG:-r03}_row; step=${step#row:};
   elif [ "${step#w4:}" != "$step" ]; then export LSG_SIG_SCALE=4 TAG=${LSG_TAG:-r03}_w4; step=${step#w4:};
   elif [ "${step#nodedup:}" != "$step" ]; then export LSG_MSG_DEDUP=0 TAG=${LSG_TAG:-r03}_nodedup; step=${step#nodedup:};
-  else unset LSG_SERIAL LSG_SIG_SCALE LSG_MSG_DEDUP; TAG=${LSG_TAG:-r03}; fi
+  elif [ "${step#noagg:}" != "$step" ]; then export LSG_MSG_AGG=0 TAG=${LSG_TAG:-r03}_noagg; step=${step#noagg:};
+  elif [ "${step#agg:}" != "$step" ]; then export LSG_MSG_AGG=1 TAG=${LSG_TAG:-r03}_agg; step=${step#agg:};
+  else unset LSG_SERIAL LSG_SIG_SCALE LSG_MSG_DEDUP LSG_MSG_AGG; TAG=${LSG_TAG:-r03}; fi
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ;;
     test-*) run "pytest_${step#test-}" 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "${step#test-}" ;;
