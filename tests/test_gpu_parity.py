@@ -170,12 +170,15 @@ def test_adversarial_jobs_match_oracle(ctx):
     check_jobs(ctx, jobs, seed=99)
 
 
-def test_shared_messages_match_oracle(ctx):
+@pytest.mark.parametrize("agg", ["0", "1"])
+def test_shared_messages_match_oracle(ctx, monkeypatch, agg):
     """Sets that sign one message (a committee's attestations) share one hash_to_G2 per
-    package (stage_sets message table, k_h2c_gather): verdicts, errors and counters stay the
-    oracle's, with corrupted sets inside the shared groups and sets whose corruption gives
-    them a message of their own."""
+    package (stage_sets message table, k_h2c_gather) and, with LSG_MSG_AGG=1, one Miller pair
+    (the masked sum of their scaled keys): verdicts, errors and counters stay the oracle's,
+    with corrupted sets inside the shared groups and sets whose corruption gives them a
+    message of their own."""
     import random
+    monkeypatch.setenv("LSG_MSG_AGG", agg)
     rng = random.Random(5)
     msgs = [bd.msg("committee", c) for c in range(3)]
     sets = []
