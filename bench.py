@@ -571,6 +571,8 @@ def main():
         - sf["miller_multi2_per_set"]
     per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
     per_set_muls -= (1.0 - wl.msgs_per_set) * sf["hash_map"]  # hash_to_G2 once per distinct message
+    if os.environ.get("LSG_MSG_AGG", "1") != "0":  # and one Miller pair per distinct message
+        per_set_muls -= (1.0 - wl.msgs_per_set) * (sf["miller_fused_per_set"] if fused else sf["miller_multi2_per_set"])
     node_mads = value * per_set_muls * opc["mads_per_fp_mul"]
     if rank == 0:
         cpu = None

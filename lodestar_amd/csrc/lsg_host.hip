@@ -840,11 +840,11 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
 // Packages of up to LSG_SLP_ITEMS sets (default 2048; 0: never) run one-set Miller items as
 // straight-line programs (lsg_slp.hip, one workgroup per set, ~0.8 ms) instead of the fused
 // kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
-// one Miller pair per distinct message in the package group (LSG_MSG_AGG=1; default: per set);
+// one Miller pair per distinct message in the package group (LSG_MSG_AGG=0: one per set);
 // read per package, so that a test can compare both forms in one process
 static bool msg_agg_on() {
   const char* e = getenv("LSG_MSG_AGG");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 size_t slp_items_max() {
