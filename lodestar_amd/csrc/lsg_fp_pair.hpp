@@ -54,19 +54,34 @@ LSG_PFN uint32_t pdown(uint32_t x) {                           // lane 0 <- lane
   const uint32_t v = pdpp<0xF5>(x);
   return pair_h() ? 0u : v;
 }
+#ifndef LSG_LEAF_DPP_AND  // A/B builds: 0 = the round-2 moves (DPP move, then and / select)
+#define LSG_LEAF_DPP_AND 1
+#endif
+#if LSG_LEAF_DPP_AND
 LSG_PFN uint32_t pup(uint32_t x) {  // lane 1 <- lane 0, lane 0 <- 0: one v_and_b32 with a DPP source
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xf, 0xf, true) & (0u - pair_h());
 }
+#else
+LSG_PFN uint32_t pup(uint32_t x) {
+  const uint32_t v = pdpp<0xA0>(x);
+  return pair_h() ? v : 0u;
+}
+#endif
 // pdown(x & M29) and pbcast<0>(x) & M29 as ONE v_and_b32 each: the DPP move folds into the and
 // (GCNDPPCombine) when the mask is a register operand -- lmask = M29 on lane 0 and 0 on lane 1
 // also does pdown's zeroing of lane 1, so the retire step loses an and and a cndmask and the m
 // broadcast an and
+#if LSG_LEAF_DPP_AND
 LSG_PFN uint32_t pdown_and(uint32_t x, uint32_t lmask) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xF5, 0xf, 0xf, true) & lmask;
 }
 LSG_PFN uint32_t pbcast0_and(uint32_t x, uint32_t m29) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xf, 0xf, true) & m29;
 }
+#else
+LSG_PFN uint32_t pdown_and(uint32_t x, uint32_t) { return pdown(x & LSG_M29); }
+LSG_PFN uint32_t pbcast0_and(uint32_t x, uint32_t) { return pbcast<0>(x & LSG_M29); }
+#endif
 #else
 #define LSG_PFN LSG_INL
 #define LSG_PLEAF LSG_NOINL
