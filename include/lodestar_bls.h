@@ -76,6 +76,9 @@ extern "C" {
 
 /* ---- job flags (VerifySignatureOpts, interface.ts:3-18; priority/same-message are extensions) */
 #define LSG_JOB_BATCHABLE 1u
+/* A package with a priority job (verifyOnMainThread, BlsGpuSingleThreadVerifier) is never held
+ * by coalescing and runs on its slot's high-priority streams: its kernels are dispatched ahead
+ * of the packages in flight.  Verdicts are unaffected. */
 #define LSG_JOB_PRIORITY 2u
 
 typedef struct lsg_ctx lsg_ctx;

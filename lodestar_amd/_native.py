@@ -10,6 +10,9 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSG_LIB", os.path.join(HERE, "liblodestar_bls.so"))  # LSG_LIB: A/B builds
+# the A/B and test build (lodestar_amd/build.py build_ab, csrc/lsg_ab.h): the same C ABI with
+# the stage switches read from the environment -- tests that compare two forms of a stage
+AB_LIB_PATH = os.path.join(HERE, "liblodestar_bls_ab.so")
 
 LSG_OK = 0
 LSG_ERR_NO_DEVICE = 2
@@ -277,8 +280,8 @@ class Context:
     """A device context (lsg_ctx) over `device`, or over the list `devices` (lsg_init_devices).
     Raises NativeUnavailable without a gfx950 GPU."""
 
-    def __init__(self, device=0, devices=None):
-        self.lib = load_library()
+    def __init__(self, device=0, devices=None, lib=None):
+        self.lib = load_library(lib or LIB_PATH)
         h = ctypes.c_void_p()
         if devices is None:
             rc = self.lib.lsg_init(int(device), ctypes.byref(h))

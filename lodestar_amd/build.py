@@ -13,12 +13,20 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblodestar_bls.so")
 # kernel translation units compile in parallel; lsg_host.hip is the orchestration + C ABI
-SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip", "lsg_k_reduce.hip", "lsg_serial.hip", "lsg_serial_wide.hip",
-           "lsg_serial_pair.hip", "lsg_serial_pair_wide.hip", "lsg_slp.hip", "lsg_host.hip"]
+SOURCES = ["lsg_k_hash.hip", "lsg_k_sig.hip", "lsg_k_pk.hip", "lsg_k_miller.hip", "lsg_k_reduce.hip", "lsg_slp.hip",
+           "lsg_host.hip"]
 HEADERS = ["lsg_types.hpp", "lsg_fp_lane.hpp", "lsg_fp_elem.hpp", "lsg_tower.hpp", "lsg_curve.hpp", "lsg_h2c.hpp",
            "lsg_pairing.hpp", "lsg_constants.hpp", "lsg_fp_pair.hpp", "lsg_constants_r29.hpp", "lsg_io.hpp",
-           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h", "lsg_slp_progs.h", "lsg_slp_exec.hpp", "lsg_inv.hpp"]
+           "lsg_serial.h", "lsg_kcommon.hpp", "lsg_launch.h", "lsg_layout.h", "lsg_slp_progs.h", "lsg_slp_exec.hpp", "lsg_inv.hpp",
+           "lsg_ab.h"]
 OBJ = os.path.join(HERE, "_obj")
+# The A/B and test build (lsg_ab.h): the orchestration compiled with -DLSG_AB (its switches read
+# from the environment) plus the row-backend serial kernels (LSG_SERIAL=row); every other
+# translation unit is the shipped library's own object.  Tests that compare two forms of a
+# stage load it beside the shipped library (lodestar_amd._native.load_library(AB_OUT)).
+AB_OUT = os.path.join(HERE, "liblodestar_bls_ab.so")
+AB_SOURCES = ["lsg_host.hip", "lsg_serial.hip", "lsg_serial_wide.hip"]
+AB_FLAGS = ["-DLSG_AB=1"]
 
 
 def hipcc():
@@ -33,11 +41,11 @@ def _deps():
                                                        os.path.abspath(__file__)]
 
 
-def needs_rebuild():
-    if not os.path.exists(OUT):
+def needs_rebuild(out=OUT, sources=SOURCES):
+    if not os.path.exists(out):
         return True
-    deps = [os.path.join(CSRC, f) for f in SOURCES] + _deps()
-    return max(os.path.getmtime(d) for d in deps if os.path.exists(d)) > os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in sources] + _deps()
+    return max(os.path.getmtime(d) for d in deps if os.path.exists(d)) > os.path.getmtime(out)
 
 
 # Tower functions (Fp2/Fp6/Fp12, LSG_BIGFN) inlined into the device kernels: as calls they
@@ -94,13 +102,33 @@ def build(force=False, verbose=True, extra=None, out=None):
     jobs = int(os.environ.get("LSG_BUILD_JOBS", str(min(8, os.cpu_count() or 4))))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose, extra), SOURCES))
+    _link(objs, out, verbose)
+    return out
+
+
+def _link(objs, out, verbose):
     cmd = [hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared"] + objs + ["-L/opt/rocm/lib", "-lrccl",
                                                                            "-Wl,-rpath,/opt/rocm/lib", "-o", out + ".tmp"]
     if verbose:
         print("[lodestar_amd.build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(out + ".tmp", out)
-    return out
+
+
+def build_ab(verbose=True):
+    """The A/B and test library (AB_OUT): AB_SOURCES with AB_FLAGS, the rest shared with the
+    shipped build (build() first)."""
+    from concurrent.futures import ThreadPoolExecutor
+    build(verbose=verbose)
+    if not needs_rebuild(AB_OUT, SOURCES + AB_SOURCES):
+        return AB_OUT
+    os.makedirs(_obj_dir(AB_FLAGS), exist_ok=True)
+    with ThreadPoolExecutor(max_workers=len(AB_SOURCES)) as ex:
+        ab = dict(zip(AB_SOURCES, ex.map(lambda s: _compile(s, verbose, AB_FLAGS), AB_SOURCES)))
+    objs = [ab.get(s) or os.path.join(OBJ, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    objs += [ab[s] for s in AB_SOURCES if s not in SOURCES]
+    _link(objs, AB_OUT, verbose)
+    return AB_OUT
 
 
 NAPI_SRC = os.path.join(HERE, "napi", "lsg_napi.c")
@@ -128,4 +156,5 @@ def build_napi(verbose=True):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_ab()
     build_napi()

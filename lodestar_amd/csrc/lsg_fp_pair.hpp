@@ -350,7 +350,7 @@ LSG_PFN fp_duo pair_fp2_mul(const fp_t& a0, const fp_t& a1, const fp_t& b0, cons
   return pair_fp2_mul_v(fp_pack(a0), fp_pack(a1), fp_pack(b0), LSG_TAIL_ARGS(b1));
 }
 LSG_PFN fp_duo pair_fp2_sqr(const fp_t& a0, const fp_t& a1) { return pair_fp2_sqr_v(fp_pack(a0), fp_pack(a1)); }
-#if LSG_LEAF_MODE != 0 && !defined(LSG_PAIR_SPLIT)
+#if LSG_LEAF_MODE != 0
 #define LSG_FP2_LEAF 1  // lsg_tower.hpp's fp2_mul / fp2_sqr call the two leaves above
 #endif
 
@@ -381,60 +381,7 @@ LSG_PFN fp_t fp_sub(const fp_t& a, const fp_t& b) {
 }
 LSG_PFN fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
 LSG_PFN fp_t fp_mul(const fp_t& a, const fp_t& b) { return pair_mont_mul(a, b); }
-#ifdef LSG_PAIR_SPLIT
-// ---- one item per wave (the serial per-group stages, lsg_serial_pair.hip): every lane pair
-// holds the whole item; a batch of N independent products (fp_mul_list, lsg_tower.hpp) is
-// split over the wave's 32 lane pairs -- pair q multiplies operands q, q + 32, ... (picked
-// from its replicated copies with selects), one leaf call for the whole batch -- and every
-// pair collects the N results with ds_bpermute (7 words each).  A batch of 18 then costs
-// about two products' time instead of 18.  Everything outside the batches runs replicated.
-#define LSG_ROW_SPLIT 1
-#define LSG_SPLIT_MIN 2
-LSG_PFN uint32_t pair_q() { return __lane_id() >> 1; }
-// only lane pair 0 stores bytes (the other pairs hold the same values)
-LSG_PFN bool pair_writer() { return __lane_id() < 2; }
-template <int N>
-LSG_PFN void fp_mul_list_rows(fp_t* r, const fp_t* x, const fp_t* y) {
-  constexpr int M = (N + 31) / 32;
-  const uint32_t q = pair_q();
-  fp_t o[M];
-#pragma unroll
-  for (int j = 0; j < M; j++) {
-    fp_t a = x[32 * j], b = y[32 * j];  // a pair past the end repeats product 32j
-#pragma unroll
-    for (int t = 1; t < 32; t++) {
-      if (32 * j + t < N) {
-        const bool s = q == (uint32_t)t;
-        a = fp_select(s, x[32 * j + t], a);
-        b = fp_select(s, y[32 * j + t], b);
-      }
-    }
-    o[j] = pair_mont_mul(a, b);
-  }
-  const int h = (int)pair_h();
-#pragma unroll
-  for (int k = 0; k < N; k++)
-#pragma unroll
-    for (int l = 0; l < LSG_PL; l++)
-      r[k].l[l] = (uint32_t)__builtin_amdgcn_ds_bpermute((2 * (k % 32) + h) << 2, (int)o[k / 32].l[l]);
-}
-LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
-  const fp_t x[2] = {a0, a1}, y[2] = {b0, b1};
-  fp_t r[2];
-  fp_mul_list_rows<2>(r, x, y);
-  r0 = r[0];
-  r1 = r[1];
-}
-LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1,
-                     const fp_t& a2, const fp_t& b2) {
-  const fp_t x[3] = {a0, a1, a2}, y[3] = {b0, b1, b2};
-  fp_t r[3];
-  fp_mul_list_rows<3>(r, x, y);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-}
-#elif LSG_LEAF_MODE == 0
+#if LSG_LEAF_MODE == 0
 LSG_PFN void fp_mul2(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& b0, const fp_t& a1, const fp_t& b1) {
   fp_t t = pair_mont_mul(a0, b0);
   r1 = pair_mont_mul(a1, b1);
@@ -463,12 +410,8 @@ LSG_PFN void fp_mul3(fp_t& r0, fp_t& r1, fp_t& r2, const fp_t& a0, const fp_t& b
 }
 #endif
 LSG_PFN void fp_mul9(fp_t* r, const fp_t* a, const fp_t* b) {
-#ifdef LSG_PAIR_SPLIT
-  fp_mul_list_rows<9>(r, a, b);
-#else
 #pragma unroll
   for (int g = 0; g < 9; g += 3) fp_mul3(r[g], r[g + 1], r[g + 2], a[g], b[g], a[g + 1], b[g + 1], a[g + 2], b[g + 2]);
-#endif
 }
 
 // the Fp2 leaves declared above (they need fp_add / fp_sub)
@@ -652,9 +595,6 @@ LSG_PFN void fp_to_be48(uint8_t* b, const fp_t& a) {
     w[k] = (uint32_t)x;
   }
   constexpr int PW = 12 / LSG_GROUP;
-#ifdef LSG_PAIR_SPLIT
-  if (!pair_writer()) return;
-#endif
 #pragma unroll
   for (int j = 0; j < PW; j++) {
     const int k = PW * (int)pair_h() + j;

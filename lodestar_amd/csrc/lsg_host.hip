@@ -42,6 +42,7 @@
 #include "lsg_launch.h"
 #include "lsg_layout.h"
 #include "lsg_serial.h"
+#include "lsg_ab.h"
 
 using namespace lsgl;
 
@@ -245,6 +246,8 @@ struct PendingPkg {
 struct MergeTicket {
   int slot = -1;  // -1: not launched yet
   int sub = -1;
+  int rc = 0;       // != 0: its coalesced launch failed (the wait reports rc and err)
+  std::string err;
 };
 
 struct Dev;
@@ -294,6 +297,10 @@ struct Slot {
   int index = 0;
   hipStream_t st[2] = {nullptr, nullptr};  // [0] main, [1] side
   bool own_streams = true;
+  // the slot's high-priority stream pair (created on first use): a package carrying an
+  // LSG_JOB_PRIORITY job runs on it, so its kernels are dispatched ahead of the packages in
+  // flight (verifyOnMainThread's latency under load)
+  hipStream_t st_norm[2] = {nullptr, nullptr}, st_prio[2] = {nullptr, nullptr};
   int cur = 0;
   hipEvent_t ev_in = nullptr, ev_sig = nullptr, ev_grp = nullptr, ev_part = nullptr, ev_done = nullptr,
              ev_node = nullptr;
@@ -355,6 +362,15 @@ struct Slot {
   lsg_stats stats;
   bool has_node = false;  // this slot computed the node check (device 0 of a multi-device ticket)
   size_t n_jobs = 0;      // device 0: the ticket's job count
+  // the package group is one set verified unscaled (r_i = 0, a plain verify): its partial is
+  // raised to a fresh 64-bit randomizer before it leaves the slot (lsg_jobs_partial*)
+  bool lone_unscaled = false;
+  uint64_t seed = 0;  // the package's randomizer seed (0: OS CSPRNG)
+  DevBuf d_xport;
+  HostBuf h_xport;
+  // multi-device ticket: the package group's final exponentiation was not launched -- the
+  // node check over every device's partial decides, and this one runs only if that fails
+  bool big_fe_pending = false;
   // coalesced launch (lsg_set_coalesce): n_sub caller packages in one slot.  sub_first: their
   // job-index bounds in the merged job list; bpos_first: their bounds in batch_order.  Each
   // one keeps its own 16-job chunks, deserialisation rule and counters; the slot is freed
@@ -539,7 +555,9 @@ int slot_create(Dev* d, Slot* s, int index, hipStream_t shared) {
     s->st[0] = s->st[1] = shared;
     s->own_streams = false;
   } else {
-    for (int k = 0; k < 2; k++) LSG_HIP(s, hipStreamCreateWithFlags(&s->st[k], hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) LSG_HIP(s, hipStreamCreateWithFlags(&s->st_norm[k], hipStreamNonBlocking));
+    s->st[0] = s->st_norm[0];
+    s->st[1] = s->st_norm[1];
   }
   hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_part, &s->ev_done, &s->ev_node};
   for (hipEvent_t* e : evs) LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -566,11 +584,12 @@ void slot_destroy(Slot* s) {
                     &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
                     &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm,
-                    &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm};
+                    &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm, &s->d_xport};
   for (DevBuf* b : bufs) free_dev(*b);
   for (auto& u : s->seg_tmp)
     for (DevBuf& b : u) free_dev(b);
-  HostBuf* hb[] = {&s->h_arena, &s->h_err, &s->h_pinf, &s->h_pkerr, &s->h_verdict, &s->h_blob, &s->h_plan, &s->h_nodeV};
+  HostBuf* hb[] = {&s->h_arena, &s->h_err, &s->h_pinf, &s->h_pkerr, &s->h_verdict, &s->h_blob, &s->h_plan, &s->h_nodeV,
+                   &s->h_xport};
   for (HostBuf* b : hb) free_host(*b);
   for (Timer& t : s->timers) {
     (void)hipEventDestroy(t.a);
@@ -580,10 +599,34 @@ void slot_destroy(Slot* s) {
   hipEvent_t evs[] = {s->ev_in, s->ev_sig, s->ev_grp, s->ev_part, s->ev_done, s->ev_node};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
-  if (s->own_streams)
-    for (int k = 0; k < 2; k++)
-      if (s->st[k]) (void)hipStreamDestroy(s->st[k]);
+  if (s->own_streams) {
+    for (int k = 0; k < 2; k++) {
+      if (s->st_prio[k]) (void)hipStreamSynchronize(s->st_prio[k]);
+      if (s->st_norm[k]) (void)hipStreamSynchronize(s->st_norm[k]);
+    }
+    for (int k = 0; k < 2; k++) {
+      if (s->st_norm[k]) (void)hipStreamDestroy(s->st_norm[k]);
+      if (s->st_prio[k]) (void)hipStreamDestroy(s->st_prio[k]);
+      s->st_norm[k] = s->st_prio[k] = s->st[k] = nullptr;
+    }
+  }
   s->d = nullptr;
+}
+
+// select the slot's stream pair for its next package (the slot is free: nothing of an
+// earlier package is in flight on either pair)
+int slot_streams(Slot* s, bool prio) {
+  if (!s->own_streams) return LSG_OK;
+  if (prio && !s->st_prio[0]) {
+    int least = 0, greatest = 0;
+    LSG_HIP(s, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (int k = 0; k < 2; k++)
+      LSG_HIP(s, hipStreamCreateWithPriority(&s->st_prio[k], hipStreamNonBlocking, greatest));
+  }
+  hipStream_t* p = prio ? s->st_prio : s->st_norm;
+  s->st[0] = p[0];
+  s->st[1] = p[1];
+  return LSG_OK;
 }
 
 // the pipeline slot `s` of device `d`, created on first use
@@ -622,19 +665,13 @@ int sub_of_job(const Slot* s, size_t j) {
 // runs alone for ~14 ms; smaller K trades work for latency there.  Env LSG_MILLER_K forces K.
 // The fused Miller kernel (k_miller_fused: lines in LDS, four waves per item of four pairs) is
 // the default; LSG_MILLER_FUSED=0 selects the split pair k_miller_lines / k_miller_accum<K>.
-bool miller_fused() {
-  const char* e = getenv("LSG_MILLER_FUSED");
-  return !(e && atoi(e) == 0);
-}
+bool miller_fused() { return lsg_ab_long("LSG_MILLER_FUSED", 1) != 0; }
 
 size_t slp_items_max();
 int miller_k_for(size_t n_sets) {
   if (miller_fused()) return n_sets <= slp_items_max() ? 1 : 4;  // fused: four waves' lane pairs per item
-  const char* e = getenv("LSG_MILLER_K");
-  if (e) {
-    const int v = atoi(e);
-    if (v == 1 || v == 2 || v == 4) return v;
-  }
+  const long v = lsg_ab_long("LSG_MILLER_K", 0);
+  if (v == 1 || v == 2 || v == 4) return (int)v;
   return n_sets >= 8192 ? 4 : (n_sets >= 1024 ? 2 : 1);
 }
 
@@ -642,17 +679,13 @@ int miller_k_for(size_t n_sets) {
 // fixed cost of 2040 buckets and 64 bit sums per group exceeds the per-set scalar
 // multiplications it replaces.
 size_t msm_min_group() {
-  const char* e = getenv("LSG_MSM_MIN_GROUP");
-  const long x = e ? atol(e) : 256;
+  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 256);
   return x < 1 ? (size_t)1 : (size_t)x;
 }
 
 // Phase A as the reference batches it: one RLC group per 16-job chunk instead of one package
 // group (env LSG_PACKAGE_GROUP=0; A/B and the equivalence test of the two modes)
-bool package_group_mode() {
-  const char* e = getenv("LSG_PACKAGE_GROUP");
-  return !(e && atoi(e) == 0);
-}
+bool package_group_mode() { return lsg_ab_long("LSG_PACKAGE_GROUP", 1) != 0; }
 
 void binv_sizes(size_t n, size_t* lv, size_t* iv);
 size_t binv_lv_words(size_t n) {
@@ -842,15 +875,11 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
 // kernel, whose latency is one full loop per lane whatever the package size (~5.4 ms).
 // one Miller pair per distinct message in the package group (LSG_MSG_AGG=0: one per set);
 // read per package, so that a test can compare both forms in one process
-static bool msg_agg_on() {
-  const char* e = getenv("LSG_MSG_AGG");
-  return !(e && e[0] == '0');
-}
+static bool msg_agg_on() { return lsg_ab_long("LSG_MSG_AGG", 1) != 0; }
 
 size_t slp_items_max() {
-  const char* e = getenv("LSG_SLP_ITEMS");
-  const size_t v = e ? (size_t)atol(e) : (size_t)2048;
-  return lsg_serial_mode() == LSG_SERIAL_SLP ? v : 0;
+  const long v = lsg_ab_long("LSG_SLP_ITEMS", 2048);
+  return lsg_serial_mode() == LSG_SERIAL_SLP && v > 0 ? (size_t)v : 0;
 }
 
 // hash_to_G2 of the slot's n expanded messages (d_ub) into H / hinf on the current stream
@@ -921,10 +950,7 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   // open-addressing table over the messages: slot -> distinct message id (mfirst: its set),
   // with the message's 64-bit key beside it so that a probe compares bytes only on a key match
   size_t cap = 0;
-  static const bool dedup_on = [] {
-    const char* e = getenv("LSG_MSG_DEDUP");
-    return !(e && e[0] == '0');
-  }();
+  static const bool dedup_on = lsg_ab_long("LSG_MSG_DEDUP", 1) != 0;
   // a package whose sample of 256 evenly spaced sets shows no repeated message is taken as all
   // distinct and staged without the table (the firehose of distinct gossip messages pays ~5 us,
   // not the table's ~1 ms under the context lock); committee-shaped packages repeat at once
@@ -1262,14 +1288,18 @@ int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fal
   return LSG_OK;
 }
 
-// FE of the phase's groups + verdict readback (main stream)
-int launch_fe(Slot* s, size_t ng) {
-  if (ng == 0) return LSG_OK;
+// FE of the phase's groups g0 .. g1-1 + verdict readback (main stream)
+int launch_fe_range(Slot* s, size_t g0, size_t g1) {
+  if (g1 <= g0) return LSG_OK;
   s->cur = 0;
-  KL(s, "k_row_final_exp", lsg_row_final_exp(S_(s), (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
-  LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, s->st[0]));
+  const size_t ng = g1 - g0;
+  KL(s, "k_row_final_exp",
+     lsg_row_final_exp(S_(s), (int)ng, P_<uint8_t>(s->d_Fb) + 576 * g0, P_<int32_t>(s->d_verdict) + g0));
+  LSG_HIP(s, hipMemcpyAsync(H_<int32_t>(s->h_verdict) + g0, P_<int32_t>(s->d_verdict) + g0, 4 * ng,
+                            hipMemcpyDeviceToHost, s->st[0]));
   return LSG_OK;
 }
+int launch_fe(Slot* s, size_t ng) { return launch_fe_range(s, 0, ng); }
 
 // Per-set stages of the slot's package (no host synchronisation):
 //   side: pubkeys -> aggregation -> [r_i] scaling -> signature decode -> subgroup check (ev_sig)
@@ -1454,8 +1484,12 @@ int launch_sig_prep(Slot* s, bool scale, const std::vector<uint8_t>* mode, uint3
 // first), plan and launch every per-set stage and group stage up to the canonical products
 // (ev_part).  n_node > 0: this slot also reduces the all-gathered partials of n_node devices
 // (its plan holds that product's chunk list).
+// lone_ok: a set alone in its phase-A group may be verified unscaled (a plain verify, as
+// maybeBatch.ts:34-38).  False when the package group's partial is multiplied with other
+// partials before its verdict (a multi-device ticket, lsg_batch_partial): there every r_i is
+// random and nonzero, or two forged one-set shards (sig_a + D, sig_b - D) would pass together.
 int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint64_t seed, int n_node,
-              const std::vector<size_t>* subs = nullptr) {
+              const std::vector<size_t>* subs = nullptr, bool lone_ok = true) {
   timer_reset(s);
   s->plan.clear();
   memset(&s->stats, 0, sizeof(s->stats));
@@ -1470,6 +1504,9 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   s->rs2_ready = false;
   s->rs2_scaled.clear();
   s->has_node = n_node > 0;
+  s->lone_unscaled = false;
+  s->big_fe_pending = false;
+  s->seed = seed;
   std::vector<const lsg_set*> flat;
   std::vector<size_t> nonb;
   for (int pass = 0; pass < 2; pass++)
@@ -1506,8 +1543,10 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   s->K = miller_k_for(flat.size());
   // sets alone in their phase-A group (and so in every later group): no RLC scaling
   std::vector<uint8_t> noscale(flat.size(), 0);
-  if (package_group_mode() && !subs) {
-    if (s->nb_sets == 1) noscale[0] = 1;
+  if (!lone_ok) {
+    // (non-batchable jobs below: their groups never enter the package partial)
+  } else if (package_group_mode() && !subs) {
+    if (s->nb_sets == 1) noscale[0] = s->lone_unscaled = true;
   } else {
     const auto ch = slot_chunks(s);
     for (auto& c : ch) {
@@ -1530,7 +1569,7 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     Grp g;
     g.first = first;
     g.len = len;
-    g.msm = len >= msm_min_group();
+    g.msm = len >= std::max(msm_min_group(), (size_t)2);  // an r_i = 0 set never enters a bucket MSM
     (g.msm ? gm : gs).push_back(g);
     (g.msm ? om : os).push_back(owner);
   };
@@ -1654,6 +1693,32 @@ const uint8_t* pkg_partial_dev(Slot* s) {
   return P_<uint8_t>(s->d_Fb) + 576 * (size_t)s->big_g;
 }
 
+// The package group's partial as it may leave the slot (lsg_jobs_partial*), on the main stream:
+// a lone unscaled set's f is raised to a fresh nonzero 64-bit randomizer (two
+// one-set shards holding sig_a + D and sig_b - D must not pass a product check together).
+int export_partial_dev(Slot* s, const uint8_t** src) {
+  *src = pkg_partial_dev(s);
+  if (!s->lone_unscaled) return LSG_OK;
+  uint64_t r = 0;
+  if (s->seed) {  // tests: reproducible
+    uint64_t sd = s->seed ^ 0x5851f42d4c957f2dull;
+    do r = splitmix64(sd);
+    while (r == 0);
+  } else {
+    do {
+      if (!os_random(&r, 8)) {
+        s->d->c->err = "no entropy for the exported partial's randomizer (getrandom failed)";
+        return LSG_ERR_ENTROPY;
+      }
+    } while (r == 0);
+  }
+  LSG_RC(ensure(s, s->d_xport, 576));
+  s->cur = 0;
+  KL(s, "k_fp12_pow", lsgk::fp12_pow_u64(S_(s), *src, r, P_<uint8_t>(s->d_xport)));
+  *src = P_<uint8_t>(s->d_xport);
+  return LSG_OK;
+}
+
 // node check on this slot (device 0 of the ticket): product of the n gathered partials in
 // d_gath, one final exponentiation -> h_nodeV (ev_node)
 int pkg_node_check(Slot* s, int n) {
@@ -1669,9 +1734,19 @@ int pkg_node_check(Slot* s, int n) {
   return LSG_OK;
 }
 
-// Part 2 of phase A: every group's final exponentiation and the status readback (ev_done)
-int pkg_part2(Slot* s) {
-  LSG_RC(launch_fe(s, s->phA.groups.size()));
+// Part 2 of phase A: every group's final exponentiation and the status readback (ev_done).
+// skip_big (a multi-device ticket): the package group's final exponentiation is left out --
+// the node check over all devices' partials decides it (one final
+// exponentiation per node), and it runs only when that check fails (pkg_resolve).
+int pkg_part2(Slot* s, bool skip_big = false) {
+  const size_t ng = s->phA.groups.size();
+  s->big_fe_pending = skip_big && !s->chunk_mode && s->big_g >= 0;
+  if (s->big_fe_pending) {
+    LSG_RC(launch_fe_range(s, 0, (size_t)s->big_g));
+    LSG_RC(launch_fe_range(s, (size_t)s->big_g + 1, ng));
+  } else {
+    LSG_RC(launch_fe(s, ng));
+  }
   return launch_readback(s, true);
 }
 
@@ -1763,6 +1838,23 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   return LSG_OK;
 }
 
+// the deferred final exponentiation of the package group (pkg_part2 skip_big), synchronous
+int run_big_fe(Slot* s, CtxLock* lk) {
+  s->cur = 0;
+  LSG_RC(launch_fe_range(s, (size_t)s->big_g, (size_t)s->big_g + 1));
+  LSG_HIP(s, hipEventRecord(s->ev_done, s->st[0]));
+  const int dev = s->d->device;
+  if (lk) lk->unlock();
+  hipError_t e = hipEventSynchronize(s->ev_done);
+  if (lk) {
+    lk->lock();
+    (void)hipSetDevice(dev);
+  }
+  if (e != hipSuccess) return fail(s, "hipEventSynchronize", e);
+  s->big_fe_pending = false;
+  return LSG_OK;
+}
+
 // The reference's verdict rules for this device's share of the package (worker.ts:30-106),
 // after ev_done.  node_valid: 1 = the node-wide check of all devices' partials passed, 0 = it
 // failed (this device's own package check localises), -1 = no node check (single device).
@@ -1785,15 +1877,26 @@ int32_t first_pk_error(Slot* s, size_t* job_id) {
 
 // pkfail: the package-wide deserializeSet failure (first_pk_error over every device of the
 // ticket, in caller order) -- a bad key on any device rejects every job of the package
+// node_valid 2: this ticket's own node check (lsg_init_devices: the library gathered every
+// device's partial itself) passed, and it decides the package group.
 int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
   const SetStatus ss = read_status(s);
   const PhasePlan& A = s->phA;
   std::vector<int32_t> vA(H_<int32_t>(s->h_verdict), H_<int32_t>(s->h_verdict) + A.groups.size());
-  s->stats.n_final_exps += (uint32_t)A.groups.size();
+  s->stats.n_final_exps += (uint32_t)(A.groups.size() - (s->big_fe_pending ? 1 : 0));
   const size_t nj = s->jobs.size();
   if (pkfail) {
     for (size_t j = 0; j < nj; j++) s->results[j] = {LSG_ERROR, pkfail};
     return LSG_OK;
+  }
+  if (s->big_fe_pending) {
+    if (node_valid == 2) {
+      vA[(size_t)s->big_g] = 1;
+    } else {  // the node check failed: this device's own check localises
+      LSG_RC(run_big_fe(s, lk));
+      vA[(size_t)s->big_g] = H_<int32_t>(s->h_verdict)[s->big_g];
+      s->stats.n_final_exps++;
+    }
   }
   // counters of the chunk at batch_order position q: the slot's, and its sub-package's
   auto retry_inc = [&](size_t q) {
@@ -2040,10 +2143,7 @@ void sync_slot(Slot* s) {
     if (s->st[k]) (void)hipStreamSynchronize(s->st[k]);
 }
 
-bool force_exchange() {
-  const char* e = getenv("LSG_FORCE_EXCHANGE");
-  return e && atoi(e) != 0;
-}
+bool force_exchange() { return lsg_ab_long("LSG_FORCE_EXCHANGE", 0) != 0; }
 
 // all-gather of the devices' partials into device 0's d_gath, then the node check there
 int pkg_exchange(lsg_ctx* c, int p) {
@@ -2080,7 +2180,8 @@ int pkg_exchange(lsg_ctx* c, int p) {
   return pkg_node_check(s0, n);
 }
 
-int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket) {
+int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket,
+               bool lone_ok = true) {
   int p = -1;
   for (int i = 0; i < LSG_SLOTS && p < 0; i++)
     if (c->dev[0]->slots[i].kind == SLOT_FREE) p = i;
@@ -2090,9 +2191,12 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
   }
   const int n = c->n_dev;
   const bool exch = n > 1 || force_exchange();
+  bool prio = false;
+  for (size_t j = 0; j < n_jobs; j++) prio = prio || (jobs[j].flags & LSG_JOB_PRIORITY) != 0;
   for (int d = 0; d < n; d++) {
     (void)hipSetDevice(c->dev[d]->device);
     LSG_RC(slot_ready(c->dev[d], &c->dev[d]->slots[p], p));
+    LSG_RC(slot_streams(&c->dev[d]->slots[p], prio));
   }
   (void)hipSetDevice(c->dev[0]->device);
   std::vector<std::vector<size_t>> ids(n);
@@ -2108,12 +2212,12 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
     (void)hipSetDevice(c->dev[d]->device);
     // distinct seeds per device for tests; 0 stays 0 (OS CSPRNG on every device)
     const uint64_t sd = seed ? seed + 0x9e3779b97f4a7c15ull * (uint64_t)d : 0;
-    rc = pkg_part1(&c->dev[d]->slots[p], jobs, ids[d], sd, (d == 0 && exch) ? n : 0);
+    rc = pkg_part1(&c->dev[d]->slots[p], jobs, ids[d], sd, (d == 0 && exch) ? n : 0, nullptr, lone_ok && !exch);
   }
   if (!rc && exch) rc = pkg_exchange(c, p);
   for (int d = 0; d < n && !rc; d++) {
     (void)hipSetDevice(c->dev[d]->device);
-    rc = pkg_part2(&c->dev[d]->slots[p]);
+    rc = pkg_part2(&c->dev[d]->slots[p], exch);
   }
   (void)hipSetDevice(c->dev[0]->device);
   if (rc) {
@@ -2142,7 +2246,8 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
     if (hipEventSynchronize(s->ev_done) != hipSuccess) rc = fail(s, "hipEventSynchronize", hipGetLastError());
   }
   Slot* s0 = &c->dev[0]->slots[p];
-  if (!rc && node_valid == -2) node_valid = s0->has_node ? (H_<int32_t>(s0->h_nodeV)[0] ? 1 : 0) : -1;
+  // the ticket's own node check (lsg_init_devices) decides the package groups: 2 = passed
+  if (!rc && node_valid == -2) node_valid = s0->has_node ? (H_<int32_t>(s0->h_nodeV)[0] ? 2 : 0) : -1;
   lsg_stats total;
   memset(&total, 0, sizeof(total));
   total.start_ns = s0->stats.start_ns;
@@ -2238,6 +2343,7 @@ int flush_pending(lsg_ctx* c) {
   }
   Slot* s = &c->dev[0]->slots[p];
   LSG_RC(slot_ready(c->dev[0], s, p));
+  LSG_RC(slot_streams(s, false));
   std::vector<lsg_job> all;
   std::vector<size_t> subs{0};
   uint64_t seed = c->pending[0].seed;
@@ -2252,7 +2358,14 @@ int flush_pending(lsg_ctx* c) {
   if (!rc) rc = pkg_part2(s);
   if (rc) {
     sync_slot(s);
-    for (auto& pk : c->pending) c->merged.erase(pk.serial);  // their waits report the error
+    // every held package's wait (or poll) reports this failure -- its code and message --
+    // instead of an unknown ticket; the entry goes when its ticket is waited on
+    for (auto& pk : c->pending) {
+      MergeTicket& m = c->merged[pk.serial];
+      m.slot = -1;
+      m.rc = rc;
+      m.err = c->err;
+    }
     c->pending.clear();
     c->pending_sets = 0;
     return rc;
@@ -2289,7 +2402,10 @@ int submit_merged(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed,
   c->pending_sets += n_sets;
   if (launches_in_flight(c) < c->co_inflight) {
     const int rc = flush_pending(c);
-    if (rc && rc != LSG_ERR_BUSY) return rc;  // (busy: it stays pending, a later wait launches it)
+    if (rc && rc != LSG_ERR_BUSY) {  // (busy: it stays pending, a later wait launches it)
+      c->merged.erase(serial);       // this submission fails; the others' waits report rc
+      return rc;
+    }
   }
   return LSG_OK;
 }
@@ -2303,9 +2419,16 @@ int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* st
     LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
     auto it = c->merged.find(serial);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
-    if (it->second.slot < 0) LSG_RC(flush_pending(c));  // the waiter wants it now
+    if (it->second.slot < 0 && !it->second.rc) (void)flush_pending(c);  // the waiter wants it now
     it = c->merged.find(serial);
-    if (it == c->merged.end() || it->second.slot < 0) return LSG_ERR_INVALID_ARG;
+    if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+    if (it->second.rc) {  // its coalesced launch failed
+      const int frc = it->second.rc;
+      c->err = it->second.err;
+      c->merged.erase(it);
+      return frc;
+    }
+    if (it->second.slot < 0) return LSG_ERR_INVALID_ARG;
     p = it->second.slot;
     k = it->second.sub;
     ev = c->dev[0]->slots[p].ev_done;
@@ -2647,7 +2770,9 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
   for (size_t j = 0; j < n_jobs; j++)
     if (jobs[j].n_sets && !jobs[j].sets) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
-  if (c->co_max_sets && c->n_dev == 1) {
+  bool prio = false;
+  for (size_t j = 0; j < n_jobs; j++) prio = prio || (jobs[j].flags & LSG_JOB_PRIORITY) != 0;
+  if (c->co_max_sets && c->n_dev == 1 && !prio) {  // (a priority package is never held back)
     size_t ns = 0;
     for (size_t j = 0; j < n_jobs; j++) ns += jobs[j].n_sets;
     if (ns <= c->co_max_sets) return submit_merged(c, jobs, n_jobs, seed, ns, ticket);
@@ -2706,10 +2831,18 @@ int lsg_jobs_partial(lsg_ctx* c, lsg_ticket ticket, uint8_t* out576, int32_t* ha
   if (p < 0) return LSG_ERR_INVALID_ARG;
   Slot* s = &c->dev[0]->slots[p];
   const bool has = !s->phA.groups.empty() && s->big_g >= 0;
-  if (has)
+  if (has && s->lone_unscaled) {
+    const uint8_t* src;
+    LSG_RC(export_partial_dev(s, &src));
+    LSG_RC(ensure_host(s, s->h_xport, 576));
+    LSG_HIP(s, hipMemcpyAsync(s->h_xport.p, src, 576, hipMemcpyDeviceToHost, s->st[0]));
+    LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+    memcpy(out576, s->h_xport.p, 576);
+  } else if (has) {
     memcpy(out576, H_<uint8_t>(s->h_blob) + 576 * (size_t)s->big_g, 576);
-  else
+  } else {
     memcpy(out576, fp12_one_blob(), 576);
+  }
   if (has_batch) *has_batch = has ? 1 : 0;
   return LSG_OK;
 }
@@ -2727,7 +2860,9 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
   Slot* s = &c->dev[0]->slots[p];
   const bool has = !s->phA.groups.empty() && s->big_g >= 0;
   if (has) {
-    LSG_HIP(s, hipMemcpyAsync(dev_out576, pkg_partial_dev(s), 576, hipMemcpyDeviceToDevice, s->st[0]));
+    const uint8_t* src;
+    LSG_RC(export_partial_dev(s, &src));
+    LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, s->st[0]));
   } else {
     LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, s->st[0]));
   }
@@ -2769,11 +2904,16 @@ int lsg_poll(lsg_ctx* c, lsg_ticket ticket, int32_t* done) {
   } else if (((ticket >> 8) & 255) == SLOT_MERGE) {
     auto it = c->merged.find(ticket >> 16);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+    if (it->second.rc) {  // its launch failed: done (the wait reports the failure)
+      *done = 1;
+      return LSG_OK;
+    }
     if (it->second.slot < 0) {  // not launched: launch when the device has room
       maybe_flush(c);
       it = c->merged.find(ticket >> 16);
-      if (it == c->merged.end() || it->second.slot < 0) {
-        *done = 0;
+      if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+      if (it->second.slot < 0) {
+        *done = it->second.rc ? 1 : 0;
         return LSG_OK;
       }
     }
@@ -2810,7 +2950,7 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
     job.sets = sets;
     job.n_sets = (uint32_t)n_sets;
     job.flags = LSG_JOB_BATCHABLE;
-    int rc = submit_pkg(c, &job, 1, seed, &t);
+    int rc = submit_pkg(c, &job, 1, seed, &t, false);  // the partial leaves: every r_i random
     if (rc) return rc;
   }
   const int prc = presync_pkg(c, t, false);

@@ -149,6 +149,25 @@ __global__ void LSG_KERNEL_ATTR k_fp12_to_canon(int n, const uint32_t* __restric
   fp12_to_canon_bytes(out + 576 * item, lane_load<fp12_t>(in, item));
 }
 
+// f^r for a nonzero 64-bit r (square-and-multiply, one item): the partial of a package group
+// that is one set verified unscaled leaves the slot as f^r, so that FE(product of partials) is
+// the RLC check prod_i e_i^(r_i) whatever the other partials are (FE(f^r) = FE(f)^r)
+__global__ void LSG_KERNEL_ATTR_W(1) k_fp12_pow_u64(const uint8_t* __restrict__ in576, uint64_t r,
+                                                    uint8_t* __restrict__ out576) {
+  LANE_ITEM(1);
+  (void)lead;
+  const fp12_t f = fp12_from_canon_bytes(in576);
+  fp12_t acc = f;
+  int top = 63;
+  while (top > 0 && !((r >> top) & 1u)) top--;
+#pragma unroll 1
+  for (int b = top - 1; b >= 0; b--) {
+    acc = fp12_sqr(acc);
+    if ((r >> b) & 1u) acc = fp12_mul(acc, f);
+  }
+  fp12_to_canon_bytes(out576, acc);
+}
+
 // roofline probe: 4 independent limb-parallel Montgomery chains per pair
 __global__ void LSG_KERNEL_ATTR k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
   LANE_ITEM(n);
@@ -207,6 +226,9 @@ hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* 
 }
 hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out576) {
   LSG_LAUNCH_ITEMS(k_fp12_to_canon, n, st, n, in, out576);
+}
+hipError_t fp12_pow_u64(hipStream_t st, const uint8_t* in576, uint64_t r, uint8_t* out576) {
+  LSG_LAUNCH_ITEMS(k_fp12_pow_u64, 1, st, in576, r, out576);
 }
 hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io) {
   LSG_LAUNCH_ITEMS(k_probe_fp_mul, items, st, items, iters, io);

@@ -42,9 +42,9 @@ __global__ void LSG_KERNEL_ATTR k_sig_subgroup(int n, const uint32_t* __restrict
 // The point set i adds to its group's signature sum S_g = sum r_i sig_i: the identity for a
 // set that cannot contribute (undecodable or infinite signature, infinite aggregated key: the
 // verdict rules exclude such sets, lsg_host.hip), else sig_i (k_sig_proj: bucket MSM groups
-// scale later) or [r_i] sig_i (k_sig_scale, 4-bit windows: groups below the MSM threshold,
-// sets whose mode byte is set).  Two kernels, so that the MSM path never carries the scaled
-// path's window table (3 KB of scratch per lane).
+// scale later) or [r_i] sig_i (k_sig_scale3: groups below the MSM threshold, sets whose mode
+// byte is set).  Two kernels, so that the MSM path never carries the scaled path's window
+// table.
 LSG_DEVI bool sig_usable(size_t i, const uint8_t* inf, const int32_t* err, const uint8_t* pinf) {
   return err[i] == 0 && !inf[i] && !(pinf && pinf[i]);
 }
@@ -57,42 +57,22 @@ __global__ void LSG_KERNEL_ATTR k_sig_proj(int n, const uint32_t* __restrict__ s
   if (sig_usable(item, inf, err, pinf)) r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
   lane_store(out, item, r);
 }
-// Two forms of [r_i] sig_i: 4-bit windows (k_sig_scale: 62 doublings + 30 additions, the
-// per-lane table in scratch, 2 waves per SIMD) and signed 3-bit windows (k_sig_scale3: 65 + 22,
-// the table in 512 registers at 1 wave per SIMD, no scratch); LSG_SIG_SCALE=4 selects the first.
-template <int FORM>
-LSG_DEVI void sig_scale_item(size_t item, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
-                             const int32_t* __restrict__ err, const uint8_t* __restrict__ pinf,
-                             const uint64_t* __restrict__ rnd, const uint8_t* __restrict__ mode,
-                             uint32_t* __restrict__ out) {
-  if (mode && !mode[item]) return;  // a set of an MSM group: k_sig_proj wrote its point
-  g2p_t r = proj_inf<fp2_t>();
-  if (sig_usable(item, inf, err, pinf)) {
-    r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
-    if (rnd[item] != 0)  // r_i = 0: a set verified alone, not scaled
-      r = FORM == 0 ? proj_mul_u64(r, rnd[item]) : proj_mul_u64_s3(r, rnd[item]);
-  }
-  lane_store(out, item, r);
-}
-__global__ void LSG_KERNEL_ATTR k_sig_scale(int n, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
-                                            const int32_t* __restrict__ err, const uint8_t* __restrict__ pinf,
-                                            const uint64_t* __restrict__ rnd, const uint8_t* __restrict__ mode,
-                                            uint32_t* __restrict__ out) {
-  LANE_ITEM(n);
-  (void)lead;
-  sig_scale_item<0>(item, sig_aff, inf, err, pinf, rnd, mode, out);
-}
+// [r_i] sig_i with signed 3-bit windows (65 doublings + 22 additions, the window table in
+// 512 registers at 1 wave per SIMD, no scratch; 4-bit windows with the table in scratch were
+// measured slower: profiles/r03_*_scale3ab.json)
 __global__ void LSG_KERNEL_ATTR_W(1) k_sig_scale3(int n, const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ inf,
                                                   const int32_t* __restrict__ err, const uint8_t* __restrict__ pinf,
                                                   const uint64_t* __restrict__ rnd, const uint8_t* __restrict__ mode,
                                                   uint32_t* __restrict__ out) {
   LANE_ITEM(n);
   (void)lead;
-  sig_scale_item<1>(item, sig_aff, inf, err, pinf, rnd, mode, out);
-}
-static bool sig_scale_w4() {
-  const char* e = getenv("LSG_SIG_SCALE");
-  return e && e[0] == '4';
+  if (mode && !mode[item]) return;  // a set of an MSM group: k_sig_proj wrote its point
+  g2p_t r = proj_inf<fp2_t>();
+  if (sig_usable(item, inf, err, pinf)) {
+    r = proj_from_aff(lane_load<g2a_t>(sig_aff, item));
+    if (rnd[item] != 0) r = proj_mul_u64_s3(r, rnd[item]);  // r_i = 0: a set verified alone, not scaled
+  }
+  lane_store(out, item, r);
 }
 
 __global__ void LSG_KERNEL_ATTR k_g2a_to_bytes(int n, const uint32_t* __restrict__ pts, const uint8_t* __restrict__ inf,
@@ -180,7 +160,6 @@ hipError_t sig_prep(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_
 }
 hipError_t sig_scale_only(hipStream_t st, int n, const uint32_t* sig_aff, const uint8_t* inf, const int32_t* err,
                           const uint8_t* pinf, const uint64_t* rnd, const uint8_t* mode, uint32_t* out) {
-  if (sig_scale_w4()) LSG_LAUNCH_ITEMS(k_sig_scale, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
   LSG_LAUNCH_ITEMS(k_sig_scale3, n, st, n, sig_aff, inf, err, pinf, rnd, mode, out);
 }
 hipError_t g2a_to_bytes(hipStream_t st, int n, const uint32_t* pts, const uint8_t* inf, uint8_t* out192) {

@@ -21,17 +21,6 @@ LSG_ROW_DECL(lsg_row_miller_neg_g1, int ng, const uint8_t* S288, uint8_t* out576
 // out576[g] = ML(-G1, sum_k 2^k C_{g,k}) for ng groups of 64 canonical 288-byte projective G2
 // points each (the bucket MSM's per-bit sums): Horner and the Miller loop in one row chain
 LSG_ROW_DECL(lsg_row_horner_miller, int ng, const uint8_t* C288, uint8_t* out576)
-// The same stages on the pair backend (lsg_serial_pair.hip): _ps one group per wave with its
-// product batches split over the lane pairs (latency), _pw one group per lane pair (groups).
-#define LSG_PAIR_DECL(name, ...)                     \
-  hipError_t name##_ps(hipStream_t st, __VA_ARGS__); \
-  hipError_t name##_pw(hipStream_t st, __VA_ARGS__);
-LSG_PAIR_DECL(lsg_pair_final_exp, int ng, const uint8_t* F576, int32_t* verdict)
-LSG_PAIR_DECL(lsg_pair_miller_neg_g1, int ng, const uint8_t* S288, uint8_t* out576)
-LSG_PAIR_DECL(lsg_pair_horner_miller, int ng, const uint8_t* C288, uint8_t* out576)
-#ifndef LSG_PAIR_WIDE_MIN
-#define LSG_PAIR_WIDE_MIN 512
-#endif
 // The same stages as straight-line programs (lsg_slp.hip, tools/gen_slp.py): one group per
 // workgroup, each step's independent products spread over the lane pairs.
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict);
@@ -50,35 +39,30 @@ hipError_t lsg_slp_g2_scale(hipStream_t st, int n, const uint32_t* sig_aff, cons
 hipError_t lsg_slp_miller_items1(hipStream_t st, int n_items, const int32_t* item_first, const uint32_t* P,
                                  const uint8_t* pinf, const uint8_t* hinf, const int32_t* err, const uint32_t* H,
                                  uint32_t* f);
-// Default: the straight-line programs.  env LSG_SERIAL=row selects the row kernels, =pair
-// the pair kernels (A/B).  The pair kernels were measured slower than the rows -- final
-// exponentiation 9.3 ms against 4.0 ms for one group, 51 against 26 ms for a fallback phase's
-// thousands (profiles/r03_serial_pair_ab.txt): a pair Fp12 is 84 VGPRs (12 on a row), so the
-// exponentiation's live state spills around every product leaf call.
-#include <stdlib.h>
-#include <string.h>
-enum { LSG_SERIAL_SLP = 0, LSG_SERIAL_ROW = 1, LSG_SERIAL_PAIR = 2 };
-inline int lsg_serial_mode() {
-  static const int v = [] {
-    const char* e = getenv("LSG_SERIAL");
-    if (e && strcmp(e, "row") == 0) return (int)LSG_SERIAL_ROW;
-    if (e && strcmp(e, "pair") == 0) return (int)LSG_SERIAL_PAIR;
-    return (int)LSG_SERIAL_SLP;
-  }();
+// The straight-line programs run the serial stages.  The row kernels above are compiled only
+// into the A/B build (liblodestar_bls_ab.so, -DLSG_AB; lsg_ab.h), where env LSG_SERIAL=row
+// selects them; the shipped library has no runtime switch here.
+#include "lsg_ab.h"
+enum { LSG_SERIAL_SLP = 0, LSG_SERIAL_ROW = 1 };
+#ifdef LSG_AB
+static inline int lsg_serial_mode() {
+  static const int v = lsg_ab_str_is("LSG_SERIAL", "row") ? (int)LSG_SERIAL_ROW : (int)LSG_SERIAL_SLP;
   return v;
 }
-#define LSG_SERIAL_PICK(name, ng, ...)                                                                    \
-  (lsg_serial_mode() == LSG_SERIAL_SLP                                                                     \
-       ? lsg_slp_##name(__VA_ARGS__)                                                                       \
-       : lsg_serial_mode() == LSG_SERIAL_ROW                                                               \
-             ? ((ng) >= LSG_ROW_WIDE_MIN ? lsg_row_##name##_r1(__VA_ARGS__) : lsg_row_##name##_r4(__VA_ARGS__)) \
-             : ((ng) >= LSG_PAIR_WIDE_MIN ? lsg_pair_##name##_pw(__VA_ARGS__) : lsg_pair_##name##_ps(__VA_ARGS__)))
-inline hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
+#define LSG_SERIAL_PICK(name, ng, ...)                                                                  \
+  (lsg_serial_mode() == LSG_SERIAL_SLP                                                                   \
+       ? lsg_slp_##name(__VA_ARGS__)                                                                     \
+       : ((ng) >= LSG_ROW_WIDE_MIN ? lsg_row_##name##_r1(__VA_ARGS__) : lsg_row_##name##_r4(__VA_ARGS__)))
+#else
+static constexpr int lsg_serial_mode() { return LSG_SERIAL_SLP; }
+#define LSG_SERIAL_PICK(name, ng, ...) lsg_slp_##name(__VA_ARGS__)
+#endif
+static inline hipError_t lsg_row_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   return LSG_SERIAL_PICK(final_exp, ng, st, ng, F576, verdict);
 }
-inline hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
+static inline hipError_t lsg_row_miller_neg_g1(hipStream_t st, int ng, const uint8_t* S288, uint8_t* out576) {
   return LSG_SERIAL_PICK(miller_neg_g1, ng, st, ng, S288, out576);
 }
-inline hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
+static inline hipError_t lsg_row_horner_miller(hipStream_t st, int ng, const uint8_t* C288, uint8_t* out576) {
   return LSG_SERIAL_PICK(horner_miller, ng, st, ng, C288, out576);
 }

@@ -348,12 +348,8 @@ hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, 
 
 // Two waves per item (steps of 64 operations, each wave on its own SIMD) while the items fit
 // the chip one wave per SIMD; one wave per item beyond (a fallback phase's thousands of
-// groups: throughput).  env LSG_SLP_W2_MAX (default 512).
-static int slp_waves(int n) {
-  const char* e = getenv("LSG_SLP_W2_MAX");
-  const int lim = e ? atoi(e) : 512;
-  return n <= lim ? 2 : 1;
-}
+// groups: throughput).
+static int slp_waves(int n) { return n <= 512 ? 2 : 1; }
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   return slp_waves(ng) == 2 ? launch<SLP_FE, 2, 0>(st, ng, F576, 576, nullptr, verdict)
                             : launch<SLP_FE, 1, 0>(st, ng, F576, 576, nullptr, verdict);

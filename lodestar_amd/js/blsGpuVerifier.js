@@ -147,6 +147,27 @@ function serializeSet(set) {
   return {pubkeys, message: set.signingRoot, signature: set.signature};
 }
 
+/**
+ * verifySignatureSetsMaybeBatch(sets) (maybeBatch.ts:16-39) as ONE non-batchable job sent
+ * straight to the addon, outside the queue and ahead of it: verifyPacked's priority flag runs it
+ * on the addon's priority thread (never behind the package threads' queue) and on the
+ * library's high-priority streams.  The reference runs this path synchronously on the main
+ * thread (multithread/index.ts:155-168, ~0.9 ms of blst); here the caller's promise settles
+ * with the verdict and the JS thread keeps running meanwhile.  No retry: one job is one
+ * maybeBatch call; an error rejects with its BLST code (e.g. BLST_INVALID_SIZE).
+ */
+async function verifyDirect(addon, ctx, sets, seed) {
+  const block = new VerdictBlock(false, false);
+  block.add(sets, true);
+  block.seal();
+  const pkg = packBlocks([block], sets.length, undefined);
+  if (pkg.jobBlock.length === 1) {
+    const r = await addon.verifyPacked(ctx, pkg.arena, pkg.setDesc, pkg.jobDesc, seed, true);
+    block.settle(0, r.status[0], r.errCode[0]);
+  }
+  return block.verdict(0);
+}
+
 /** utils.ts:19-26 */
 function getAggregatedPubkeysCount(sets) {
   let n = 0;
@@ -519,16 +540,12 @@ class BlsGpuVerifier {
       if (this.metrics && this.metrics.bls) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
 
       if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
-        // verifySignatureSetsMaybeBatch on the calling thread: no retry, errors propagate
+        // verifySignatureSetsMaybeBatch without the queue: no retry, errors reject
         const m = this.metrics && this.metrics.blsThreadPool;
         const timer = m ? m.mainThreadDurationInThreadPool.startTimer() : null;
-        try {
-          const r = this.addon.verifySets(this.ctx, sets.map(serializeSet), this.seed);
-          if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
-          return Promise.resolve(r.status === LSG_VALID);
-        } finally {
-          if (timer) timer();
-        }
+        const p = verifyDirect(this.addon, this.ctx, sets, this.seed);
+        if (timer) p.then(timer, timer);
+        return p;
       }
 
       for (let i = 0; i < sets.length; i++) checkSet(sets[i]);
@@ -756,10 +773,11 @@ class BlsGpuVerifier {
 
 /**
  * BlsSingleThreadVerifier (chain/bls/singleThread.ts:14-35) on the GPU: each call is one
- * verifySignatureSetsMaybeBatch (lsg_verify_sets) made synchronously from the calling thread,
- * with no queue and no retry; opts are ignored, errors propagate as throws.  The duration is
- * observed after the call as the reference does (it observes the total and the per-set time;
- * its startNs - endNs has the sign inverted, here the duration is positive).
+ * verifySignatureSetsMaybeBatch (verifyDirect: one priority job, no queue) with no retry; opts
+ * are ignored, errors reject.  The reference blocks the event loop for the call; here the
+ * promise settles when the GPU answers.  The duration is observed after the call as the
+ * reference does (it observes the total and the per-set time; its startNs - endNs has the
+ * sign inverted, here the duration is positive).
  */
 class BlsGpuSingleThreadVerifier {
   /**
@@ -775,11 +793,9 @@ class BlsGpuSingleThreadVerifier {
 
   async verifySignatureSets(sets) {
     if (this.metrics && this.metrics.bls) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
-    const setsAggregated = sets.map(serializeSet);
-    // Count time after aggregating
+    // Count time after aggregating (serialisation happens inside verifyDirect)
     const startNs = process.hrtime.bigint();
-    const r = this.addon.verifySets(this.ctx, setsAggregated, this.seed);
-    if (r.status === LSG_ERROR) throw Error(errorMessage(r.errCode));
+    const valid = await verifyDirect(this.addon, this.ctx, sets, this.seed);
     // Don't use a try/catch, only count run without exceptions
     const endNs = process.hrtime.bigint();
     const totalSec = Number(endNs - startNs) / 1e9;
@@ -788,7 +804,7 @@ class BlsGpuSingleThreadVerifier {
       m.mainThreadDurationInThreadPool.observe(totalSec);
       m.mainThreadDurationInThreadPool.observe(totalSec / sets.length);
     }
-    return r.status === LSG_VALID;
+    return valid;
   }
 
   async close() {

@@ -20,12 +20,13 @@
  *   close(ctx)                              lsg_destroy
  *   slots(ctx) -> n                         packages in flight: min(lsg_pipeline_slots, 16 threads)
  *   deviceName(ctx) -> string               lsg_device_name
- *   verifyPacked(ctx, arena, setDesc, jobDesc, seed) -> Promise<{status: Uint8Array,
+ *   verifyPacked(ctx, arena, setDesc, jobDesc, seed[, priority]) -> Promise<{status: Uint8Array,
  *       errCode: Int32Array, batchRetries, batchSigsSuccess, startNs, endNs, finalExps,
  *       submitUs, keyError, workerId}>     lsg_submit_jobs + lsg_wait_jobs on a package thread
  *       (layout below, at js_verify_packed).  startNs / endNs are CLOCK_MONOTONIC nanoseconds
  *       (process.hrtime.bigint()'s clock); workerId is the pipeline slot that ran the package
- *       (the reference's workerId label)
+ *       (the reference's workerId label).  priority = true (verifyOnMainThread): the package
+ *       goes ahead of every queued one, onto the addon's priority thread
  *   sign(ctx, sks, msgs) / skToPk(ctx, sks)  test and bench input generation
  *   verifySets(ctx, sets, seed) -> {status, errCode}                   lsg_verify_sets
  *   aggregatePubkeys(ctx, pubkeys[]) -> {errCode, bytes: Uint8Array(96)} lsg_aggregate_pubkeys
@@ -314,17 +315,27 @@ typedef struct pkg_req {
   char err[320];
 } pkg_req;
 
+typedef struct addon_ctx addon_ctx;
 typedef struct {
+  addon_ctx* a;
+  int prio_only; /* the priority thread: serves only the priority queue */
+} engine_arg;
+
+struct addon_ctx {
   lsg_ctx* c;
-  /* engine (started by the first verifyPacked) */
+  /* engine (started by the first verifyPacked): LSG_NAPI_THREADS package threads plus one
+   * priority thread, so that a priority package (verifyOnMainThread) never waits for a
+   * package thread blocked on an earlier package */
   int started, stop, n_threads;
-  pthread_t th[LSG_NAPI_THREADS];
+  pthread_t th[LSG_NAPI_THREADS + 1];
+  engine_arg targ[LSG_NAPI_THREADS + 1];
   pthread_mutex_t mu;
   pthread_cond_t cv;
-  pkg_req *head, *tail;
+  pkg_req *head, *tail;   /* packages, FIFO */
+  pkg_req *phead, *ptail; /* priority packages, FIFO, served first by every thread */
   napi_threadsafe_function tsfn;
   uint32_t pending; /* promises not yet settled (JS thread only) */
-} addon_ctx;
+};
 
 static addon_ctx* get_actx(napi_env env, napi_value v) {
   void* p = NULL;
@@ -381,17 +392,24 @@ static int build_jobs(pkg_req* r, lsg_set** sets_out, lsg_job** jobs_out) {
 }
 
 static void* engine_main(void* arg) {
-  addon_ctx* a = (addon_ctx*)arg;
+  addon_ctx* a = ((engine_arg*)arg)->a;
+  const int prio_only = ((engine_arg*)arg)->prio_only;
   for (;;) {
     pthread_mutex_lock(&a->mu);
-    while (!a->head && !a->stop) pthread_cond_wait(&a->cv, &a->mu);
-    pkg_req* r = a->head;
+    while (!a->phead && (prio_only || !a->head) && !a->stop) pthread_cond_wait(&a->cv, &a->mu);
+    pkg_req* r = a->phead;
+    if (r) {
+      a->phead = r->next;
+      if (!a->phead) a->ptail = NULL;
+    } else if (!prio_only && a->head) {
+      r = a->head;
+      a->head = r->next;
+      if (!a->head) a->tail = NULL;
+    }
     if (!r) { /* stopping and drained */
       pthread_mutex_unlock(&a->mu);
       break;
     }
-    a->head = r->next;
-    if (!a->head) a->tail = NULL;
     pthread_mutex_unlock(&a->mu);
     lsg_set* sets = NULL;
     lsg_job* jobs = NULL;
@@ -467,9 +485,13 @@ static int engine_start(napi_env env, addon_ctx* a) {
   pthread_cond_init(&a->cv, NULL);
   int32_t slots = LSG_NAPI_THREADS;
   lsg_pipeline_slots(a->c, &slots);
-  a->n_threads = slots < LSG_NAPI_THREADS ? slots : LSG_NAPI_THREADS;
+  a->n_threads = (slots < LSG_NAPI_THREADS ? slots : LSG_NAPI_THREADS) + 1;
   a->started = 1;
-  for (int i = 0; i < a->n_threads; i++) pthread_create(&a->th[i], NULL, engine_main, a);
+  for (int i = 0; i < a->n_threads; i++) {
+    a->targ[i].a = a;
+    a->targ[i].prio_only = i == a->n_threads - 1;
+    pthread_create(&a->th[i], NULL, engine_main, &a->targ[i]);
+  }
   return 0;
 }
 
@@ -498,8 +520,8 @@ static int typed_info(napi_env env, napi_value v, napi_typedarray_type want, voi
 }
 
 static napi_value js_verify_packed(napi_env env, napi_callback_info info) {
-  size_t argc = 5;
-  napi_value argv[5];
+  size_t argc = 6;
+  napi_value argv[6];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   addon_ctx* a = get_actx(env, argv[0]);
   if (!a) return NULL;
@@ -513,6 +535,8 @@ static napi_value js_verify_packed(napi_env env, napi_callback_info info) {
   }
   double seedd = 0;
   if (argc >= 5) napi_get_value_double(env, argv[4], &seedd);
+  bool prio = false;
+  if (argc >= 6) napi_get_value_bool(env, argv[5], &prio);
   if (engine_start(env, a)) {
     napi_throw_error(env, NULL, "lsg_napi: could not start the package threads");
     return NULL;
@@ -531,12 +555,21 @@ static napi_value js_verify_packed(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_create_promise(env, &r->deferred, &promise));
   if (a->pending++ == 0) napi_ref_threadsafe_function(env, a->tsfn);
   pthread_mutex_lock(&a->mu);
-  if (a->tail)
-    a->tail->next = r;
-  else
-    a->head = r;
-  a->tail = r;
-  pthread_cond_signal(&a->cv);
+  if (prio) {
+    if (a->ptail)
+      a->ptail->next = r;
+    else
+      a->phead = r;
+    a->ptail = r;
+    pthread_cond_broadcast(&a->cv); /* the priority thread may be the only one free */
+  } else {
+    if (a->tail)
+      a->tail->next = r;
+    else
+      a->head = r;
+    a->tail = r;
+    pthread_cond_signal(&a->cv);
+  }
   pthread_mutex_unlock(&a->mu);
   return promise;
 }

@@ -35,6 +35,8 @@ function unpack(arena, setDesc, jobDesc) {
 function mockAddon(slots = 2, {holdWaits = false} = {}) {
   const m = {
     packages: [],
+    priorityPackages: [],
+    pendingPriority: 0,
     syncCalls: 0,
     opened: 0,
     closed: 0,
@@ -70,13 +72,19 @@ function mockAddon(slots = 2, {holdWaits = false} = {}) {
       }
       return {status: ok ? 1 : 0, errCode: 0};
     },
-    verifyPacked(ctx, arena, setDesc, jobDesc, seed) {
-      // the engine runs at most `slots` packages at once (one package thread each)
-      if (m.pending.length >= slots) throw Error("mock: more packages in flight than package threads");
+    verifyPacked(ctx, arena, setDesc, jobDesc, seed, priority) {
+      // the engine runs at most `slots` packages at once (one package thread each), plus
+      // priority packages on its priority thread
       const jobs = unpack(arena, setDesc, jobDesc);
-      m.packages.push(jobs);
-      const t = {ticket: m.packages.length, jobs};
+      if (priority) {
+        m.priorityPackages.push(jobs);
+      } else {
+        if (m.pending.length - m.pendingPriority >= slots) throw Error("mock: more packages in flight than package threads");
+        m.packages.push(jobs);
+      }
+      const t = {ticket: m.packages.length, jobs, priority: !!priority};
       m.pending.push(t);
+      if (priority) m.pendingPriority++;
       const vs = jobs.map((j) => m.jobVerdict(j.sets));
       // GPU package start/end on process.hrtime's clock (lsg_stats is CLOCK_MONOTONIC)
       const startNs = Number(process.hrtime.bigint());
@@ -91,6 +99,7 @@ function mockAddon(slots = 2, {holdWaits = false} = {}) {
       };
       const finish = () => {
         m.pending.splice(m.pending.indexOf(t), 1);
+        if (t.priority) m.pendingPriority--;
         return done;
       };
       if (!holdWaits) return new Promise((r) => setTimeout(() => r(finish()), 1));
@@ -248,21 +257,58 @@ test("aggregate sets send every pubkey (summed on the GPU, utils.ts:11)", async 
   await pool.close();
 });
 
-test("verifyOnMainThread runs synchronously through verifySets and throws errors (index.ts:155-168)", async () => {
+test("verifyOnMainThread: one priority job outside the queue, no retry, errors reject (index.ts:155-168)", async () => {
   const a = mockAddon();
   const pool = new V.BlsGpuVerifier({}, {addon: a});
   assert.strictEqual(await pool.verifySignatureSets([set(1), set(2)], {verifyOnMainThread: true}), true);
-  assert.strictEqual(a.syncCalls, 1);
+  assert.strictEqual(a.syncCalls, 0);
   assert.strictEqual(a.packages.length, 0);
+  assert.strictEqual(a.priorityPackages.length, 1);
+  // one non-batchable priority job holding both sets: maybeBatch over them (no retry)
+  assert.strictEqual(a.priorityPackages[0].length, 1);
+  assert.strictEqual(a.priorityPackages[0][0].sets.length, 2);
+  assert.strictEqual(a.priorityPackages[0][0].flags, 2 /* LSG_JOB_PRIORITY, not batchable */);
+  assert.strictEqual(await pool.verifySignatureSets([set(3, false)], {verifyOnMainThread: true}), false);
   const bad = Object.assign({}, set(1), {signature: new Uint8Array(10)});
   await assert.rejects(pool.verifySignatureSets([bad], {verifyOnMainThread: true}), /BLST_INVALID_SIZE/);
-  assert.strictEqual(a.syncCalls, 2);
+  await assert.rejects(pool.verifySignatureSets([], {verifyOnMainThread: true}), /Empty signature set/);
+  assert.strictEqual(a.syncCalls, 0);
   // blsVerifyAllMultiThread forces the queue path
   const pool2 = new V.BlsGpuVerifier({blsVerifyAllMultiThread: true}, {addon: a});
   assert.strictEqual(await pool2.verifySignatureSets([set(1)], {verifyOnMainThread: true}), true);
-  assert.strictEqual(a.syncCalls, 2);
+  assert.strictEqual(a.packages.length, 1);
   await pool.close();
   await pool2.close();
+});
+
+test("verifyOnMainThread does not block the event loop: setImmediate fires while it is pending (VERDICT r3 4)", async () => {
+  const a = mockAddon(2, {holdWaits: true});
+  const pool = new V.BlsGpuVerifier({}, {addon: a});
+  let settled = false;
+  const p = pool.verifySignatureSets([set(1)], {verifyOnMainThread: true}).then((v) => {
+    settled = true;
+    return v;
+  });
+  let immediate = false;
+  await new Promise((r) => setImmediate(() => {
+    immediate = true;
+    r();
+  }));
+  assert.strictEqual(immediate, true);
+  assert.strictEqual(settled, false); // the GPU has not answered: the JS thread kept running
+  assert.strictEqual(a.pending.length, 1);
+  // it overtakes a full pool: both package threads busy with held packages
+  const q1 = pool.verifySignatureSets([set(2)]);
+  const q2 = pool.verifySignatureSets([set(3)]);
+  await sleep(5);
+  a.pending[0].release();
+  assert.strictEqual(await p, true);
+  while (a.pending.length) {
+    a.pending[0].release();
+    await sleep(2);
+  }
+  assert.deepStrictEqual(await Promise.all([q1, q2]), [true, true]);
+  await pool.close();
 });
 
 test("canAcceptWork: back-pressure on sets pending (queued + buffered + in flight) (index.ts:143-149)", async () => {
@@ -449,7 +495,8 @@ test("BlsGpuSingleThreadVerifier: one maybeBatch per call, no retry, throws (sin
   const bad = set(2);
   bad.signature = new Uint8Array(32);
   await assert.rejects(v.verifySignatureSets([bad]), /BLST_INVALID_SIZE/);
-  assert.strictEqual(a.syncCalls, 3);
+  assert.strictEqual(a.syncCalls, 0);
+  assert.strictEqual(a.priorityPackages.length, 3, "one priority job per call");
   assert.strictEqual(a.packages.length, 0, "no queue, no worker packages");
   assert.strictEqual(rec.mainThreadDurationInThreadPool.length, 4, "total and per-set time of the two successful calls");
   assert.ok(rec.mainThreadDurationInThreadPool.every((x) => x >= 0));

@@ -200,10 +200,11 @@ def test_config_e_adversarial_4096(ctx, keys):
     check_against_oracle(ctx, jobs, per[:pos])
 
 
-def test_package_group_matches_chunk_mode(ctx, keys, monkeypatch):
+def test_package_group_matches_chunk_mode(ab_ctx, keys, monkeypatch):
     """The one-group phase A (default) and the reference's chunk-16 phase A
-    (LSG_PACKAGE_GROUP=0) give identical per-job verdicts AND batch_retries /
+    (LSG_PACKAGE_GROUP=0, A/B build) give identical per-job verdicts AND batch_retries /
     batch_sigs_success, on a valid and on an adversarial package."""
+    ctx = ab_ctx
     sets = single_sets(ctx, keys, b"modes", 600)
     bad, _ = corrupt(ctx, keys, sets, 0.02, 3)
     for pkg in (sets, bad):
@@ -276,6 +277,15 @@ def test_multi_device_context_duplicate_ids(keys):
         good = [([s], 1) for s in sets]
         g, st = c2.verify_jobs(good)
         assert g == [(1, 0)] * 512 and st["batch_retries"] == 0
+        # the node check over both devices' partials decides -- ONE final
+        # exponentiation for a passing package (the devices' own checks are not launched)
+        assert st["n_final_exps"] == 1, st
+        # a lone batchable set per device: both randomised (a multi-device partial leaves its
+        # slot), and an offset forgery split over the two devices is still rejected
+        from tests.test_gpu_parity import _offset_pair
+        fa, fb = _offset_pair(940, "multi-offs")
+        g, st = c2.verify_jobs([([fa], 1), ([fb], 1)])
+        assert g == [(0, 0), (0, 0)], (g, st)
     finally:
         c2.close()
         c1.close()
@@ -283,18 +293,20 @@ def test_multi_device_context_duplicate_ids(keys):
 
 def test_rccl_exchange_single_device(keys, monkeypatch):
     """The RCCL all-gather path of lsg_init_devices exercised on one GPU
-    (LSG_FORCE_EXCHANGE=1: a one-rank communicator, the node check on the gathered partial)."""
-    from lodestar_amd._native import Context
+    (LSG_FORCE_EXCHANGE=1, A/B build: a one-rank communicator, the node check on the gathered
+    partial, which decides: a passing package runs ONE final exponentiation, the node's)."""
+    from lodestar_amd._native import AB_LIB_PATH, Context
     monkeypatch.setenv("LSG_FORCE_EXCHANGE", "1")
-    c = Context(devices=[0])
+    c = Context(devices=[0], lib=AB_LIB_PATH)
     try:
         sets = single_sets(c, keys, b"rccl", 256)
         bad = list(sets)
         bad[5] = bd.corrupt_wrong_message(bad[5])
         g, st = c.verify_jobs([([s], 1) for s in sets])
-        assert g == [(1, 0)] * 256 and st["n_final_exps"] == 2  # package FE + node FE
+        assert g == [(1, 0)] * 256 and st["n_final_exps"] == 1  # the node FE only
         g, st = c.verify_jobs([([s], 1) for s in bad])
         assert [x[0] for x in g] == [0 if i == 5 else 1 for i in range(256)]
+        assert st["n_final_exps"] >= 2  # node check failed: the device's own check localises
     finally:
         c.close()
 
@@ -302,7 +314,8 @@ def test_rccl_exchange_single_device(keys, monkeypatch):
 # ---- the fused Miller kernel (lines in LDS, four waves per item) and the one-set straight-line
 # program items against the split kernels
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 37, 300])
-def test_fused_miller_matches_split(ctx, keys, n, monkeypatch):
+def test_fused_miller_matches_split(ab_ctx, keys, n, monkeypatch):
+    ctx = ab_ctx  # (A/B build: LSG_MILLER_FUSED, LSG_SLP_ITEMS)
     sets = single_sets(ctx, keys, b"fused", n)
     monkeypatch.setenv("LSG_MILLER_FUSED", "0")
     split, _, _ = ctx.batch_partial(sets, seed=11)

@@ -171,14 +171,16 @@ def test_adversarial_jobs_match_oracle(ctx):
 
 
 @pytest.mark.parametrize("agg", ["0", "1"])
-def test_shared_messages_match_oracle(ctx, monkeypatch, agg):
+def test_shared_messages_match_oracle(ctx, ab_ctx, monkeypatch, agg):
     """Sets that sign one message (a committee's attestations) share one hash_to_G2 per
     package (stage_sets message table, k_h2c_gather) and, with LSG_MSG_AGG=1, one Miller pair
     (the masked sum of their scaled keys): verdicts, errors and counters stay the oracle's,
     with corrupted sets inside the shared groups and sets whose corruption gives them a
     message of their own."""
     import random
-    monkeypatch.setenv("LSG_MSG_AGG", agg)
+    if agg == "0":  # one Miller pair per set: the A/B build's LSG_MSG_AGG=0
+        monkeypatch.setenv("LSG_MSG_AGG", agg)
+        ctx = ab_ctx
     rng = random.Random(5)
     msgs = [bd.msg("committee", c) for c in range(3)]
     sets = []
@@ -217,6 +219,49 @@ def test_batch_partial_and_final_verify(ctx):
     p3, _, _ = ctx.batch_partial(bad, seed=2)
     assert not ctx.final_verify([p1, p3])
     assert ctx.final_verify([p1]) and not ctx.final_verify([p3])
+
+
+def _offset_pair(i, tag):
+    """Two sets whose signatures are sig_a + D and sig_b - D (D in G2): each one invalid, their
+    unrandomised sum valid -- the forgery an exported partial without RLC would pass."""
+    from oracle.curves import E2, G2_GEN, g2_compress, g2_uncompress
+    a, b = bd.single_set(i, tag=tag), bd.single_set(i + 1, tag=tag)
+    D = E2.mul(G2_GEN, 123456789)
+    sa = E2.add(g2_uncompress(a[2]), D)
+    sb = E2.add(g2_uncompress(b[2]), E2.neg(D))
+    return (a[0], a[1], g2_compress(sa)), (b[0], b[1], g2_compress(sb))
+
+
+def test_one_set_shards_offset_forgery_rejected(ctx):
+    """a one-set shard's exported partial keeps a random RLC coefficient.
+    Two shards holding sig_a + D and sig_b - D: every local check fails, and so must the
+    product of their partials -- through lsg_batch_partial and through lsg_jobs_partial(_device)
+    (a lone batchable set is verified unscaled inside its package, and its partial leaves the
+    slot raised to a fresh randomizer)."""
+    fa, fb = _offset_pair(880, "offs")
+    pa, _, ea = ctx.batch_partial([fa], seed=5)
+    pb, _, eb = ctx.batch_partial([fb], seed=6)
+    assert not ea and not eb
+    assert not ctx.final_verify([pa]) and not ctx.final_verify([pb])
+    assert not ctx.final_verify([pa, pb])
+    # the jobs path: each package one batchable single-set job (the lone-set shortcut)
+    parts = []
+    for s in (fa, fb):
+        t = ctx.submit_jobs([([s], 1)])
+        part, has = ctx.jobs_partial(t)
+        assert has
+        parts.append(part)
+        got, _ = ctx.wait_jobs(t)
+        assert got == [(0, 0)]
+    assert not ctx.final_verify(parts)
+    # valid lone sets still pass through the randomised export
+    va, vb = bd.single_set(890, tag="offs"), bd.single_set(891, tag="offs")
+    parts = []
+    for s in (va, vb):
+        t = ctx.submit_jobs([([s], 1)])
+        parts.append(ctx.jobs_partial(t)[0])
+        assert ctx.wait_jobs(t)[0] == [(1, 0)]
+    assert ctx.final_verify(parts)
 
 
 def test_probe_rate_positive(ctx):
@@ -379,9 +424,11 @@ def _f12_bytes(f):
     return b"".join(int(c[0]).to_bytes(48, "big") + int(c[1]).to_bytes(48, "big") for c in f12_coeffs(f))
 
 
-def test_msm_signature_sums_match_scalar_path(ctx, monkeypatch):
+def test_msm_signature_sums_match_scalar_path(ab_ctx, monkeypatch):
     """Bucket MSM vs per-set [r_i] sig_i for the package group's signature sum: identical
-    partials, including an infinite and an undecodable signature (identity contributions)."""
+    partials, including an infinite and an undecodable signature (identity contributions).
+    (A/B build: LSG_MSM_MIN_GROUP.)"""
+    ctx = ab_ctx
     sets = [bd.single_set(700 + i, tag="msm") for i in range(40)]
     sets[5] = bd.corrupt_infinity(sets[5])
     sets[22] = bd.corrupt_truncate(sets[22])
@@ -396,9 +443,10 @@ def test_msm_signature_sums_match_scalar_path(ctx, monkeypatch):
     assert not ctx.final_verify([out["msm"]])  # 5: infinity sig; 31: wrong msg
 
 
-def test_batch_partial_bit_exact_vs_oracle(ctx, monkeypatch):
+def test_batch_partial_bit_exact_vs_oracle(ab_ctx, monkeypatch):
     """The per-shard Miller product (SURVEY 8e partial) equals the oracle's, byte for byte,
-    with the same randomizers, through the MSM signature sum."""
+    with the same randomizers, through the MSM signature sum (A/B build: LSG_MSM_MIN_GROUP)."""
+    ctx = ab_ctx
     monkeypatch.setenv("LSG_MSM_MIN_GROUP", "1")
     sets = [bd.single_set(760 + i, tag="msm") for i in range(7)]
     sets[2] = bd.corrupt_infinity(sets[2])
