@@ -568,7 +568,9 @@ static napi_value js_verify_packed(napi_env env, napi_callback_info info) {
     else
       a->head = r;
     a->tail = r;
-    pthread_cond_signal(&a->cv);
+    /* broadcast, not signal: one wakeup could go to the priority thread, which does not
+     * take this package, and the package threads would sleep on */
+    pthread_cond_broadcast(&a->cv);
   }
   pthread_mutex_unlock(&a->mu);
   return promise;
