@@ -68,7 +68,7 @@ class Workload:
     """Builds the distinct packages of one workload: .packages = list of (jobs, expected)
     with expected = per-job (status, code) or None (all valid)."""
 
-    def __init__(self, ctx, name, rank, sets_per_step, n_packages):
+    def __init__(self, ctx, name, rank, sets_per_step, n_packages, blocks=64):
         from lodestar_amd._native import PkIndices
         self.name = name
         sks = [interop_sk(i) for i in range(N_KEYS)]
@@ -101,7 +101,7 @@ class Workload:
             errs = ctx.pubkey_table_set(0, pks)
             if any(errs):
                 raise SystemExit("pubkey table load failed")
-            blocks, per_block = 64, 128
+            per_block = 128
             for p in range(n_packages):
                 jobs, npk = [], 0
                 for b in range(blocks):
@@ -335,6 +335,7 @@ def main():
                     default="jobs")
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
+    ap.add_argument("--blocks", type=int, default=64, help="block workload: blocks (128-set jobs) per package")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
@@ -380,7 +381,7 @@ def main():
         ctx = Context(devices=list(range(args.devices)))
     else:
         ctx = Context(local)
-    wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages)
+    wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages, blocks=args.blocks)
     prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
     n_sets = wl.sets_per_package
     max_pks = int(n_sets * wl.pks_per_set) + 1
@@ -592,7 +593,7 @@ def main():
                     "single-pubkey gossip sets, one batchable job each, through lsg_submit_jobs/lsg_wait_jobs",
             "adversarial": "adversarial (SURVEY 8d config E): the firehose package with 1% corrupted sets, "
                            "batch failure + chunk/per-job retry, every verdict checked",
-            "block": "block-body (SURVEY 8d config C): 64 blocks per package, each a non-batchable job of 128 "
+            "block": f"block-body (SURVEY 8d config C): {args.blocks} blocks per package, each a non-batchable job of 128 "
                      "aggregate sets of 440-460 signers named by index into the device pubkey table",
             "sync": "sync-committee contributions (SURVEY 8d config B): 256 batchable jobs per package, each one "
                     "512-signer aggregate set (keys by index)",

@@ -216,6 +216,13 @@ int lsg_verify_sets(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint64_t s
  * pk_len == LSG_PK_INDEX, pks holds n uint32 indices into the pubkey table. */
 int lsg_aggregate_pubkeys(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, size_t n, uint8_t* out96,
                           int32_t* err_code);
+/* PublicKey.aggregate for n_sets sets in one device pass (utils.ts:11 getAggregatedPubkey over
+ * a block's aggregate sets, indexedAttestation.ts:21-47): set i's keys are sets[i].pks /
+ * pk_len / n_pks (bytes or table indices; msg and sig are ignored).  out96[96 i..] = set i's
+ * uncompressed sum; err[i] = its first bad key's BLST_* / LSG_ERR_BAD_INDEX, or
+ * LSG_ERR_EMPTY_AGGREGATE for no keys.  Large inputs (>= 32768 keys) run the batch-affine
+ * aggregation tree of the jobs path, smaller ones its serial fold. */
+int lsg_aggregate_pubkeys_multi(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint8_t* out96, int32_t* err);
 
 /* hash_to_G2(msg_i, DST) for n messages of msg_len bytes each -> n x 192-byte uncompressed points. */
 int lsg_hash_to_g2(lsg_ctx* ctx, const uint8_t* msgs, uint32_t msg_len, size_t n, const uint8_t* dst,

@@ -102,7 +102,7 @@ EXPORTS = [
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
     "lsg_signing_roots", "lsg_attestation_signing_roots", "lsg_jobs_partial_device", "lsg_final_submit_device",
-    "lsg_set_coalesce",
+    "lsg_set_coalesce", "lsg_aggregate_pubkeys_multi",
 ]
 
 
@@ -135,6 +135,7 @@ def load_library(path=LIB_PATH):
                                         ctypes.POINTER(LsgStats)]
         lib.lsg_verify_sets.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.POINTER(LsgJobResult)]
         lib.lsg_aggregate_pubkeys.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
+        lib.lsg_aggregate_pubkeys_multi.argtypes = [vp, ctypes.POINTER(LsgSet), sz, ctypes.c_char_p, pi32]
         lib.lsg_hash_to_g2.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, u32, ctypes.c_char_p]
         lib.lsg_sig_decode.argtypes = [vp, ctypes.c_char_p, u32, sz, ctypes.c_char_p, pi32]
         lib.lsg_batch_partial.argtypes = [vp, ctypes.POINTER(LsgSet), sz, u64, ctypes.c_char_p, pi32, pi32]
@@ -435,6 +436,18 @@ class Context:
         self._check(self.lib.lsg_aggregate_pubkeys(self.h, pkb, pk_len, len(pks), out, ctypes.byref(err)),
                     "lsg_aggregate_pubkeys")
         return out.raw, err.value
+
+    def aggregate_pubkeys_multi(self, key_lists):
+        """PublicKey.aggregate for every list of keys (encoded bytes, or PkIndices) in one device
+        pass: [(uncompressed 96 B, BLST / LSG error code)] per list."""
+        n = len(key_lists)
+        if n == 0:
+            return []
+        b = SetBuffer([(k, b"", b"") for k in key_lists])
+        out = ctypes.create_string_buffer(96 * n)
+        err = (ctypes.c_int32 * n)()
+        self._check(self.lib.lsg_aggregate_pubkeys_multi(self.h, b.arr, n, out, err), "lsg_aggregate_pubkeys_multi")
+        return [(out.raw[96 * i:96 * i + 96], err[i]) for i in range(n)]
 
     def pubkey_table_set(self, first_index, pks):
         """index2pubkey[first_index + k] = pks[k] on the device; returns per-key BLST codes."""

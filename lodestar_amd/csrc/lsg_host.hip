@@ -287,6 +287,24 @@ struct PhasePlan {
   size_t n_magg = 0, magg_off = 0, n_set_items = 0;
 };
 
+// PublicKey.aggregate as the batch-affine pairwise tree (lsg_k_pk.hip k_agg_*): per level, the
+// participating segments' plan (cum, in_off, len, out_off in the plan arena), the level's item
+// count and chunk size T, and the level's input / output bases in the point arena
+struct AggLevelPlan {
+  size_t plan_off = 0;
+  int n_seg = 0, n_items = 0, T = 1;
+  size_t base_in = 0, base_out = 0;
+};
+struct AggPlan {
+  bool tree = false;
+  std::vector<AggLevelPlan> levels;
+  size_t src_off = 0;    // per set (base, off, len) of its remaining points (k_agg_final)
+  size_t n_points = 0;   // points over all levels (arena size)
+  size_t max_items = 0;  // largest level
+};
+constexpr int AGG_FINAL_MAX = 8;          // a segment of at most this many points is summed directly
+constexpr size_t AGG_TREE_MIN_KEYS = 32768;  // smaller packages: the serial fold + butterfly
+
 struct JobRec {
   size_t first = 0, count = 0;  // staged set range
   uint32_t flags = 0;
@@ -337,7 +355,9 @@ struct Slot {
   HostBuf h_plan;
   DevBuf d_plan;
   PhasePlan phA;   // phase A: the package group + non-batchable jobs
-  SegPlan pkagg;   // pubkey aggregation of multi-key sets
+  SegPlan pkagg;   // pubkey aggregation of multi-key sets (small packages)
+  AggPlan agg;     // ... and as the batch-affine tree (large packages)
+  DevBuf d_agga, d_aggi, d_aggpre, d_aggtot, d_aggtinv;
   SegPlan phA_node;  // device 0 of a multi-device ticket: product of the gathered partials
   HostBuf h_mode;  // per-set sig_prep modes of a phase
   // pinned result mirrors
@@ -584,7 +604,8 @@ void slot_destroy(Slot* s) {
                     &s->binv_lv[1], &s->binv_iv[0], &s->binv_iv[1], &s->d_lines, &s->d_S, &s->d_F, &s->d_verdict,
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
                     &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm,
-                    &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm, &s->d_xport};
+                    &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm, &s->d_xport,
+                    &s->d_agga, &s->d_aggi, &s->d_aggpre, &s->d_aggtot, &s->d_aggtinv};
   for (DevBuf* b : bufs) free_dev(*b);
   for (auto& u : s->seg_tmp)
     for (DevBuf& b : u) free_dev(b);
@@ -674,6 +695,10 @@ int miller_k_for(size_t n_sets) {
   if (v == 1 || v == 2 || v == 4) return (int)v;
   return n_sets >= 8192 ? 4 : (n_sets >= 1024 ? 2 : 1);
 }
+
+// PublicKey.aggregate of large packages as the batch-affine tree (A/B build: LSG_AGG_TREE=0
+// keeps the serial fold + butterfly of k_seg_reduce<0> for every package)
+bool agg_tree_on() { return lsg_ab_long("LSG_AGG_TREE", 1) != 0; }
 
 // Minimum RLC group size for the bucket MSM (env LSG_MSM_MIN_GROUP): below ~150 sets the
 // fixed cost of 2040 buckets and 64 bit sums per group exceeds the per-set scalar
@@ -1301,6 +1326,8 @@ int launch_fe_range(Slot* s, size_t g0, size_t g1) {
 }
 int launch_fe(Slot* s, size_t ng) { return launch_fe_range(s, 0, ng); }
 
+int launch_agg_tree(Slot* s, const AggPlan& P, uint32_t* agg);
+
 // Per-set stages of the slot's package (no host synchronisation):
 //   side: pubkeys -> aggregation -> [r_i] scaling -> signature decode -> subgroup check (ev_sig)
 //   main: expand_message -> hash_to_G2 [-> lines] -> wait ev_sig -> Miller items f (fall)
@@ -1312,14 +1339,18 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, const PhasePlan& Ph, uint32
   LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
   s->cur = 1;
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
-  if (np > 0) {
-    // single-key sets decode straight into their aggregate slot
-    uint32_t* dst = s->single_keys ? P_<uint32_t>(s->d_agg) : P_<uint32_t>(s->d_pkp);
-    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen), dst,
-                                         P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok),
-                                         (uint32_t)d->pktab_n));
+  if (!s->single_keys && s->agg.tree) {
+    LSG_RC(launch_agg_tree(s, s->agg, P_<uint32_t>(s->d_agg)));
+  } else {
+    if (np > 0) {
+      // single-key sets decode straight into their aggregate slot
+      uint32_t* dst = s->single_keys ? P_<uint32_t>(s->d_agg) : P_<uint32_t>(s->d_pkp);
+      KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen), dst,
+                                           P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok),
+                                           (uint32_t)d->pktab_n));
+    }
+    if (!s->single_keys) LSG_RC(run_seg(s, 0, "g1_aggregate", *pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
   }
-  if (!s->single_keys) LSG_RC(run_seg(s, 0, "g1_aggregate", *pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
   KL(s, "k_pk_scale", lsgk::pk_scale(S_(s), n, P_<uint32_t>(s->d_agg), P_<uint64_t>(s->d_rnd), P_<uint32_t>(s->d_Pp),
                                      P_<uint32_t>(s->d_zP), P_<uint8_t>(s->d_pinf)));
   LSG_RC(batch_inv(s, 1, "binv_pk", P_<uint32_t>(s->d_zP), (size_t)n, P_<uint32_t>(s->d_zPi)));
@@ -1383,6 +1414,96 @@ SegPlan plan_pk_agg(Slot* s) {
     len[i] = (int32_t)s->pk_cnt[i];
   }
   return plan_seg(s->plan, 0, off, len, false, 0, 0);
+}
+
+// The batch-affine tree's plan for the slot's sets (keys of set i: pk_first[i] .. + pk_cnt[i],
+// gathered in that order into level 0).  A set takes part in a level while it has more than
+// AGG_FINAL_MAX points; then k_agg_final sums what it has left.
+AggPlan plan_agg_tree(Slot* s) {
+  AggPlan P;
+  P.tree = true;
+  const size_t n = s->n_sets;
+  std::vector<int32_t> len(n), off(n), base(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    len[i] = (int32_t)s->pk_cnt[i];
+    off[i] = (int32_t)s->pk_first[i];
+  }
+  size_t level_base = 0, level_size = s->n_pks;
+  std::vector<int32_t> parts;
+  for (;;) {
+    parts.clear();
+    for (size_t i = 0; i < n; i++)
+      if (len[i] > AGG_FINAL_MAX) parts.push_back((int32_t)i);
+    if (parts.empty()) break;
+    AggLevelPlan L;
+    L.n_seg = (int)parts.size();
+    L.base_in = level_base;
+    L.base_out = level_base + level_size;
+    L.plan_off = s->plan.size();
+    const size_t np = parts.size();
+    s->plan.resize(L.plan_off + 4 * np + 1);
+    int32_t* cum = s->plan.data() + L.plan_off;
+    int32_t* in_off = cum + np + 1;
+    int32_t* ln = in_off + np;
+    int32_t* out_off = ln + np;
+    int32_t items = 0;
+    for (size_t k = 0; k < np; k++) {
+      const int32_t i = parts[k];
+      cum[k] = items;
+      in_off[k] = off[i];
+      ln[k] = len[i];
+      out_off[k] = items;  // one output point per item
+      const int32_t m = (len[i] + 1) / 2;
+      items += m;
+      off[i] = out_off[k];
+      len[i] = m;
+      base[i] = (int32_t)L.base_out;
+    }
+    cum[np] = items;
+    L.n_items = items;
+    // chunks of T items per lane pair: up to 16 while at least 32k lane pairs stay busy
+    L.T = (int)std::max<int32_t>(1, std::min<int32_t>(16, items / 32768));
+    P.levels.push_back(L);
+    P.max_items = std::max(P.max_items, (size_t)items);
+    level_base = L.base_out;
+    level_size = (size_t)items;
+  }
+  P.n_points = level_base + level_size;
+  P.src_off = s->plan.size();
+  for (size_t i = 0; i < n; i++) {
+    s->plan.push_back(base[i]);
+    s->plan.push_back(off[i]);
+    s->plan.push_back(len[i]);
+  }
+  return P;
+}
+
+// the tree over the staged keys into d_agg (side stream: after the inputs' upload)
+int launch_agg_tree(Slot* s, const AggPlan& P, uint32_t* agg) {
+  Dev* d = s->d;
+  const size_t nk = std::max(s->n_pks, (size_t)1);
+  LSG_RC(ensure(s, s->d_agga, 4 * W_G1A * std::max(P.n_points, nk)));
+  LSG_RC(ensure(s, s->d_aggi, std::max(P.n_points, nk)));
+  LSG_RC(ensure(s, s->d_aggpre, 4 * W_FP * std::max(P.max_items, (size_t)1)));
+  LSG_RC(ensure(s, s->d_aggtot, 4 * W_FP * std::max(P.max_items, (size_t)1)));
+  LSG_RC(ensure(s, s->d_aggtinv, 4 * W_FP * std::max(P.max_items, (size_t)1)));
+  uint32_t* pts = P_<uint32_t>(s->d_agga);
+  uint8_t* inf = P_<uint8_t>(s->d_aggi);
+  KL(s, "k_pk_gather_aff", lsgk::pk_gather_aff(S_(s), (int)s->n_pks, P_<uint8_t>(s->d_pk), s->pk_stride,
+                                               P_<uint32_t>(s->d_pklen), pts, inf, P_<int32_t>(s->d_pkerr),
+                                               P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
+  for (const AggLevelPlan& L : P.levels) {
+    const int32_t* plan = PL(s, L.plan_off);
+    const size_t n_chunks = ((size_t)L.n_items + L.T - 1) / L.T;
+    KL(s, "g1_aggregate", lsgk::agg_fold(S_(s), L.n_items, L.T, plan, L.n_seg, pts + W_G1A * L.base_in, inf + L.base_in,
+                                         P_<uint32_t>(s->d_aggpre), P_<uint32_t>(s->d_aggtot)));
+    LSG_RC(batch_inv(s, 1, "binv_agg", P_<uint32_t>(s->d_aggtot), n_chunks, P_<uint32_t>(s->d_aggtinv)));
+    KL(s, "g1_aggregate", lsgk::agg_unfold(S_(s), L.n_items, L.T, plan, L.n_seg, pts + W_G1A * L.base_in,
+                                           inf + L.base_in, P_<uint32_t>(s->d_aggpre), P_<uint32_t>(s->d_aggtinv),
+                                           pts + W_G1A * L.base_out, inf + L.base_out));
+  }
+  KL(s, "g1_aggregate", lsgk::agg_final(S_(s), (int)s->n_sets, PL(s, P.src_off), pts, inf, agg));
+  return LSG_OK;
 }
 
 // D2H of per-set status into the pinned mirrors, then ev_done on the main stream
@@ -1624,7 +1745,13 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
       s->job_group[(size_t)om[g]] = (int)g;
   }
   LSG_RC(size_state(s, s->n_sets, s->n_pks, A.groups.size(), gm.size(), 1));
-  if (!s->single_keys) s->pkagg = plan_pk_agg(s);
+  s->agg = AggPlan();
+  if (!s->single_keys) {
+    if (s->n_pks >= AGG_TREE_MIN_KEYS && agg_tree_on())
+      s->agg = plan_agg_tree(s);
+    else
+      s->pkagg = plan_pk_agg(s);
+  }
   // sets of the package group that share a message share one Miller pair: Π e(r_i pk_i, H(m))
   // = e(Σ r_i pk_i, H(m)) exactly.  Its per-set items are then never computed, so a failing
   // package group's chunks (phase B) run their own items and phase C goes per job.
@@ -2611,9 +2738,9 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
   if (need > d->pktab_cap) {
     const size_t cap = std::max(std::max(need, 2 * d->pktab_cap), (size_t)1024);
     DevBuf nt, nok;
-    LSG_HIPC(c, hipMalloc(&nt.p, 4 * W_G1P * cap));
+    LSG_HIPC(c, hipMalloc(&nt.p, 4 * W_G1A * cap));
     g_allocs++;
-    nt.cap = 4 * W_G1P * cap;
+    nt.cap = 4 * W_G1A * cap;
     hipError_t e = hipMalloc(&nok.p, cap);
     if (e != hipSuccess) {
       free_dev(nt);
@@ -2623,7 +2750,7 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
     nok.cap = cap;
     LSG_HIPC(c, hipMemset(nok.p, 0, cap));
     if (d->pktab_n) {
-      LSG_HIPC(c, hipMemcpy(nt.p, d->d_pktab.p, 4 * W_G1P * d->pktab_n, hipMemcpyDeviceToDevice));
+      LSG_HIPC(c, hipMemcpy(nt.p, d->d_pktab.p, 4 * W_G1A * d->pktab_n, hipMemcpyDeviceToDevice));
       LSG_HIPC(c, hipMemcpy(nok.p, d->d_pktab_ok.p, d->pktab_n, hipMemcpyDeviceToDevice));
     }
     free_dev(d->d_pktab);
@@ -2633,15 +2760,20 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
     d->pktab_cap = cap;
   }
   LSG_RC(util_stage_keys(s, pks, pk_len, n));
-  // decode straight into the table rows first .. first + n - 1
-  KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)n, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
-                                       P_<uint32_t>(d->d_pktab) + W_G1P * first, P_<int32_t>(s->d_pkerr), nullptr,
-                                       nullptr, 0u));
+  // decode straight into the table rows first .. first + n - 1: affine points (the first
+  // level of the aggregation tree reads them as they are), row flag 1 = a finite key, 2 = the
+  // infinity key, 0 = no key
+  LSG_RC(ensure(s, s->d_ub, n));
+  KL(s, "k_pk_gather_aff", lsgk::pk_gather_aff(S_(s), (int)n, P_<uint8_t>(s->d_pk), s->pk_stride,
+                                               P_<uint32_t>(s->d_pklen), P_<uint32_t>(d->d_pktab) + W_G1A * first,
+                                               P_<uint8_t>(s->d_ub), P_<int32_t>(s->d_pkerr), nullptr, nullptr, 0u));
   pkerr.assign(n, 0);
+  std::vector<uint8_t> inf(n);
   LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(inf.data(), s->d_ub.p, n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   std::vector<uint8_t> ok(n);
-  for (size_t k = 0; k < n; k++) ok[k] = pkerr[k] == 0 ? 1 : 0;
+  for (size_t k = 0; k < n; k++) ok[k] = pkerr[k] != 0 ? 0 : (inf[k] ? 2 : 1);
   LSG_HIP(s, hipMemcpy(P_<uint8_t>(d->d_pktab_ok) + first, ok.data(), n, hipMemcpyHostToDevice));
   d->pktab_n = std::max(d->pktab_n, need);
   keep_times(s);
@@ -3101,6 +3233,58 @@ int lsg_aggregate_pubkeys(lsg_ctx* c, const uint8_t* pks, uint32_t pk_len, size_
       *err_code = pkerr[k];
       break;
     }
+  return LSG_OK;
+}
+
+int lsg_aggregate_pubkeys_multi(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint8_t* out96, int32_t* err) {
+  if (!c || (n_sets && (!sets || !out96 || !err)) || n_sets > 0x7fffffffull) return LSG_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n_sets; i++)
+    if (sets[i].n_pks && (!sets[i].pks || (sets[i].pk_len != 48 && sets[i].pk_len != 96 && sets[i].pk_len != LSG_PK_INDEX)))
+      return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  Dev* d = c->dev[0];
+  Slot* s = &d->util;
+  timer_reset(s);
+  if (n_sets == 0) return LSG_OK;
+  std::vector<lsg_set> ks(n_sets);
+  std::vector<const lsg_set*> sp(n_sets);
+  for (size_t i = 0; i < n_sets; i++) {
+    memset(&ks[i], 0, sizeof(lsg_set));
+    ks[i].pks = sets[i].pks;
+    ks[i].pk_len = sets[i].pk_len;
+    ks[i].n_pks = sets[i].n_pks;
+    sp[i] = &ks[i];
+  }
+  LSG_RC(stage_sets(s, sp.data(), n_sets, 0, false));
+  const size_t np = s->n_pks;
+  LSG_RC(size_state(s, n_sets, np, 1, 0));
+  s->plan.clear();
+  const bool tree = np >= AGG_TREE_MIN_KEYS && agg_tree_on();
+  s->single_keys = false;
+  if (tree)
+    s->agg = plan_agg_tree(s);
+  else
+    s->pkagg = plan_pk_agg(s);
+  LSG_RC(upload_plan(s));
+  if (tree) {
+    LSG_RC(launch_agg_tree(s, s->agg, P_<uint32_t>(s->d_agg)));
+  } else if (np) {
+    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
+                                         P_<uint32_t>(s->d_pkp), P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab),
+                                         P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
+    LSG_RC(run_seg(s, 0, "g1_aggregate", s->pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
+  }
+  LSG_RC(ensure(s, s->d_aux, 96 * n_sets));
+  KL(s, "k_g1p_to_bytes", lsgk::g1p_to_bytes(S_(s), (int)n_sets, P_<uint32_t>(s->d_agg), P_<uint8_t>(s->d_aux)));
+  std::vector<int32_t> pkerr(std::max(np, (size_t)1));
+  if (np) LSG_HIP(s, hipMemcpyAsync(pkerr.data(), s->d_pkerr.p, 4 * np, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipMemcpyAsync(out96, s->d_aux.p, 96 * n_sets, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  keep_times(s);
+  for (size_t i = 0; i < n_sets; i++) {
+    err[i] = s->pk_cnt[i] == 0 ? LSG_ERR_EMPTY_AGGREGATE : 0;
+    for (uint32_t q = 0; q < s->pk_cnt[i] && !err[i]; q++) err[i] = pkerr[s->pk_first[i] + q];
+  }
   return LSG_OK;
 }
 

@@ -49,6 +49,17 @@ hipError_t sign(hipStream_t st, int n, const uint8_t* sks, const uint32_t* H, ui
 hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
                      int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
 hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err);
+// keys -> affine points + infinity flags + per-key errors (table rows by index, or decoded bytes)
+hipError_t pk_gather_aff(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
+                         uint8_t* inf, int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
+// the batch-affine aggregation tree (lsg_k_pk.hip): one level = fold (chunks of T items) +
+// batched inversion of the chunk products (host) + unfold; k_agg_final sums each set's rest
+hipError_t agg_fold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
+                    const uint8_t* inf, uint32_t* pre, uint32_t* tot);
+hipError_t agg_unfold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
+                      const uint8_t* inf, uint32_t* pre, const uint32_t* tinv, uint32_t* out_pts, uint8_t* out_inf);
+hipError_t agg_final(hipStream_t st, int n_sets, const int32_t* src, const uint32_t* arena, const uint8_t* inf_arena,
+                     uint32_t* agg);
 hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* rnd, uint32_t* Pp, uint32_t* zP,
                     uint8_t* pinf);
 hipError_t pk_affine(hipStream_t st, int n, const uint32_t* Pp, const uint32_t* zinv, uint32_t* P);

@@ -158,7 +158,10 @@ def test_config_c_block_128x450(table_ctx, keys):
     assert co.verify_each([agg_pks[77]], [msgs[76]], [sigs[77]]) == [0]
     got, _ = c.verify_jobs([(wrong[:64], 0), (wrong[64:], 0)])
     assert got == [(1, 0), (0, 0)]
-    # the aggregated keys themselves, bit-exact against the oracle's (sum sk) G1
+    # the aggregated keys themselves, bit-exact against the oracle's (sum sk) G1: all 128 sets
+    # in one pass of the jobs path's batch-affine aggregation tree (57k keys), and a few through
+    # the single-set serial fold
+    assert c.aggregate_pubkeys_multi([PkIndices(ix) for ix in idx]) == [(agg_pks[g], 0) for g in range(n)]
     for g in (0, 77, 127):
         assert c.aggregate_pubkeys(PkIndices(idx[g])) == (agg_pks[g], 0)
 

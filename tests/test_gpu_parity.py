@@ -484,6 +484,55 @@ def test_pubkey_table_aggregation_by_index(table_ctx):
     assert c.aggregate_pubkeys(PkIndices([]))[1] == 101  # EMPTY_AGGREGATE_ARRAY
 
 
+def test_aggregation_tree_edge_cases(table_ctx):
+    """The batch-affine aggregation tree (lsg_k_pk.hip k_agg_*, packages of >= 32768 keys)
+    against the oracle's PublicKey.aggregate, bit-exact, on the cases its affine additions must
+    route around: P + P (doubling), P + (-P) (infinity), infinity keys in the table, lone last
+    points, segments that skip the levels (<= 8 keys), a key list of period 40 whose higher
+    levels are full of equal pairs, bad indices and empty sets."""
+    from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
+    from oracle.curves import E1, G1_GEN
+    c = table_ctx
+    # rows 40 = -pk(3), 41 = the infinity key (uncompressed encoding)
+    neg3 = g1_serialize(E1.neg(bd.pk_point(3)))
+    assert c.pubkey_table_set(40, [neg3, bytes([0x40]) + bytes(95)]) == [0, 0]
+    sk = {i: bd.sk(i) for i in range(40)}
+    from oracle.fields import R as ORDER
+    sk[40] = (-bd.sk(3)) % ORDER
+    sk[41] = 0
+
+    def expect(ix):
+        t = sum(sk[i] for i in ix) % ORDER
+        return g1_serialize(E1.mul(G1_GEN, t) if t else None)
+
+    cases = [
+        [3, 40],                          # P + (-P): infinity (final kernel)
+        [3, 40] * 6 + [9],                # 13 points: six P - P pairs in a level, then 9
+        [5] * 9,                          # doublings in the levels
+        [5] * 16,
+        [41] * 12,                        # only infinity keys
+        [41, 7, 41, 8, 41, 41, 9, 10, 11, 41, 12],
+        list(range(40)),
+        [7],
+        [0, 1],
+        list(range(9)),                   # 9: one level with a lone last point
+        [i % 40 for i in range(33000)],   # period 40: equal pairs from level 3 on
+        [i % 7 for i in range(300)] + [40, 3],
+    ]
+    got = c.aggregate_pubkeys_multi([PkIndices(ix) for ix in cases] + [PkIndices([1, 99999]), PkIndices([])])
+    for k, ix in enumerate(cases):
+        assert got[k] == (expect(ix), 0), (k, len(ix))
+    assert got[-2][1] == LSG_ERR_BAD_INDEX and got[-1][1] == 101
+    # the same through byte-encoded keys (decoded in the tree's gather), below and above the
+    # tree's threshold
+    few = [bd.pk_bytes(i % 40) for i in range(50)]
+    many = [bd.pk_bytes(i % 40, compressed=(i % 3 == 0)) for i in range(33000)]
+    g2 = c.aggregate_pubkeys_multi([few, many[:33000 // 2], many[33000 // 2:]])
+    assert g2[0] == (expect([i % 40 for i in range(50)]), 0)
+    assert g2[1] == (expect([i % 40 for i in range(16500)]), 0)
+    assert g2[2] == (expect([i % 40 for i in range(16500, 33000)]), 0)
+
+
 def test_pubkey_table_rejects_bad_keys_and_grows(table_ctx):
     from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
     c = table_ctx
