@@ -564,13 +564,18 @@ def main():
         (128 if args.workload in ("block", "gossip") else 1)
     if group >= 256:
         per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / group
+    elif group >= 32:  # 4-bit-window bucket MSM (lsg_host.hip plan_phase)
+        per_set_muls = opc["batched_single_set_msm4_fp_muls"] + opc["per_batch_msm4_fp_muls"] / group
     else:
         per_set_muls = opc["batched_single_set_fp_muls"] + opc["per_batch_fp_muls"] / group
     fused = os.environ.get("LSG_MILLER_FUSED", "1") != "0"
     sf = opc["stage_fp_muls"]
     per_set_muls += (sf["miller_fused_per_set"] if fused else sf["miller_lines"] + sf[accum_key]) \
         - sf["miller_multi2_per_set"]
-    per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_extra_per_pubkey_fp_muls"]
+    # extra signers: the batch-affine tree for packages of >= 32768 keys, else the serial fold
+    tree = wl.pks_per_set * n_sets >= 32768
+    per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_tree_extra_per_pubkey_fp_muls" if tree else
+                                                "aggregate_extra_per_pubkey_fp_muls"]
     per_set_muls -= (1.0 - wl.msgs_per_set) * sf["hash_map"]  # hash_to_G2 once per distinct message
     if os.environ.get("LSG_MSG_AGG", "1") != "0":  # and one Miller pair per distinct message
         per_set_muls -= (1.0 - wl.msgs_per_set) * (sf["miller_fused_per_set"] if fused else sf["miller_multi2_per_set"])

@@ -700,13 +700,16 @@ int miller_k_for(size_t n_sets) {
 // keeps the serial fold + butterfly of k_seg_reduce<0> for every package)
 bool agg_tree_on() { return lsg_ab_long("LSG_AGG_TREE", 1) != 0; }
 
-// Minimum RLC group size for the bucket MSM (env LSG_MSM_MIN_GROUP): below ~150 sets the
-// fixed cost of 2040 buckets and 64 bit sums per group exceeds the per-set scalar
-// multiplications it replaces.
+// Minimum RLC group size for the bucket MSM (A/B build: env LSG_MSM_MIN_GROUP).  With 4-bit
+// windows a group of n sets costs 16 n + 512 G2 additions and a Horner program (~4k Fp
+// products more than the plain ML(-G1, S) one) against a 64-bit scalar multiplication per set
+// (~2.2k Fp products each): the MSM wins from ~20 sets.
 size_t msm_min_group() {
-  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 256);
+  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 32);
   return x < 1 ? (size_t)1 : (size_t)x;
 }
+// groups of at least this many sets take 8-bit windows, smaller ones 4-bit (plan_phase)
+constexpr size_t MSM_C8_MIN = 256;
 
 // Phase A as the reference batches it: one RLC group per 16-job chunk instead of one package
 // group (env LSG_PACKAGE_GROUP=0; A/B and the equivalence test of the two modes)
@@ -1138,19 +1141,34 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
   const size_t ng = Ph.groups.size();
   Ph.n_msm = 0;
   while (Ph.n_msm < ng && Ph.groups[Ph.n_msm].msm) Ph.n_msm++;
-  // bucket MSM: per MSM group, bucket (w, d) = the sets whose w-th byte of r_i is d
+  // bucket MSM: per MSM group, bucket (w, d) = the sets whose w-th c-bit digit of r_i is d.
+  // c = 8 (8 windows x 255 buckets) for large groups; c = 4 (16 x 15) below MSM_C8_MIN sets,
+  // where 2040 buckets' bit sums would cost more than the sets' bucket additions (a block's
+  // 128-set groups: 16 additions per set + 512 per group instead of a 64-bit scalar
+  // multiplication per set).  Buckets are numbered compactly (group bases); bit k = c w + j
+  // sums the buckets (w, d) whose digit d has bit j set, so every group has 64 bit sums and
+  // one Horner program whatever its c.
   if (Ph.n_msm) {
-    const size_t nb = (size_t)MSM_WINDOWS * MSM_DIGITS;
-    std::vector<int32_t> cnt(Ph.n_msm * nb, 0);
-    for (size_t g = 0; g < Ph.n_msm; g++)
+    std::vector<int> cw(Ph.n_msm);
+    std::vector<size_t> gbase(Ph.n_msm + 1, 0);
+    for (size_t g = 0; g < Ph.n_msm; g++) {
+      cw[g] = Ph.groups[g].len >= MSM_C8_MIN ? 8 : 4;
+      gbase[g + 1] = gbase[g] + (size_t)(64 / cw[g]) * (size_t)((1u << cw[g]) - 1);
+    }
+    auto bucket = [&](size_t g, int w, uint32_t d) { return gbase[g] + (size_t)w * ((1u << cw[g]) - 1) + d - 1; };
+    std::vector<int32_t> cnt(gbase[Ph.n_msm], 0);
+    for (size_t g = 0; g < Ph.n_msm; g++) {
+      const int c = cw[g], nw = 64 / c;
+      const uint64_t dm = (1ull << c) - 1;
       for (size_t i = Ph.groups[g].first; i < Ph.groups[g].first + Ph.groups[g].len; i++) {
         const uint64_t r = s->rnd[i];
-        for (int w = 0; w < MSM_WINDOWS; w++) {
-          const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
-          if (d) cnt[g * nb + (size_t)w * MSM_DIGITS + d - 1]++;
+        for (int w = 0; w < nw; w++) {
+          const uint32_t d = (uint32_t)((r >> (c * w)) & dm);
+          if (d) cnt[bucket(g, w, d)]++;
         }
       }
-    std::vector<int32_t> seg_off(Ph.n_msm * nb), seg_len(cnt);
+    }
+    std::vector<int32_t> seg_off(cnt.size()), seg_len(cnt);
     int32_t tot = 0;
     for (size_t b = 0; b < cnt.size(); b++) {
       seg_off[b] = tot;
@@ -1160,26 +1178,31 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
     A.resize(idx_off + (size_t)tot);
     int32_t* idx = A.data() + idx_off;
     std::vector<int32_t> fill(seg_off);
-    for (size_t g = 0; g < Ph.n_msm; g++)
+    for (size_t g = 0; g < Ph.n_msm; g++) {
+      const int c = cw[g], nw = 64 / c;
+      const uint64_t dm = (1ull << c) - 1;
       for (size_t i = Ph.groups[g].first; i < Ph.groups[g].first + Ph.groups[g].len; i++) {
         const uint64_t r = s->rnd[i];
-        for (int w = 0; w < MSM_WINDOWS; w++) {
-          const uint32_t d = (uint32_t)(r >> (8 * w)) & 255u;
-          if (d) idx[fill[g * nb + (size_t)w * MSM_DIGITS + d - 1]++] = (int32_t)i;
+        for (int w = 0; w < nw; w++) {
+          const uint32_t d = (uint32_t)((r >> (c * w)) & dm);
+          if (d) idx[fill[bucket(g, w, d)]++] = (int32_t)i;
         }
       }
+    }
     Ph.buckets = plan_seg(A, 1, seg_off, seg_len, true, idx_off, 0);
-    // bit (g, k = 8w + j): the buckets (g, w, d) whose digit d has bit j set
+    // bit (g, k = c w + j): the buckets (g, w, d) whose digit d has bit j set
     const size_t bidx = A.size();
     std::vector<int32_t> boff, blen;
-    for (size_t g = 0; g < Ph.n_msm; g++)
-      for (int w = 0; w < MSM_WINDOWS; w++)
-        for (int j = 0; j < 8; j++) {
+    for (size_t g = 0; g < Ph.n_msm; g++) {
+      const int c = cw[g], nw = 64 / c;
+      for (int w = 0; w < nw; w++)
+        for (int j = 0; j < c; j++) {
           boff.push_back((int32_t)(A.size() - bidx));
-          for (uint32_t d = 1; d <= 255; d++)
-            if ((d >> j) & 1u) A.push_back((int32_t)(g * nb + (size_t)w * MSM_DIGITS + d - 1));
+          for (uint32_t d = 1; d < (1u << c); d++)
+            if ((d >> j) & 1u) A.push_back((int32_t)bucket(g, w, d));
           blen.push_back((int32_t)(A.size() - bidx) - boff.back());
         }
+    }
     Ph.bits = plan_seg(A, 1, boff, blen, true, bidx, 0);
   }
   // scaled groups: S_g = sum of the contiguous scaled points

@@ -47,6 +47,19 @@ def main():
     msm_per_set = 8 * c["g2_add"]
     msm_per_group = (64 * 127 + 126) * c["g2_add"]
     per_set_msm = per_set - c["sig_scale"] - c["g2_add"] + msm_per_set
+    # groups of 32..255 sets: 4-bit windows (lsg_host.hip plan_phase): 16 digits per set, the
+    # 64 bit sums over 8 buckets each (64 * 7 additions), the same Horner pass
+    msm4_per_set = 16 * c["g2_add"]
+    msm4_per_group = (64 * 7 + 126) * c["g2_add"]
+    per_set_msm4 = per_set - c["sig_scale"] - c["g2_add"] + msm4_per_set
+    # PublicKey.aggregate of large packages (>= 32768 keys) as the batch-affine tree (lsg_k_pk.hip
+    # k_agg_*): per pairwise item 1 prefix product (fold) + 5 (unfold: the item's inverse, the
+    # running inverse, lambda, lambda^2, lambda (x1 - x3)); per chunk of 16 items the batched
+    # inversion of its product (2 + 1 products and one zero test ~ 1 product per value: 4 / 16)
+    # and the zero test of its inverse (1 / 16); a set's last <= 8 points summed with complete
+    # mixed additions (11 products; ~7 per set of ~450 keys, spread over its keys)
+    tree_per_item = 6 + (4 + 1) / 16
+    tree_per_pubkey = round((439 * tree_per_item + 7 * 11) / 446, 2)
     out = {
         "unit": "Fp multiplications (381-bit Montgomery); 1 = 300 v_mad_u64_u32",
         "mads_per_fp_mul": 300,
@@ -56,7 +69,11 @@ def main():
         "msm": {"per_set_fp_muls": msm_per_set, "per_group_fp_muls": msm_per_group},
         "batched_single_set_msm_fp_muls": per_set_msm,
         "per_batch_msm_fp_muls": per_batch + msm_per_group,
+        "msm4": {"per_set_fp_muls": msm4_per_set, "per_group_fp_muls": msm4_per_group},
+        "batched_single_set_msm4_fp_muls": per_set_msm4,
+        "per_batch_msm4_fp_muls": per_batch + msm4_per_group,
         "aggregate_extra_per_pubkey_fp_muls": c["g1_add"],
+        "aggregate_tree_extra_per_pubkey_fp_muls": tree_per_pubkey,
         "survey_estimate_blst_equivalent": {"batched_single_set": 16000, "per_batch": 15000, "per_pubkey": 11},
         "source": "tools/gen_opcount.py over tests/native/hostcheck.hip (LSG_COUNT_MULS)",
     }
