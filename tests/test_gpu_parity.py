@@ -526,7 +526,7 @@ def test_aggregation_tree_edge_cases(table_ctx):
     # the same through byte-encoded keys (decoded in the tree's gather), below and above the
     # tree's threshold
     few = [bd.pk_bytes(i % 40) for i in range(50)]
-    many = [bd.pk_bytes(i % 40, compressed=(i % 3 == 0)) for i in range(33000)]
+    many = [bd.pk_bytes(i % 40, compressed=(i >= 16500)) for i in range(33000)]  # (one encoding per set)
     g2 = c.aggregate_pubkeys_multi([few, many[:33000 // 2], many[33000 // 2:]])
     assert g2[0] == (expect([i % 40 for i in range(50)]), 0)
     assert g2[1] == (expect([i % 40 for i in range(16500)]), 0)
