@@ -347,6 +347,7 @@ struct Slot {
   DevBuf d_lines;
   bool rs2_ready = false;
   std::vector<uint8_t> rs2_scaled;  // per set: [r_i] sig_i is in d_rs2 (fallback phases share it)
+  std::vector<uint8_t> rs_raw;      // per set: d_rs holds the unscaled point (a phase-A MSM group's)
   // groups
   DevBuf d_S, d_F, d_verdict, d_Sb, d_fgb, d_Fb, d_bkt, d_bits, d_aux, d_gath, d_nodeF, d_nodeV;
   DevBuf seg_tmp[3][2];  // reduction scratch per use: [0] pubkeys, [1] signature sums, [2] Fp12 products
@@ -700,16 +701,18 @@ int miller_k_for(size_t n_sets) {
 // keeps the serial fold + butterfly of k_seg_reduce<0> for every package)
 bool agg_tree_on() { return lsg_ab_long("LSG_AGG_TREE", 1) != 0; }
 
-// Minimum RLC group size for the bucket MSM (A/B build: env LSG_MSM_MIN_GROUP).  With 4-bit
-// windows a group of n sets costs 16 n + 512 G2 additions and a Horner program (~4k Fp
-// products more than the plain ML(-G1, S) one) against a 64-bit scalar multiplication per set
-// (~2.2k Fp products each): the MSM wins from ~20 sets.
+// Minimum RLC group size for the bucket MSM (A/B build: env LSG_MSM_MIN_GROUP).  With 2-bit
+// windows a set costs ~24 bucket additions plus 4 of the group's 64 bit sums (~1k Fp
+// products) against a 64-bit scalar multiplication (~2.25k), and the group one Horner program
+// (~4k Fp products more than the plain ML(-G1, S) one): the MSM wins from ~4 sets.
 size_t msm_min_group() {
-  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 32);
+  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 4);
   return x < 1 ? (size_t)1 : (size_t)x;
 }
-// groups of at least this many sets take 8-bit windows, smaller ones 4-bit (plan_phase)
-constexpr size_t MSM_C8_MIN = 256;
+// Window width c of a group's bucket MSM (plan_phase): per set 64/c digits (bucket
+// additions), per group the 64 bit sums over 2^(c-1) buckets each.  n sets cost about
+// n (64/c) + 2^(c-1) 64 G2 additions: c = 2 below 48 sets, 4 below 256, 8 from there.
+int msm_window_bits(size_t n) { return n >= 256 ? 8 : (n >= 48 ? 4 : 2); }
 
 // Phase A as the reference batches it: one RLC group per 16-job chunk instead of one package
 // group (env LSG_PACKAGE_GROUP=0; A/B and the equivalence test of the two modes)
@@ -1152,7 +1155,7 @@ int plan_phase(Slot* s, PhasePlan& Ph) {
     std::vector<int> cw(Ph.n_msm);
     std::vector<size_t> gbase(Ph.n_msm + 1, 0);
     for (size_t g = 0; g < Ph.n_msm; g++) {
-      cw[g] = Ph.groups[g].len >= MSM_C8_MIN ? 8 : 4;
+      cw[g] = msm_window_bits(Ph.groups[g].len);
       gbase[g + 1] = gbase[g] + (size_t)(64 / cw[g]) * (size_t)((1u << cw[g]) - 1);
     }
     auto bucket = [&](size_t g, int w, uint32_t d) { return gbase[g] + (size_t)w * ((1u << cw[g]) - 1) + d - 1; };
@@ -1304,13 +1307,17 @@ int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall, bool 
 }
 
 // side stream: signature sums -> ML(-G1, S_g) -> fall slots; main stream: products, export, FE
-int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fall, bool export_blobs) {
+// rs: the scaled points [r_i] sig_i the plain groups sum; rs_msm: the unscaled points the
+// bucket MSM groups read (phase A: one buffer holds both kinds, by set)
+int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fall, bool export_blobs,
+                 const uint32_t* rs_msm = nullptr) {
+  if (!rs_msm) rs_msm = rs;
   const size_t ng = Ph.groups.size();
   if (ng == 0) return LSG_OK;
   LSG_RC(size_state(s, s->n_sets, s->n_pks, ng, Ph.n_msm, 2));
   s->cur = 1;
   if (Ph.n_msm) {
-    LSG_RC(run_seg(s, 1, "msm_buckets", Ph.buckets, rs, P_<uint32_t>(s->d_bkt)));
+    LSG_RC(run_seg(s, 1, "msm_buckets", Ph.buckets, rs_msm, P_<uint32_t>(s->d_bkt)));
     LSG_RC(run_seg(s, 1, "msm_bits", Ph.bits, P_<uint32_t>(s->d_bkt), P_<uint32_t>(s->d_bits)));
     KL(s, "k_g2p_to_canon", lsgk::g2p_to_canon(S_(s), (int)(MSM_BITS * Ph.n_msm), P_<uint32_t>(s->d_bits),
                                                P_<uint8_t>(s->d_Sb)));
@@ -1816,6 +1823,8 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   LSG_RC(upload_plan(s));
   LSG_RC(launch_set_stages(s, &s->pkagg, A, P_<uint32_t>(s->d_fall)));
   // signature points: unscaled for MSM groups, [r_i] sig_i for the rest
+  s->rs_raw.assign(s->n_sets, 0);
+  for (size_t g = 0; g < A.n_msm; g++) memset(s->rs_raw.data() + A.groups[g].first, 1, A.groups[g].len);
   if (!A.groups.empty()) {
     const bool any_small = A.n_msm < A.groups.size();
     std::vector<uint8_t> mode;
@@ -1914,15 +1923,32 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
                        const std::vector<std::pair<int32_t, int32_t>>* given, std::vector<int32_t>& v) {
   v.assign(groups.size(), 0);
   if (groups.empty()) return LSG_OK;
+  // Signature sums: a group whose sets' unscaled points are resident (they were in a phase-A
+  // bucket-MSM group: d_rs) and that is large enough sums them by its own bucket MSM (no
+  // per-set scaling); the others sum [r_i] sig_i (d_rs2, scaled below).  MSM groups go first
+  // (plan_phase); `order` maps the phase's group k to the caller's.
+  std::vector<size_t> order;
+  std::vector<uint8_t> gm(groups.size(), 0);
+  for (size_t g = 0; g < groups.size(); g++) {
+    bool ok = groups[g].len >= std::max(msm_min_group(), (size_t)2) && s->rs_raw.size() == s->n_sets;
+    for (size_t i = groups[g].first; ok && i < groups[g].first + groups[g].len; i++) ok = s->rs_raw[i] != 0;
+    gm[g] = ok;
+    if (ok) order.push_back(g);
+  }
+  const size_t n_msm = order.size();
+  for (size_t g = 0; g < groups.size(); g++)
+    if (!gm[g]) order.push_back(g);
   // size this phase's buffers BEFORE any pointer into them is taken or any launch queued:
   // a phase with more groups than phase A had grows d_fall2 (and the group buffers), and a
   // pointer saved earlier would name the freed allocation
-  LSG_RC(size_state(s, s->n_sets, s->n_pks, groups.size(), 0, 2));
+  LSG_RC(size_state(s, s->n_sets, s->n_pks, groups.size(), n_msm, 2));
   s->cur = 0;  // the phase's kernel timers follow phase A's (lsg_last_kernel_times: the whole ticket)
   s->plan.clear();
   PhasePlan Ph;
-  Ph.groups = groups;
-  for (auto& g : Ph.groups) g.msm = false;
+  for (size_t k = 0; k < order.size(); k++) {
+    Ph.groups.push_back(groups[order[k]]);
+    Ph.groups.back().msm = gm[order[k]] != 0;
+  }
   // groups of one set each (the per-job phase of single-set jobs): one-set Miller items in
   // the list form instead of four-wave fused items holding one pair
   size_t singles = 0;
@@ -1931,7 +1957,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   if (!given && 2 * singles >= groups.size()) s->K = 1;
   if (given) {
     Ph.reuse_items = true;
-    Ph.given = *given;
+    for (size_t k = 0; k < order.size(); k++) Ph.given.push_back((*given)[order[k]]);
     Ph.n_items = s->phA.n_items;
     Ph.term_base = s->phA.n_items + s->phA.groups.size();  // after phase A's own terms
   }
@@ -1943,12 +1969,14 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   if (s->rs2_scaled.size() != s->n_sets) s->rs2_scaled.assign(s->n_sets, 0);
   std::vector<uint8_t> mode(s->n_sets, 0);
   bool any = false;
-  for (auto& g : groups)
-    for (size_t i = g.first; i < g.first + g.len; i++)
+  for (size_t g = 0; g < groups.size(); g++) {
+    if (gm[g]) continue;  // (its MSM reads the unscaled points)
+    for (size_t i = groups[g].first; i < groups[g].first + groups[g].len; i++)
       if (!s->rs2_scaled[i]) {
         mode[i] = s->rs2_scaled[i] = 1;
         any = true;
       }
+  }
   // the side stream needs the plan: order it after the upload on the main stream
   LSG_HIP(s, hipEventRecord(s->ev_in, s->st[0]));
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
@@ -1972,7 +2000,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   s->cur = 0;
   uint32_t* fall = given ? P_<uint32_t>(s->d_fall) : P_<uint32_t>(s->d_fall2);
   if (!given) LSG_RC(launch_accum(s, Ph.n_items, Ph.item_off, fall, Ph.single_items));
-  LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), fall, false));
+  LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), fall, false, P_<uint32_t>(s->d_rs)));
   LSG_RC(launch_fe(s, groups.size()));
   LSG_RC(launch_readback(s, false));
   const int dev = s->d->device;
@@ -1984,7 +2012,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   }
   if (e != hipSuccess) return fail(s, "hipEventSynchronize", e);
   s->stats.n_final_exps += (uint32_t)groups.size();
-  memcpy(v.data(), s->h_verdict.p, 4 * groups.size());
+  for (size_t k = 0; k < order.size(); k++) v[order[k]] = H_<int32_t>(s->h_verdict)[k];
   return LSG_OK;
 }
 

@@ -52,6 +52,11 @@ def main():
     msm4_per_set = 16 * c["g2_add"]
     msm4_per_group = (64 * 7 + 126) * c["g2_add"]
     per_set_msm4 = per_set - c["sig_scale"] - c["g2_add"] + msm4_per_set
+    # groups of 4..47 sets (16-job chunks, fallback groups): 2-bit windows, 32 digits per set,
+    # the 64 bit sums over 2 buckets each (64 additions)
+    msm2_per_set = 32 * c["g2_add"]
+    msm2_per_group = (64 + 126) * c["g2_add"]
+    per_set_msm2 = per_set - c["sig_scale"] - c["g2_add"] + msm2_per_set
     # PublicKey.aggregate of large packages (>= 32768 keys) as the batch-affine tree (lsg_k_pk.hip
     # k_agg_*): per pairwise item 1 prefix product (fold) + 5 (unfold: the item's inverse, the
     # running inverse, lambda, lambda^2, lambda (x1 - x3)); per chunk of 16 items the batched
@@ -69,6 +74,9 @@ def main():
         "msm": {"per_set_fp_muls": msm_per_set, "per_group_fp_muls": msm_per_group},
         "batched_single_set_msm_fp_muls": per_set_msm,
         "per_batch_msm_fp_muls": per_batch + msm_per_group,
+        "msm2": {"per_set_fp_muls": msm2_per_set, "per_group_fp_muls": msm2_per_group},
+        "batched_single_set_msm2_fp_muls": per_set_msm2,
+        "per_batch_msm2_fp_muls": per_batch + msm2_per_group,
         "msm4": {"per_set_fp_muls": msm4_per_set, "per_group_fp_muls": msm4_per_group},
         "batched_single_set_msm4_fp_muls": per_set_msm4,
         "per_batch_msm4_fp_muls": per_batch + msm4_per_group,
