@@ -54,6 +54,7 @@ sys.path.insert(0, ROOT)
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 METRIC = "BLS signature sets verified/sec (whole node) at 1/2/4/8 MI355X; p50 batch latency"
 N_KEYS = 1024
+N_VALIDATORS = 1 << 20  # block workload: the pubkey table's rows (~1M validators, mainnet 2023)
 
 
 def interop_sk(i):
@@ -68,7 +69,7 @@ class Workload:
     """Builds the distinct packages of one workload: .packages = list of (jobs, expected)
     with expected = per-job (status, code) or None (all valid)."""
 
-    def __init__(self, ctx, name, rank, sets_per_step, n_packages, blocks=64):
+    def __init__(self, ctx, name, rank, sets_per_step, n_packages, blocks=64, validators=N_VALIDATORS):
         from lodestar_amd._native import PkIndices
         self.name = name
         sks = [interop_sk(i) for i in range(N_KEYS)]
@@ -98,7 +99,13 @@ class Workload:
             self.sets_per_package = n
             self.pks_per_set = 1.0
         elif name == "block":
-            errs = ctx.pubkey_table_set(0, pks)
+            # a mainnet-sized index2pubkey: N_VALIDATORS rows, validator v holding key v mod
+            # 1024, each attestation's signers a random committee subset of them --
+            # the table gathers are scattered over ~112 MB of HBM as on mainnet
+            import random as _random
+            table = [pks[v % N_KEYS] for v in range(validators)]
+            errs = ctx.pubkey_table_set(0, table)
+            del table
             if any(errs):
                 raise SystemExit("pubkey table load failed")
             per_block = 128
@@ -109,10 +116,9 @@ class Workload:
                     for i in range(per_block):
                         g = ((rank * n_packages + p) * blocks + b) * per_block + i
                         size = 440 + (g * 7) % 21
-                        start = (g * 53) % N_KEYS
-                        ix = [(start + j) % N_KEYS for j in range(size)]
+                        ix = _random.Random(g).sample(range(validators), size)
                         idx.append(PkIndices(ix))
-                        agg.append(sum(sks[k] for k in ix) % R_ORDER)
+                        agg.append(sum(sks[k % N_KEYS] for k in ix) % R_ORDER)
                         msgs.append(msg(tag, g))
                         npk += size
                     sigs = ctx.sign(agg, msgs)
@@ -336,6 +342,8 @@ def main():
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
     ap.add_argument("--blocks", type=int, default=64, help="block workload: blocks (128-set jobs) per package")
+    ap.add_argument("--validators", type=int, default=N_VALIDATORS,
+                    help="block workload: pubkey table rows (validator v holds key v mod 1024)")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waits", choices=["thread", "inline"], default="thread",
@@ -381,7 +389,8 @@ def main():
         ctx = Context(devices=list(range(args.devices)))
     else:
         ctx = Context(local)
-    wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages, blocks=args.blocks)
+    wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages, blocks=args.blocks,
+                  validators=args.validators)
     prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
     n_sets = wl.sets_per_package
     max_pks = int(n_sets * wl.pks_per_set) + 1
@@ -603,7 +612,7 @@ def main():
             "adversarial": "adversarial (SURVEY 8d config E): the firehose package with 1% corrupted sets, "
                            "batch failure + chunk/per-job retry, every verdict checked",
             "block": f"block-body (SURVEY 8d config C): {args.blocks} blocks per package, each a non-batchable job of 128 "
-                     "aggregate sets of 440-460 signers named by index into the device pubkey table",
+                     "aggregate sets of 440-460 random signers named by index into a device pubkey table of --validators rows",
             "sync": "sync-committee contributions (SURVEY 8d config B): 256 batchable jobs per package, each one "
                     "512-signer aggregate set (keys by index)",
             "gossip": "gossip-128 (SURVEY 8d config A): one batchable job of 128 single sets per package",
@@ -620,7 +629,7 @@ def main():
             "data": "synthetic (interop keys, GPU-signed; fresh OS-CSPRNG randomizers per package)",
             "config": {"workload": desc, "sets_per_step_per_gpu": n_sets // n_dev, "global_batch": n_sets * world,
                        "jobs_per_package": len(wl.packages[0][0]), "pubkeys_per_set": round(wl.pks_per_set, 1),
-                       "keys": N_KEYS,
+                       "keys": N_KEYS, "validators": args.validators if args.workload == "block" else None,
                        "parallelism": f"devices{args.devices} (one context, RCCL exchange)" if args.devices else f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),

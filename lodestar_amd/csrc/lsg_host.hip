@@ -287,22 +287,17 @@ struct PhasePlan {
   size_t n_magg = 0, magg_off = 0, n_set_items = 0;
 };
 
-// PublicKey.aggregate as the batch-affine pairwise tree (lsg_k_pk.hip k_agg_*): per level, the
-// participating segments' plan (cum, in_off, len, out_off in the plan arena), the level's item
-// count and chunk size T, and the level's input / output bases in the point arena
-struct AggLevelPlan {
-  size_t plan_off = 0;
-  int n_seg = 0, n_items = 0, T = 1;
-  size_t base_in = 0, base_out = 0;
-};
+// PublicKey.aggregate as the batch-affine pairwise tree (lsg_k_pk.hip k_agg_*, lsg_launch.h
+// AggTreeArgs): L levels, T items per lane pair, n_c0 level-0 lane pairs, N0 level-0 points;
+// plan arena offsets of the per-block set map, the per-set (o0, len, pk0) and k_agg_final's
+// per-set sources
+constexpr int64_t LSG_ITEMS_PER_BLOCK_HOST = 128;  // lane pairs per block (lsg_kcommon.hpp)
 struct AggPlan {
   bool tree = false;
-  std::vector<AggLevelPlan> levels;
-  size_t src_off = 0;    // per set (base, off, len) of its remaining points (k_agg_final)
-  size_t n_points = 0;   // points over all levels (arena size)
-  size_t max_items = 0;  // largest level
+  int L = 0, T = 1;
+  int64_t n_c0 = 0, N0 = 0;
+  size_t blk_off = 0, o0_off = 0, len_off = 0, pk0_off = 0, src_off = 0;
 };
-constexpr int AGG_FINAL_MAX = 8;          // a segment of at most this many points is summed directly
 constexpr size_t AGG_TREE_MIN_KEYS = 32768;  // smaller packages: the serial fold + butterfly
 
 struct JobRec {
@@ -358,7 +353,7 @@ struct Slot {
   PhasePlan phA;   // phase A: the package group + non-batchable jobs
   SegPlan pkagg;   // pubkey aggregation of multi-key sets (small packages)
   AggPlan agg;     // ... and as the batch-affine tree (large packages)
-  DevBuf d_agga, d_aggi, d_aggpre, d_aggtot, d_aggtinv;
+  DevBuf d_agga, d_aggi, d_aggpre, d_aggtot, d_aggflag;
   SegPlan phA_node;  // device 0 of a multi-device ticket: product of the gathered partials
   HostBuf h_mode;  // per-set sig_prep modes of a phase
   // pinned result mirrors
@@ -606,7 +601,7 @@ void slot_destroy(Slot* s) {
                     &s->d_Sb,   &s->d_fgb,    &s->d_Fb,   &s->d_bkt,    &s->d_bits,   &s->d_aux,   &s->d_gath,
                     &s->d_nodeF, &s->d_nodeV, &s->d_plan, &s->d_mid, &s->d_Hm, &s->d_hinfm,
                     &s->d_mmask, &s->d_PmP, &s->d_Pm, &s->d_pinfm, &s->d_errm, &s->d_xport,
-                    &s->d_agga, &s->d_aggi, &s->d_aggpre, &s->d_aggtot, &s->d_aggtinv};
+                    &s->d_agga, &s->d_aggi, &s->d_aggpre, &s->d_aggtot, &s->d_aggflag};
   for (DevBuf* b : bufs) free_dev(*b);
   for (auto& u : s->seg_tmp)
     for (DevBuf& b : u) free_dev(b);
@@ -697,16 +692,23 @@ int miller_k_for(size_t n_sets) {
   return n_sets >= 8192 ? 4 : (n_sets >= 1024 ? 2 : 1);
 }
 
-// PublicKey.aggregate of large packages as the batch-affine tree (A/B build: LSG_AGG_TREE=0
-// keeps the serial fold + butterfly of k_seg_reduce<0> for every package)
-bool agg_tree_on() { return lsg_ab_long("LSG_AGG_TREE", 1) != 0; }
+// PublicKey.aggregate of large packages as the batch-affine tree: A/B build only
+// (LSG_AGG_TREE=1).  Measured slower than the fused gather + mixed-addition fold
+// (k_pk_agg_seg) on config C: 2.7 ms against 1.44 ms for a 3.7M-key block package alone,
+// 0.90M against 0.98M sets/s loaded -- the per-level inversion, heap and
+// point round trips cost more than the four products per key the affine additions save.
+bool agg_tree_on() { return lsg_ab_long("LSG_AGG_TREE", 0) != 0; }
 
-// Minimum RLC group size for the bucket MSM (A/B build: env LSG_MSM_MIN_GROUP).  With 2-bit
-// windows a set costs ~24 bucket additions plus 4 of the group's 64 bit sums (~1k Fp
-// products) against a 64-bit scalar multiplication (~2.25k), and the group one Horner program
-// (~4k Fp products more than the plain ML(-G1, S) one): the MSM wins from ~4 sets.
+// Minimum RLC group size for the bucket MSM (A/B build: env LSG_MSM_MIN_GROUP).  By operation
+// count the MSM wins from ~4 sets (2-bit windows: ~24 bucket additions plus 4 of the group's 64
+// bit sums, ~1k Fp products, against ~2.25k for a 64-bit scalar multiplication; the group's
+// Horner program ~4k more), but the per-set [r_i] sig_i kernel runs near 0.3 of the mad peak
+// and the bucket and bit-sum reductions far below it, plus a Horner program per group: on
+// config C (64 groups of 128 sets) 1.05-1.08M sets/s without the MSM against 1.01M with it
+// (profiles/r04_msm_ab.txt).  The MSM stays for groups of 256 and more (8-bit windows: the
+// firehose's package group, the fallback phases' halves).
 size_t msm_min_group() {
-  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 4);
+  const long x = lsg_ab_long("LSG_MSM_MIN_GROUP", 256);
   return x < 1 ? (size_t)1 : (size_t)x;
 }
 // Window width c of a group's bucket MSM (plan_phase): per set 64/c digits (bucket
@@ -846,6 +848,26 @@ int run_seg(Slot* s, int use, const char* name, const SegPlan& P, const uint32_t
     const uint32_t* in = q.src == 0 ? src : tmp[q.src];
     KL(s, name, lsgk::seg_reduce(S_(s), P.op, q.n_chunks, q.ips_log2, PL(s, q.chunk_off), k == 0 ? idx : nullptr, in, dst,
                                  tmp[q.tmp_out]));
+  }
+  return LSG_OK;
+}
+
+// PublicKey.aggregate of the slot's multi-key sets by the segmented reduction, its first pass
+// fetching the staged keys itself (lsg_k_pk.hip k_pk_agg_seg; P = plan_pk_agg)
+int run_pk_seg(Slot* s, const SegPlan& P, uint32_t* dst) {
+  LSG_RC(size_seg(s, 0, P));
+  Dev* d = s->d;
+  uint32_t* tmp[3] = {nullptr, P_<uint32_t>(s->seg_tmp[0][0]), P_<uint32_t>(s->seg_tmp[0][1])};
+  for (size_t k = 0; k < P.passes.size(); k++) {
+    const SegPass& q = P.passes[k];
+    if (k == 0)
+      KL(s, "g1_aggregate", lsgk::pk_agg_seg(S_(s), q.n_chunks, q.ips_log2, PL(s, q.chunk_off), P_<uint8_t>(s->d_pk),
+                                             s->pk_stride, P_<uint32_t>(s->d_pklen), P_<int32_t>(s->d_pkerr),
+                                             P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n,
+                                             dst, tmp[q.tmp_out]));
+    else
+      KL(s, "g1_aggregate", lsgk::seg_reduce(S_(s), 0, q.n_chunks, q.ips_log2, PL(s, q.chunk_off), nullptr,
+                                             tmp[q.src], dst, tmp[q.tmp_out]));
   }
   return LSG_OK;
 }
@@ -1371,15 +1393,14 @@ int launch_set_stages(Slot* s, const SegPlan* pkagg, const PhasePlan& Ph, uint32
   LSG_HIP(s, hipStreamWaitEvent(s->st[1], s->ev_in, 0));
   if (!s->single_keys && s->agg.tree) {
     LSG_RC(launch_agg_tree(s, s->agg, P_<uint32_t>(s->d_agg)));
+  } else if (s->single_keys) {
+    // single-key sets decode straight into their aggregate slot
+    if (np > 0)
+      KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
+                                           P_<uint32_t>(s->d_agg), P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab),
+                                           P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
   } else {
-    if (np > 0) {
-      // single-key sets decode straight into their aggregate slot
-      uint32_t* dst = s->single_keys ? P_<uint32_t>(s->d_agg) : P_<uint32_t>(s->d_pkp);
-      KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen), dst,
-                                           P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok),
-                                           (uint32_t)d->pktab_n));
-    }
-    if (!s->single_keys) LSG_RC(run_seg(s, 0, "g1_aggregate", *pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
+    LSG_RC(run_pk_seg(s, *pkagg, P_<uint32_t>(s->d_agg)));  // (every staged key is in one set)
   }
   KL(s, "k_pk_scale", lsgk::pk_scale(S_(s), n, P_<uint32_t>(s->d_agg), P_<uint64_t>(s->d_rnd), P_<uint32_t>(s->d_Pp),
                                      P_<uint32_t>(s->d_zP), P_<uint8_t>(s->d_pinf)));
@@ -1446,93 +1467,112 @@ SegPlan plan_pk_agg(Slot* s) {
   return plan_seg(s->plan, 0, off, len, false, 0, 0);
 }
 
-// The batch-affine tree's plan for the slot's sets (keys of set i: pk_first[i] .. + pk_cnt[i],
-// gathered in that order into level 0).  A set takes part in a level while it has more than
-// AGG_FINAL_MAX points; then k_agg_final sums what it has left.
+// The batch-affine tree's plan for the slot's sets (keys of set i: pk_first[i] .. + pk_cnt[i]).
+// L is chosen by cost: a tree set of n keys costs ~7 products per level-0 point (padded to
+// 2^L: one fold product, five in the step, a share of the heaps) plus 11 per complete mixed
+// addition of its ceil(n / 2^L) level-L points; a set the tree would not make cheaper (few
+// keys, or padding too large) is summed from its keys directly by k_agg_final.
 AggPlan plan_agg_tree(Slot* s) {
   AggPlan P;
   P.tree = true;
   const size_t n = s->n_sets;
-  std::vector<int32_t> len(n), off(n), base(n, 0);
-  for (size_t i = 0; i < n; i++) {
-    len[i] = (int32_t)s->pk_cnt[i];
-    off[i] = (int32_t)s->pk_first[i];
-  }
-  size_t level_base = 0, level_size = s->n_pks;
-  std::vector<int32_t> parts;
-  for (;;) {
-    parts.clear();
-    for (size_t i = 0; i < n; i++)
-      if (len[i] > AGG_FINAL_MAX) parts.push_back((int32_t)i);
-    if (parts.empty()) break;
-    AggLevelPlan L;
-    L.n_seg = (int)parts.size();
-    L.base_in = level_base;
-    L.base_out = level_base + level_size;
-    L.plan_off = s->plan.size();
-    const size_t np = parts.size();
-    s->plan.resize(L.plan_off + 4 * np + 1);
-    int32_t* cum = s->plan.data() + L.plan_off;
-    int32_t* in_off = cum + np + 1;
-    int32_t* ln = in_off + np;
-    int32_t* out_off = ln + np;
-    int32_t items = 0;
-    for (size_t k = 0; k < np; k++) {
-      const int32_t i = parts[k];
-      cum[k] = items;
-      in_off[k] = off[i];
-      ln[k] = len[i];
-      out_off[k] = items;  // one output point per item
-      const int32_t m = (len[i] + 1) / 2;
-      items += m;
-      off[i] = out_off[k];
-      len[i] = m;
-      base[i] = (int32_t)L.base_out;
+  auto tree_cost = [](int64_t len, int L) {
+    const int64_t A = (int64_t)1 << L;
+    return ((len + A - 1) / A) * A * 7 + ((len + A - 1) / A) * 11;
+  };
+  int64_t best = -1;
+  for (int L = 0; L <= 9; L++) {
+    int64_t cost = 0;
+    for (size_t i = 0; i < n; i++) {
+      const int64_t len = (int64_t)s->pk_cnt[i];
+      cost += L > 0 ? std::min(tree_cost(len, L), len * 11) : len * 11;
     }
-    cum[np] = items;
-    L.n_items = items;
-    // chunks of T items per lane pair: up to 16 while at least 32k lane pairs stay busy
-    L.T = (int)std::max<int32_t>(1, std::min<int32_t>(16, items / 32768));
-    P.levels.push_back(L);
-    P.max_items = std::max(P.max_items, (size_t)items);
-    level_base = L.base_out;
-    level_size = (size_t)items;
+    if (best < 0 || cost < best) {
+      best = cost;
+      P.L = L;
+    }
   }
-  P.n_points = level_base + level_size;
-  P.src_off = s->plan.size();
+  const int64_t A = (int64_t)1 << P.L;
+  P.T = (int)std::max<long>(1, std::min<long>(64, lsg_ab_long("LSG_AGG_T", 8)));
+  std::vector<int32_t> o0(n, 0), src(3 * n);
+  int64_t N0 = 0;
   for (size_t i = 0; i < n; i++) {
-    s->plan.push_back(base[i]);
-    s->plan.push_back(off[i]);
-    s->plan.push_back(len[i]);
+    const int64_t len = (int64_t)s->pk_cnt[i];
+    if (P.L > 0 && tree_cost(len, P.L) < len * 11) {
+      o0[i] = (int32_t)N0;
+      src[3 * i] = 0;
+      src[3 * i + 1] = (int32_t)(N0 >> P.L);
+      src[3 * i + 2] = (int32_t)((len + A - 1) / A);
+      N0 += (len + A - 1) / A * A;
+    } else {
+      src[3 * i] = 1;
+      src[3 * i + 1] = (int32_t)s->pk_first[i];
+      src[3 * i + 2] = (int32_t)len;
+    }
   }
+  P.N0 = N0;
+  if (N0 == 0) P.L = 0;
+  if (P.L > 0) {
+    // lane pairs: a multiple of 128 << (L - 1), so that every level's grid is whole blocks
+    const int64_t unit = (int64_t)LSG_ITEMS_PER_BLOCK_HOST << (P.L - 1);
+    const int64_t need = (N0 / 2 + P.T - 1) / P.T;
+    P.n_c0 = (need + unit - 1) / unit * unit;
+    P.blk_off = s->plan.size();
+    s->plan.resize(P.blk_off + (size_t)(N0 >> P.L));
+    int32_t* blk = s->plan.data() + P.blk_off;
+    for (size_t i = 0; i < n; i++)
+      if (src[3 * i] == 0)
+        for (int32_t b = src[3 * i + 1], e = b + src[3 * i + 2]; b < e; b++) blk[b] = (int32_t)i;
+  }
+  P.o0_off = s->plan.size();
+  s->plan.insert(s->plan.end(), o0.begin(), o0.end());
+  P.len_off = s->plan.size();
+  for (size_t i = 0; i < n; i++) s->plan.push_back((int32_t)s->pk_cnt[i]);
+  P.pk0_off = s->plan.size();
+  for (size_t i = 0; i < n; i++) s->plan.push_back((int32_t)s->pk_first[i]);
+  P.src_off = s->plan.size();
+  s->plan.insert(s->plan.end(), src.begin(), src.end());
   return P;
 }
 
 // the tree over the staged keys into d_agg (side stream: after the inputs' upload)
 int launch_agg_tree(Slot* s, const AggPlan& P, uint32_t* agg) {
   Dev* d = s->d;
-  const size_t nk = std::max(s->n_pks, (size_t)1);
-  LSG_RC(ensure(s, s->d_agga, 4 * W_G1A * std::max(P.n_points, nk)));
-  LSG_RC(ensure(s, s->d_aggi, std::max(P.n_points, nk)));
-  LSG_RC(ensure(s, s->d_aggpre, 4 * W_FP * std::max(P.max_items, (size_t)1)));
-  LSG_RC(ensure(s, s->d_aggtot, 4 * W_FP * std::max(P.max_items, (size_t)1)));
-  LSG_RC(ensure(s, s->d_aggtinv, 4 * W_FP * std::max(P.max_items, (size_t)1)));
-  uint32_t* pts = P_<uint32_t>(s->d_agga);
-  uint8_t* inf = P_<uint8_t>(s->d_aggi);
-  KL(s, "k_pk_gather_aff", lsgk::pk_gather_aff(S_(s), (int)s->n_pks, P_<uint8_t>(s->d_pk), s->pk_stride,
-                                               P_<uint32_t>(s->d_pklen), pts, inf, P_<int32_t>(s->d_pkerr),
-                                               P_<uint32_t>(d->d_pktab), P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
-  for (const AggLevelPlan& L : P.levels) {
-    const int32_t* plan = PL(s, L.plan_off);
-    const size_t n_chunks = ((size_t)L.n_items + L.T - 1) / L.T;
-    KL(s, "g1_aggregate", lsgk::agg_fold(S_(s), L.n_items, L.T, plan, L.n_seg, pts + W_G1A * L.base_in, inf + L.base_in,
-                                         P_<uint32_t>(s->d_aggpre), P_<uint32_t>(s->d_aggtot)));
-    LSG_RC(batch_inv(s, 1, "binv_agg", P_<uint32_t>(s->d_aggtot), n_chunks, P_<uint32_t>(s->d_aggtinv)));
-    KL(s, "g1_aggregate", lsgk::agg_unfold(S_(s), L.n_items, L.T, plan, L.n_seg, pts + W_G1A * L.base_in,
-                                           inf + L.base_in, P_<uint32_t>(s->d_aggpre), P_<uint32_t>(s->d_aggtinv),
-                                           pts + W_G1A * L.base_out, inf + L.base_out));
+  lsgk::AggTreeArgs a;
+  a.L = P.L;
+  a.T = P.T;
+  a.n_c0 = P.n_c0;
+  a.N0 = P.N0;
+  a.blk_set = PL(s, P.blk_off);
+  a.set_o0 = PL(s, P.o0_off);
+  a.set_len = PL(s, P.len_off);
+  a.set_pk0 = PL(s, P.pk0_off);
+  a.pk = P_<uint8_t>(s->d_pk);
+  a.stride = s->pk_stride;
+  a.pk_len = P_<uint32_t>(s->d_pklen);
+  a.pk_err = P_<int32_t>(s->d_pkerr);
+  a.tab = P_<uint32_t>(d->d_pktab);
+  a.tab_ok = P_<uint8_t>(d->d_pktab_ok);
+  a.tab_n = (uint32_t)d->pktab_n;
+  if (P.L > 0) {
+    const size_t npts = (size_t)(2 * P.N0), pre_w = W_FP * (size_t)(P.T * P.n_c0), cinv_w = W_FP * (size_t)P.n_c0;
+    LSG_RC(ensure(s, s->d_agga, 4 * W_G1A * npts));
+    LSG_RC(ensure(s, s->d_aggi, npts));
+    LSG_RC(ensure(s, s->d_aggpre, 4 * 2 * pre_w));
+    LSG_RC(ensure(s, s->d_aggtot, 4 * 2 * cinv_w));
+    LSG_RC(ensure(s, s->d_aggflag, 2 * (size_t)P.n_c0));
+    a.pts = P_<uint32_t>(s->d_agga);
+    a.inf = P_<uint8_t>(s->d_aggi);
+    a.pre[0] = P_<uint32_t>(s->d_aggpre);
+    a.pre[1] = a.pre[0] + pre_w;
+    a.cinv[0] = P_<uint32_t>(s->d_aggtot);
+    a.cinv[1] = a.cinv[0] + cinv_w;
+    a.flag[0] = P_<uint8_t>(s->d_aggflag);
+    a.flag[1] = a.flag[0] + P.n_c0;
+    KL(s, "g1_aggregate", lsgk::agg_leaf(S_(s), a));
+    for (int t = 0; t < P.L; t++) KL(s, "g1_aggregate", lsgk::agg_step(S_(s), a, t));
   }
-  KL(s, "g1_aggregate", lsgk::agg_final(S_(s), (int)s->n_sets, PL(s, P.src_off), pts, inf, agg));
+  KL(s, "g1_aggregate", lsgk::agg_final(S_(s), a, (int)s->n_sets, PL(s, P.src_off), agg));
   return LSG_OK;
 }
 
@@ -2789,9 +2829,9 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
   if (need > d->pktab_cap) {
     const size_t cap = std::max(std::max(need, 2 * d->pktab_cap), (size_t)1024);
     DevBuf nt, nok;
-    LSG_HIPC(c, hipMalloc(&nt.p, 4 * W_G1A * cap));
+    LSG_HIPC(c, hipMalloc(&nt.p, 4 * W_TAB * cap));
     g_allocs++;
-    nt.cap = 4 * W_G1A * cap;
+    nt.cap = 4 * W_TAB * cap;
     hipError_t e = hipMalloc(&nok.p, cap);
     if (e != hipSuccess) {
       free_dev(nt);
@@ -2801,7 +2841,7 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
     nok.cap = cap;
     LSG_HIPC(c, hipMemset(nok.p, 0, cap));
     if (d->pktab_n) {
-      LSG_HIPC(c, hipMemcpy(nt.p, d->d_pktab.p, 4 * W_G1A * d->pktab_n, hipMemcpyDeviceToDevice));
+      LSG_HIPC(c, hipMemcpy(nt.p, d->d_pktab.p, 4 * W_TAB * d->pktab_n, hipMemcpyDeviceToDevice));
       LSG_HIPC(c, hipMemcpy(nok.p, d->d_pktab_ok.p, d->pktab_n, hipMemcpyDeviceToDevice));
     }
     free_dev(d->d_pktab);
@@ -2816,7 +2856,7 @@ int dev_pktab_set(Dev* d, size_t first, const uint8_t* pks, uint32_t pk_len, siz
   // infinity key, 0 = no key
   LSG_RC(ensure(s, s->d_ub, n));
   KL(s, "k_pk_gather_aff", lsgk::pk_gather_aff(S_(s), (int)n, P_<uint8_t>(s->d_pk), s->pk_stride,
-                                               P_<uint32_t>(s->d_pklen), P_<uint32_t>(d->d_pktab) + W_G1A * first,
+                                               P_<uint32_t>(s->d_pklen), P_<uint32_t>(d->d_pktab) + W_TAB * first,
                                                P_<uint8_t>(s->d_ub), P_<int32_t>(s->d_pkerr), nullptr, nullptr, 0u));
   pkerr.assign(n, 0);
   std::vector<uint8_t> inf(n);
@@ -3320,10 +3360,7 @@ int lsg_aggregate_pubkeys_multi(lsg_ctx* c, const lsg_set* sets, size_t n_sets, 
   if (tree) {
     LSG_RC(launch_agg_tree(s, s->agg, P_<uint32_t>(s->d_agg)));
   } else if (np) {
-    KL(s, "k_pk_decode", lsgk::pk_decode(S_(s), (int)np, P_<uint8_t>(s->d_pk), s->pk_stride, P_<uint32_t>(s->d_pklen),
-                                         P_<uint32_t>(s->d_pkp), P_<int32_t>(s->d_pkerr), P_<uint32_t>(d->d_pktab),
-                                         P_<uint8_t>(d->d_pktab_ok), (uint32_t)d->pktab_n));
-    LSG_RC(run_seg(s, 0, "g1_aggregate", s->pkagg, P_<uint32_t>(s->d_pkp), P_<uint32_t>(s->d_agg)));
+    LSG_RC(run_pk_seg(s, s->pkagg, P_<uint32_t>(s->d_agg)));
   }
   LSG_RC(ensure(s, s->d_aux, 96 * n_sets));
   KL(s, "k_g1p_to_bytes", lsgk::g1p_to_bytes(S_(s), (int)n_sets, P_<uint32_t>(s->d_agg), P_<uint8_t>(s->d_aux)));

@@ -20,7 +20,8 @@ LSG_DEVI int pk_fetch_aff(size_t item, const uint8_t* __restrict__ pk, uint32_t 
     const uint8_t* b = pk + (size_t)stride * item;
     const uint32_t idx = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
     const uint8_t ok = idx < tab_n ? tab_ok[idx] : 0;
-    a = lane_load<g1a_t>(tab, ok == 1 ? idx : 0);  // (row 0 for an infinite or missing key: unused)
+    // one 128-byte row per key (row 0 for an infinite or missing key: unused)
+    a = lane_load<g1a_t>(tab + (size_t)(ok == 1 ? idx : 0) * lsgl::W_TAB, 0);
     is_inf = ok != 1;
     return ok ? 0 : LSG_ERR_BAD_INDEX;
   }
@@ -46,8 +47,49 @@ __global__ void LSG_KERNEL_ATTR k_pk_decode(int n, const uint8_t* __restrict__ p
   if (lead) err[item] = e;
 }
 
-// pubkey -> affine G1 + infinity flag (the first level of the aggregation tree below; the
-// table rows of lsg_pubkey_table_set)
+// PublicKey.aggregate of many sets' keys straight from the staged keys (utils.ts:11; SURVEY.md
+// 8a M1): one pass of the segmented reduction (lsg_k_reduce.hip k_seg_reduce, plan_seg) whose
+// elements are fetched as affine points (table row or decoded bytes) and folded with complete
+// mixed additions -- no projective copy of every key written and read back -- then the
+// chunk's lane pairs combined by a butterfly.  Chunk = (first key, count, output: >= 0 into
+// dst, < 0 into tmp for a second pass).
+__global__ void LSG_KERNEL_ATTR k_pk_agg_seg(int n_chunks, int ips_log2, const int32_t* __restrict__ chunks,
+                                             const uint8_t* __restrict__ pk, uint32_t stride,
+                                             const uint32_t* __restrict__ pk_len, int32_t* __restrict__ err,
+                                             const uint32_t* __restrict__ tab, const uint8_t* __restrict__ tab_ok,
+                                             uint32_t tab_n, uint32_t* __restrict__ dst, uint32_t* __restrict__ tmp) {
+  lsg_lane_setup();
+  const size_t item = gtid() / LSG_GROUP;
+  const bool lead = (threadIdx.x % LSG_GROUP) == 0;
+  const size_t c = item >> ips_log2;
+  const int ips = 1 << ips_log2, j = (int)(item & (size_t)(ips - 1));
+  const bool active = c < (size_t)n_chunks;
+  g1p_t acc = proj_inf<fp_t>();
+  int out = 0;
+  if (active) {
+    const int off = chunks[3 * c], len = chunks[3 * c + 1];
+    out = chunks[3 * c + 2];
+#pragma unroll 1
+    for (int k = j; k < len; k += ips) {
+      g1a_t a;
+      bool is_inf;
+      const int e = pk_fetch_aff((size_t)(off + k), pk, stride, pk_len, tab, tab_ok, tab_n, a, is_inf);
+      if (lead) err[off + k] = e;
+      if (!is_inf) acc = proj_is_inf(acc) ? proj_from_aff(a) : g1_add_mixed(acc, a);
+    }
+  }
+  // every lane runs the butterfly: a chunk never straddles a wave (ips <= 32 pairs)
+#pragma unroll 1
+  for (int o = ips >> 1; o >= 1; o >>= 1) acc = g1_add(acc, shfl_xor_t(acc, LSG_GROUP * o));
+  if (active && j == 0) {
+    if (out >= 0)
+      lane_store(dst, (size_t)out, acc);
+    else
+      lane_store(tmp, (size_t)(-out - 1), acc);
+  }
+}
+
+// pubkey -> affine G1 + infinity flag: the rows (lsgl::W_TAB words each) of lsg_pubkey_table_set
 __global__ void LSG_KERNEL_ATTR k_pk_gather_aff(int n, const uint8_t* __restrict__ pk, uint32_t stride,
                                                 const uint32_t* __restrict__ pk_len, uint32_t* __restrict__ pts,
                                                 uint8_t* __restrict__ inf, int32_t* __restrict__ err,
@@ -57,189 +99,266 @@ __global__ void LSG_KERNEL_ATTR k_pk_gather_aff(int n, const uint8_t* __restrict
   g1a_t a;
   bool is_inf;
   const int e = pk_fetch_aff(item, pk, stride, pk_len, tab, tab_ok, tab_n, a, is_inf);
-  lane_store(pts, item, a);
+  lane_store(pts + item * lsgl::W_TAB, 0, a);
   if (lead) {
     err[item] = e;
     inf[item] = is_inf ? 1 : 0;
   }
 }
 
-// ---- PublicKey.aggregate of the many keys of aggregate sets (utils.ts:11)
-// as a pairwise tree of AFFINE additions with simultaneous inversion.  Level t holds every
-// set's points (affine + infinity flag), segment s = one set; item q adds the pair (2p, 2p+1)
-// of its segment (p = q - cum[s]; a lone last point is copied) into level t+1.  An affine
-// addition is lambda = dy / dx, x3 = lambda^2 - x1 - x2, y3 = lambda (x1 - x3) - y1: three
-// products plus one shared inversion, against twelve for a complete projective addition.  The
-// inversions of a whole level are ONE inversion (Montgomery's trick): k_agg_fold multiplies
-// each chunk of AGG_T items' denominators (prefix products kept), lsg_host.hip's batched
-// inversion inverts the chunk products, k_agg_unfold walks each chunk back and adds.  Per
-// addition ~6.3 products instead of 12.  Exceptional pairs (equal x: P + P or P - P) make
-// their chunk's product zero, which the batched inversion returns as zero; such a chunk is
-// redone in k_agg_unfold with doubling / infinity denominators and its own divstep inversion.
-// Segments shorter than AGG_FINAL_MAX points skip the levels: k_agg_final sums each set's
-// remaining points with complete mixed additions.
+// ---- PublicKey.aggregate of the keys of large packages (utils.ts:11) as a
+// pairwise tree of AFFINE additions with simultaneous inversion.  An affine addition is
+// lambda = dy / dx, x3 = lambda^2 - x1 - x2, y3 = lambda (x1 - x3) - y1: three products plus
+// a share of one inversion, against eleven for a complete mixed addition.
+//
+// Layout (lsg_launch.h AggTreeArgs): level 0 holds each tree set's keys at an offset aligned
+// to 2^L, padded with infinity; level t + 1 point q = level t points 2q + 2q + 1, so no pair
+// ever straddles two sets and no segment lookup is needed above level 0.  Lane pair c owns
+// the items q = c + j n_c(t), j < T: consecutive lane pairs touch consecutive points.
+//
+// The inversions of a level are one inversion per block (Montgomery's trick in two tiers):
+// each lane pair folds its T denominators (prefix products kept), the block multiplies its
+// chunk products in an LDS heap, inverts the root with one divstep inversion and runs the heap
+// back down, leaving every chunk's inverse (cinv).  k_agg_step(t) walks each chunk back adding
+// its pairs and -- fused -- folds level t + 1's denominators: the pair partner of output q is
+// output q ^ 1, held by the adjacent lane pair at the same step (a lane shuffle); its block
+// then inverts them the same way.  One launch per level, no global reduction between levels.
+// Equal x (P + P or P - P) gives a zero denominator, which zeroes its chunk product: the fold
+// tests each chunk product once and redoes such a chunk with the pairs resolved (doubling
+// denominator 2y, or 1 for P - P), flagging it so that the step resolves its pairs again.
 enum { AGG_ADD = 0, AGG_DBL = 1, AGG_INF = 2, AGG_COPY_A = 3, AGG_COPY_B = 4 };
 
-// level plan (lsg_host.hip agg_plan): cum[0..n_seg] item prefix counts, then in_off, len,
-// out_off per participating segment
-struct AggLevel {
-  const int32_t* cum;
-  const int32_t* in_off;
-  const int32_t* len;
-  const int32_t* out_off;
-  int n_seg;
-};
-LSG_DEVI AggLevel agg_level(const int32_t* plan, int n_seg) {
-  AggLevel L;
-  L.cum = plan;
-  L.in_off = plan + n_seg + 1;
-  L.len = L.in_off + n_seg;
-  L.out_off = L.len + n_seg;
-  L.n_seg = n_seg;
-  return L;
-}
-// segment of item q: the last s with cum[s] <= q
-LSG_DEVI int agg_seg(const AggLevel& L, int32_t q) {
-  int lo = 0, hi = L.n_seg - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L.cum[mid] <= q) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-// the pair of item q: input positions a (and b = a + 1 unless a is its segment's last point)
-LSG_DEVI void agg_pair(const AggLevel& L, int s, int32_t q, int32_t& a, bool& has_b, int32_t& out) {
-  const int32_t p = q - L.cum[s];
-  a = L.in_off[s] + 2 * p;
-  has_b = 2 * p + 1 < L.len[s];
-  out = L.out_off[s] + p;
-}
-// the type of item q from the infinity flags alone (equal-x pairs are found by the inversion)
-LSG_DEVI int agg_type(bool has_b, bool ia, bool ib) {
-  if (!has_b || ib) return ia ? AGG_INF : AGG_COPY_A;
-  return ia ? AGG_COPY_B : AGG_ADD;
-}
+LSG_DEVI int64_t agg_base(const lsgk::AggTreeArgs& a, int t) { return t == 0 ? 0 : 2 * a.N0 - (a.N0 >> (t - 1)); }
 
-__global__ void LSG_KERNEL_ATTR k_agg_fold(int n_items, int T, const int32_t* __restrict__ plan, int n_seg,
-                                           const uint32_t* __restrict__ pts, const uint8_t* __restrict__ inf,
-                                           uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
-  LANE_ITEM((n_items + T - 1) / T);
-  (void)lead;
-  const AggLevel L = agg_level(plan, n_seg);
-  const int32_t first = (int32_t)item * T, last = min(n_items, first + T);
-  int s = agg_seg(L, first);
-  const fp_t one = fp_one();
-  fp_t acc = one;
-#pragma unroll 1
-  for (int32_t q = first; q < last; q++) {
-    while (L.cum[s + 1] <= q) s++;
-    int32_t a, out;
-    bool has_b;
-    agg_pair(L, s, q, a, has_b, out);
-    const int ty = agg_type(has_b, inf[a] != 0, has_b && inf[a + 1] != 0);
-    fp_t den = one;
-    if (ty == AGG_ADD) den = fp_sub(lane_load<fp_t>(pts, (size_t)(a + 1) * 2), lane_load<fp_t>(pts, (size_t)a * 2));
-    acc = q == first ? den : fp_mul(acc, den);
-    lane_store(pre, q, acc);
-  }
-  lane_store(tot, item, acc);
-}
-
-// the denominators of items first..last-1 with the equal-x pairs resolved (doubling: 2 y1;
-// P - P: 1), their prefix products rewritten into pre, and the chunk inverse by divsteps
-LSG_DEVI fp_t agg_chunk_redo(const AggLevel& L, int32_t first, int32_t last, const uint32_t* __restrict__ pts,
-                             const uint8_t* __restrict__ inf, uint32_t* __restrict__ pre) {
-  int s = agg_seg(L, first);
-  const fp_t one = fp_one();
-  fp_t acc = one;
-#pragma unroll 1
-  for (int32_t q = first; q < last; q++) {
-    while (L.cum[s + 1] <= q) s++;
-    int32_t a, out;
-    bool has_b;
-    agg_pair(L, s, q, a, has_b, out);
-    const int ty = agg_type(has_b, inf[a] != 0, has_b && inf[a + 1] != 0);
-    fp_t den = one;
-    if (ty == AGG_ADD) {
-      const g1a_t A = lane_load<g1a_t>(pts, a), B = lane_load<g1a_t>(pts, a + 1);
-      den = fp_sub(B.x, A.x);
-      if (fp_is_zero(den)) den = fp_eq(A.y, B.y) ? fp_add(A.y, A.y) : one;
+// the addition type of (A, B) with its denominator and numerator; exact: equal x resolved,
+// else such a pair gives den == 0 (found by the chunk test)
+LSG_DEVI int agg_den(const g1a_t& A, bool ia, const g1a_t& B, bool ib, bool exact, fp_t& den, fp_t& num) {
+  den = fp_one();
+  num = den;
+  if (ia) return ib ? AGG_INF : AGG_COPY_B;
+  if (ib) return AGG_COPY_A;
+  den = fp_sub(B.x, A.x);
+  num = fp_sub(B.y, A.y);
+  if (exact && fp_is_zero(den)) {
+    if (fp_is_zero(num)) {
+      den = fp_add(A.y, A.y);
+      const fp_t x2 = fp_mul(A.x, A.x);
+      num = fp_add(fp_add(x2, x2), x2);
+      return AGG_DBL;
     }
-    acc = q == first ? den : fp_mul(acc, den);
-    lane_store(pre, q, acc);
+    den = fp_one();
+    return AGG_INF;
   }
-  const fp_t d = pair_inv_gcd(pair_canon(acc));  // (acc R)^-1 as an integer
-  return pair_mont_mul(d, fp_t(FP_RCUBE));        // acc^-1 R
+  return AGG_ADD;
 }
 
-__global__ void LSG_KERNEL_ATTR k_agg_unfold(int n_items, int T, const int32_t* __restrict__ plan, int n_seg,
-                                             const uint32_t* __restrict__ pts, const uint8_t* __restrict__ inf,
-                                             uint32_t* __restrict__ pre, const uint32_t* __restrict__ tinv,
-                                             uint32_t* __restrict__ out_pts, uint8_t* __restrict__ out_inf) {
-  LANE_ITEM((n_items + T - 1) / T);
-  const AggLevel L = agg_level(plan, n_seg);
-  const int32_t first = (int32_t)item * T, last = min(n_items, first + T);
-  fp_t acc = lane_load<fp_t>(tinv, item);  // 1 / (product of the chunk's denominators)
-  // a zero chunk inverse: an equal-x pair in the chunk (rare): resolve it and invert alone
-  const bool redo = fp_is_zero(acc);
-  if (redo) acc = agg_chunk_redo(L, first, last, pts, inf, pre);
-  int s = agg_seg(L, last - 1);
-  const fp_t one = fp_one();
+// level-0 point p: key p - o of its set, or infinity in the padding
+LSG_DEVI void agg_fetch0(const lsgk::AggTreeArgs& a, int64_t p, g1a_t& P, bool& pinf, bool lead) {
+  const int s = a.blk_set[p >> a.L];
+  const int64_t k = p - a.set_o0[s];
+  pinf = true;
+  P.x = fp_zero();
+  P.y = P.x;
+  if (k < a.set_len[s]) {
+    const size_t key = (size_t)a.set_pk0[s] + (size_t)k;
+    const int e = pk_fetch_aff(key, a.pk, a.stride, a.pk_len, a.tab, a.tab_ok, a.tab_n, P, pinf);
+    if (lead) a.pk_err[key] = e;
+  }
+}
+
+// a chunk's fold again with its equal-x pairs resolved (the points are in memory): prefix
+// products rewritten, the chunk product returned.  asc: the level's fold order is j = 0..T-1.
+LSG_DEVI fp_t agg_redo(const uint32_t* __restrict__ pts, const uint8_t* __restrict__ inf, uint32_t* __restrict__ pre,
+                       int64_t c, int64_t nc, int64_t n_items, int T, bool asc) {
+  fp_t acc = fp_one();
 #pragma unroll 1
-  for (int32_t q = last - 1; q >= first; q--) {
-    while (L.cum[s] > q) s--;
-    int32_t a, o;
-    bool has_b;
-    agg_pair(L, s, q, a, has_b, o);
-    const bool ia = inf[a] != 0, ib = has_b && inf[a + 1] != 0;
-    int ty = agg_type(has_b, ia, ib);
-    const g1a_t A = lane_load<g1a_t>(pts, a);
-    g1a_t B = A;
-    if (has_b) B = lane_load<g1a_t>(pts, a + 1);
-    fp_t den = fp_sub(B.x, A.x), num = fp_sub(B.y, A.y);
-    if (redo && ty == AGG_ADD && fp_is_zero(den)) {  // equal x: P + P or P + (-P)
-      if (fp_is_zero(num)) {
-        ty = AGG_DBL;
-        den = fp_add(A.y, A.y);
-        const fp_t x2 = fp_mul(A.x, A.x);
-        num = fp_add(fp_add(x2, x2), x2);
-      } else {
-        ty = AGG_INF;
+  for (int k = 0; k < T; k++) {
+    const int64_t q = c + (int64_t)(asc ? k : T - 1 - k) * nc;
+    fp_t den = fp_one(), num;
+    if (q < n_items)
+      agg_den(lane_load<g1a_t>(pts, 2 * q), inf[2 * q] != 0, lane_load<g1a_t>(pts, 2 * q + 1), inf[2 * q + 1] != 0,
+              true, den, num);
+    acc = k == 0 ? den : fp_mul(acc, den);
+    lane_store(pre, q, acc);
+  }
+  return acc;
+}
+
+// The LDS heap of a fold group of G leaves (nodes G..2G-1; node 1 = the product of all):
+// lane pair `leaf` (< 0: none) contributes v.  Every thread of the block calls it.
+template <int G>
+LSG_DEVI void heap_up(uint32_t* Hg, int leaf, const fp_t& v) {
+  if (leaf >= 0) lane_store(Hg, G + leaf, v);
+#pragma unroll 1
+  for (int w = G / 2; w >= 1; w >>= 1) {
+    __syncthreads();
+    if (leaf >= 0 && leaf < w)
+      lane_store(Hg, w + leaf, fp_mul(lane_load<fp_t>(Hg, 2 * (w + leaf)), lane_load<fp_t>(Hg, 2 * (w + leaf) + 1)));
+  }
+  __syncthreads();
+}
+// ... and down: Ig[1] (set by the caller) = 1 / Hg[1]; leaves' inverses in Ig[G..2G-1]
+template <int G>
+LSG_DEVI void heap_down(const uint32_t* Hg, uint32_t* Ig, int leaf) {
+#pragma unroll 1
+  for (int w = 2; w <= G; w <<= 1) {
+    __syncthreads();
+    if (leaf < w) {
+      const int i = w + leaf;
+      lane_store(Ig, i, fp_mul(lane_load<fp_t>(Ig, i >> 1), lane_load<fp_t>(Hg, i ^ 1)));
+    }
+  }
+  __syncthreads();
+}
+
+// every participating lane pair's 1 / v: heap up, the root inverted (lane pair 0, divsteps),
+// heap down.  G leaves; every thread of the block calls it; H, I: 2G-node LDS heaps.
+template <int G>
+LSG_DEVI fp_t block_inv(uint32_t* H, uint32_t* I, int leaf, const fp_t& v) {
+  heap_up<G>(H, leaf, v);
+  if (leaf == 0) {
+    const fp_t d = pair_inv_gcd(pair_canon(lane_load<fp_t>(H, 1)));  // (x R)^-1 as an integer
+    lane_store(I, 1, pair_mont_mul(d, fp_t(FP_RCUBE)));                // x^-1 R
+  }
+  heap_down<G>(H, I, leaf < 0 ? G : leaf);
+  return leaf >= 0 ? lane_load<fp_t>(I, G + leaf) : v;
+}
+
+// level 0: gather each item's two keys, fold the chunk, invert the block's chunk products
+__global__ void LSG_KERNEL_ATTR k_agg_leaf(lsgk::AggTreeArgs a) {
+  __shared__ uint32_t H[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP], I[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP];
+  lsg_lane_setup();
+  const int l = (int)(threadIdx.x / LSG_GROUP);
+  const bool lead = (threadIdx.x % LSG_GROUP) == 0;
+  const int64_t c = (int64_t)blockIdx.x * LSG_ITEMS_PER_BLOCK + l, nc = a.n_c0, n_items = a.N0 >> 1;
+  fp_t acc = fp_one();
+#pragma unroll 1
+  for (int j = 0; j < a.T; j++) {
+    const int64_t q = c + (int64_t)j * nc;
+    fp_t den = fp_one(), num;
+    if (q < n_items) {
+      g1a_t A, B;
+      bool ia, ib;
+      agg_fetch0(a, 2 * q, A, ia, lead);
+      agg_fetch0(a, 2 * q + 1, B, ib, lead);
+      lane_store(a.pts, 2 * q, A);
+      lane_store(a.pts, 2 * q + 1, B);
+      if (lead) {
+        a.inf[2 * q] = ia ? 1 : 0;
+        a.inf[2 * q + 1] = ib ? 1 : 0;
       }
+      agg_den(A, ia, B, ib, false, den, num);
     }
-    if (ty != AGG_ADD && ty != AGG_DBL) den = one;
-    const fp_t inv = q > first ? fp_mul(acc, lane_load<fp_t>(pre, q - 1)) : acc;
-    if (q > first) acc = fp_mul(acc, den);
+    acc = j == 0 ? den : fp_mul(acc, den);
+    lane_store(a.pre[0], q, acc);
+  }
+  const bool redo = fp_is_zero(acc);  // an equal-x pair (rare)
+  if (redo) acc = agg_redo(a.pts, a.inf, a.pre[0], c, nc, n_items, a.T, true);
+  if (lead) a.flag[0][c] = redo ? 1 : 0;
+  lane_store(a.cinv[0], c, block_inv<LSG_ITEMS_PER_BLOCK>(H, I, l, acc));
+}
+
+// level t: chunks walked back (each pair added into level t + 1), level t + 1's denominators
+// folded on the way (even lane pairs: its item q / 2 = outputs q, q + 1) and inverted
+__global__ void LSG_KERNEL_ATTR k_agg_step(lsgk::AggTreeArgs a, int t) {
+  constexpr int G = LSG_ITEMS_PER_BLOCK / 2;
+  __shared__ uint32_t H[2 * G * lsgl::W_FP], I[2 * G * lsgl::W_FP];
+  lsg_lane_setup();
+  const int l = (int)(threadIdx.x / LSG_GROUP);
+  const bool lead = (threadIdx.x % LSG_GROUP) == 0;
+  const int64_t nc = a.n_c0 >> t, c = (int64_t)blockIdx.x * LSG_ITEMS_PER_BLOCK + l, n_items = a.N0 >> (t + 1);
+  const int T = a.T;
+  fp_t acc = lane_load<fp_t>(a.cinv[t & 1], c);  // 1 / (this chunk's product)
+
+  const bool asc = (t & 1) == 0;  // level t's fold order: j ascending for even t
+  const bool exact = a.flag[t & 1][c] != 0;
+  const bool next = t + 1 < a.L, even = (l & 1) == 0;
+  const uint32_t* pin = a.pts + lsgl::W_G1A * agg_base(a, t);
+  const uint8_t* iin = a.inf + agg_base(a, t);
+  uint32_t* pout = a.pts + lsgl::W_G1A * agg_base(a, t + 1);
+  uint8_t* iout = a.inf + agg_base(a, t + 1);
+  const uint32_t* pre = a.pre[t & 1];
+  uint32_t* pre2 = a.pre[(t + 1) & 1];
+  fp_t acc2 = fp_one();
+#pragma unroll 1
+  for (int k = T - 1; k >= 0; k--) {
+    const int64_t q = c + (int64_t)(asc ? k : T - 1 - k) * nc;
+    g1a_t A, B;
+    bool ia = true, ib = true;
+    fp_t den = fp_one(), num = den;
+    int ty = AGG_INF;
+    if (q < n_items) {
+      A = lane_load<g1a_t>(pin, 2 * q);
+      B = lane_load<g1a_t>(pin, 2 * q + 1);
+      ia = iin[2 * q] != 0;
+      ib = iin[2 * q + 1] != 0;
+      ty = agg_den(A, ia, B, ib, exact, den, num);
+    } else {
+      A.x = fp_zero();
+      A.y = A.x;
+      B = A;
+    }
+    fp_t inv = acc;
+    if (k > 0) {
+      inv = fp_mul(acc, lane_load<fp_t>(pre, c + (int64_t)(asc ? k - 1 : T - k) * nc));
+      acc = fp_mul(acc, den);
+    }
     const fp_t lam = fp_mul(num, inv);
-    const fp_t x3 = fp_sub(fp_sub(fp_mul(lam, lam), A.x), B.x);
     g1a_t R;
-    R.x = x3;
-    R.y = fp_sub(fp_mul(lam, fp_sub(A.x, x3)), A.y);
-    bool rinf = false;
+    R.x = fp_sub(fp_sub(fp_mul(lam, lam), A.x), B.x);
+    R.y = fp_sub(fp_mul(lam, fp_sub(A.x, R.x)), A.y);
+    bool rinf = ty == AGG_INF;
     if (ty == AGG_COPY_A) R = A;
     if (ty == AGG_COPY_B) R = B;
-    if (ty == AGG_INF) rinf = true;
-    if (ty == AGG_COPY_A) rinf = ia;
-    lane_store(out_pts, o, R);
-    if (lead) out_inf[o] = rinf ? 1 : 0;
+    if (q < n_items) {
+      lane_store(pout, q, R);
+      if (lead) iout[q] = rinf ? 1 : 0;
+    }
+    if (next) {  // level t + 1 item q / 2 (even lane pairs): (R, the partner's output q + 1)
+      const g1a_t Rp = shfl_xor_t(R, LSG_GROUP);
+      const bool rpinf = __shfl_xor(rinf ? 1 : 0, LSG_GROUP, 64) != 0;
+      fp_t den2, num2;
+      agg_den(R, rinf, Rp, rpinf, false, den2, num2);
+      acc2 = k == T - 1 ? den2 : fp_mul(acc2, den2);
+      if (even) lane_store(pre2, q >> 1, acc2);
+    }
   }
+  if (!next) return;  // (uniform: no barrier follows)
+  __threadfence_block();  // level t + 1's points, for a redo by the even lane pair
+  const int64_t c2 = c >> 1, nc2 = nc >> 1, n2 = n_items >> 1;
+  const bool redo = even && fp_is_zero(acc2);
+  if (redo) acc2 = agg_redo(pout, iout, pre2, c2, nc2, n2, T, !asc);
+  if (even && lead) a.flag[(t + 1) & 1][c2] = redo ? 1 : 0;
+  const fp_t inv2 = block_inv<G>(H, I, even ? l / 2 : -1, acc2);
+  if (even) lane_store(a.cinv[(t + 1) & 1], c2, inv2);
 }
 
-// each set's remaining points (segment [off, off + len) of its last level) summed with
-// complete mixed additions -> projective aggregate (the identity for none / all infinite)
-__global__ void LSG_KERNEL_ATTR k_agg_final(int n_sets, const int32_t* __restrict__ src, const uint32_t* __restrict__ arena,
-                                            const uint8_t* __restrict__ inf_arena, uint32_t* __restrict__ agg) {
+// each set's points summed with complete mixed additions -> projective aggregate (the
+// identity for none / all infinite): (0, off, n) level-L points, (1, key, n) staged keys
+__global__ void LSG_KERNEL_ATTR k_agg_final(lsgk::AggTreeArgs a, int n_sets, const int32_t* __restrict__ src,
+                                            uint32_t* __restrict__ agg) {
   LANE_ITEM(n_sets);
-  (void)lead;
-  const int32_t base = src[3 * item], off = src[3 * item + 1], len = src[3 * item + 2];
-  const uint32_t* pts = arena + (size_t)base * lsgl::W_G1A;
-  const uint8_t* inf = inf_arena + base;
+  const int32_t mode = src[3 * item], off = src[3 * item + 1], len = src[3 * item + 2];
   g1p_t acc = proj_inf<fp_t>();
+  if (mode == 0) {
+    const uint32_t* pts = a.pts + lsgl::W_G1A * agg_base(a, a.L);
+    const uint8_t* inf = a.inf + agg_base(a, a.L);
 #pragma unroll 1
-  for (int32_t k = 0; k < len; k++) {
-    if (inf[off + k]) continue;
-    const g1a_t a = lane_load<g1a_t>(pts, off + k);
-    acc = proj_is_inf(acc) ? proj_from_aff(a) : g1_add_mixed(acc, a);
+    for (int32_t k = 0; k < len; k++) {
+      if (inf[off + k]) continue;
+      const g1a_t p = lane_load<g1a_t>(pts, off + k);
+      acc = proj_is_inf(acc) ? proj_from_aff(p) : g1_add_mixed(acc, p);
+    }
+  } else {
+#pragma unroll 1
+    for (int32_t k = 0; k < len; k++) {
+      g1a_t p;
+      bool pinf;
+      const int e = pk_fetch_aff((size_t)off + k, a.pk, a.stride, a.pk_len, a.tab, a.tab_ok, a.tab_n, p, pinf);
+      if (lead) a.pk_err[off + k] = e;
+      if (pinf) continue;
+      acc = proj_is_inf(acc) ? proj_from_aff(p) : g1_add_mixed(acc, p);
+    }
   }
   lane_store(agg, item, acc);
 }
@@ -369,17 +488,23 @@ hipError_t pk_gather_aff(hipStream_t st, int n, const uint8_t* pk, uint32_t stri
                          uint8_t* inf, int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n) {
   LSG_LAUNCH_ITEMS(k_pk_gather_aff, n, st, n, pk, stride, pk_len, pts, inf, err, tab, tab_ok, tab_n);
 }
-hipError_t agg_fold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
-                    const uint8_t* inf, uint32_t* pre, uint32_t* tot) {
-  LSG_LAUNCH_ITEMS(k_agg_fold, (n_items + T - 1) / T, st, n_items, T, plan, n_seg, pts, inf, pre, tot);
+hipError_t pk_agg_seg(hipStream_t st, int n_chunks, int ips_log2, const int32_t* chunks, const uint8_t* pk, uint32_t stride,
+                      const uint32_t* pk_len, int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n,
+                      uint32_t* dst, uint32_t* tmp) {
+  LSG_LAUNCH_ITEMS(k_pk_agg_seg, (size_t)n_chunks << ips_log2, st, n_chunks, ips_log2, chunks, pk, stride, pk_len, err,
+                   tab, tab_ok, tab_n, dst, tmp);
 }
-hipError_t agg_unfold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
-                      const uint8_t* inf, uint32_t* pre, const uint32_t* tinv, uint32_t* out_pts, uint8_t* out_inf) {
-  LSG_LAUNCH_ITEMS(k_agg_unfold, (n_items + T - 1) / T, st, n_items, T, plan, n_seg, pts, inf, pre, tinv, out_pts, out_inf);
+hipError_t agg_leaf(hipStream_t st, const AggTreeArgs& a) {
+  if (a.L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_agg_leaf, dim3((unsigned)(a.n_c0 / LSG_ITEMS_PER_BLOCK)), dim3(LSG_TPB), 0, st, a);
+  return hipGetLastError();
 }
-hipError_t agg_final(hipStream_t st, int n_sets, const int32_t* src, const uint32_t* arena, const uint8_t* inf_arena,
-                     uint32_t* agg) {
-  LSG_LAUNCH_ITEMS(k_agg_final, n_sets, st, n_sets, src, arena, inf_arena, agg);
+hipError_t agg_step(hipStream_t st, const AggTreeArgs& a, int t) {
+  hipLaunchKernelGGL(k_agg_step, dim3((unsigned)((a.n_c0 >> t) / LSG_ITEMS_PER_BLOCK)), dim3(LSG_TPB), 0, st, a, t);
+  return hipGetLastError();
+}
+hipError_t agg_final(hipStream_t st, const AggTreeArgs& a, int n_sets, const int32_t* src, uint32_t* agg) {
+  LSG_LAUNCH_ITEMS(k_agg_final, n_sets, st, a, n_sets, src, agg);
 }
 hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err) {
   LSG_LAUNCH_ITEMS(k_pk_validate, n, st, n, pk, len, pts, err);

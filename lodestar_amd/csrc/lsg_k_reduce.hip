@@ -17,18 +17,6 @@ namespace {
 #include "lsg_inv.hpp"
 }  // namespace
 
-template <class T>
-LSG_DEVI T shfl_xor_t(const T& v, int lane_mask) {
-  constexpr int W = sizeof(T) / 4;
-  uint32_t w[W];
-  __builtin_memcpy(w, &v, sizeof(T));
-#pragma unroll
-  for (int k = 0; k < W; k++) w[k] = (uint32_t)__shfl_xor((int)w[k], lane_mask, 64);
-  T r;
-  __builtin_memcpy(&r, w, sizeof(T));
-  return r;
-}
-
 template <int OP>
 struct seg_op;
 template <>

@@ -61,6 +61,19 @@ static __device__ __forceinline__ T lds_unpark(const uint32_t* l) {
   return v;
 }
 
+// v from lane (lane id ^ lane_mask), word by word
+template <class T>
+static __device__ __forceinline__ T shfl_xor_t(const T& v, int lane_mask) {
+  constexpr int W = sizeof(T) / 4;
+  uint32_t w[W];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < W; k++) w[k] = (uint32_t)__shfl_xor((int)w[k], lane_mask, 64);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 #define LANE_ITEM(n)                        \
   lsg_lane_setup();                         \

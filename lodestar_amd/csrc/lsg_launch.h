@@ -49,17 +49,43 @@ hipError_t sign(hipStream_t st, int n, const uint8_t* sks, const uint32_t* H, ui
 hipError_t pk_decode(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
                      int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
 hipError_t pk_validate(hipStream_t st, int n, const uint8_t* pk, uint32_t len, uint32_t* pts, int32_t* err);
-// keys -> affine points + infinity flags + per-key errors (table rows by index, or decoded bytes)
+// keys -> pubkey-table rows (lsgl::W_TAB words: affine point) + infinity flags + per-key errors
 hipError_t pk_gather_aff(hipStream_t st, int n, const uint8_t* pk, uint32_t stride, const uint32_t* pk_len, uint32_t* pts,
                          uint8_t* inf, int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n);
-// the batch-affine aggregation tree (lsg_k_pk.hip): one level = fold (chunks of T items) +
-// batched inversion of the chunk products (host) + unfold; k_agg_final sums each set's rest
-hipError_t agg_fold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
-                    const uint8_t* inf, uint32_t* pre, uint32_t* tot);
-hipError_t agg_unfold(hipStream_t st, int n_items, int T, const int32_t* plan, int n_seg, const uint32_t* pts,
-                      const uint8_t* inf, uint32_t* pre, const uint32_t* tinv, uint32_t* out_pts, uint8_t* out_inf);
-hipError_t agg_final(hipStream_t st, int n_sets, const int32_t* src, const uint32_t* arena, const uint8_t* inf_arena,
-                     uint32_t* agg);
+// the first pass of a segmented G1 sum over staged keys (plan_seg chunks; later passes:
+// seg_reduce op 0 over tmp): keys fetched and folded with mixed additions, errors to err
+hipError_t pk_agg_seg(hipStream_t st, int n_chunks, int ips_log2, const int32_t* chunks, const uint8_t* pk, uint32_t stride,
+                      const uint32_t* pk_len, int32_t* err, const uint32_t* tab, const uint8_t* tab_ok, uint32_t tab_n,
+                      uint32_t* dst, uint32_t* tmp);
+// the batch-affine aggregation tree (lsg_k_pk.hip k_agg_*; plan: lsg_host.hip plan_agg_tree).
+// Level 0 holds every tree set's keys at an offset aligned to 2^L, padded with infinity up to
+// the next multiple (N0 points); level t + 1 point q is the sum of level t points 2q and
+// 2q + 1, so level L holds each set's sum in ceil(len / 2^L) points.  Level t's items (point
+// pairs) q = c + j n_c(t) belong to lane pair c (j < T; n_c(t) = n_c0 >> t).
+struct AggTreeArgs {
+  int L = 0, T = 1;          // levels, items per lane pair
+  int64_t n_c0 = 0, N0 = 0;  // level-0 lane pairs (a multiple of 128 << (L - 1)), points
+  const int32_t* blk_set = nullptr;  // set of each 2^L block of level 0
+  const int32_t* set_o0 = nullptr;   // per set: level-0 offset, key count, first staged key
+  const int32_t* set_len = nullptr;
+  const int32_t* set_pk0 = nullptr;
+  const uint8_t* pk = nullptr;  // staged keys (bytes or table indices), as for pk_decode
+  uint32_t stride = 0;
+  const uint32_t* pk_len = nullptr;
+  int32_t* pk_err = nullptr;
+  const uint32_t* tab = nullptr;
+  const uint8_t* tab_ok = nullptr;
+  uint32_t tab_n = 0;
+  uint32_t* pts = nullptr;  // point arena: level t at point offset 2 N0 - (N0 >> (t - 1)) (0 for t = 0)
+  uint8_t* inf = nullptr;   // infinity flags, same offsets
+  uint32_t* pre[2] = {nullptr, nullptr};   // per level (t & 1): prefix products, T n_c(t) items
+  uint32_t* cinv[2] = {nullptr, nullptr};  // per level and lane pair: 1 / (chunk product)
+  uint8_t* flag[2] = {nullptr, nullptr};   // per level and lane pair: chunk had an equal-x pair
+};
+hipError_t agg_leaf(hipStream_t st, const AggTreeArgs& a);
+hipError_t agg_step(hipStream_t st, const AggTreeArgs& a, int t);
+// per set: (0, level-L offset, count) or (1, first staged key, count) -> projective sum
+hipError_t agg_final(hipStream_t st, const AggTreeArgs& a, int n_sets, const int32_t* src, uint32_t* agg);
 hipError_t pk_scale(hipStream_t st, int n, const uint32_t* agg, const uint64_t* rnd, uint32_t* Pp, uint32_t* zP,
                     uint8_t* pinf);
 hipError_t pk_affine(hipStream_t st, int n, const uint32_t* Pp, const uint32_t* zinv, uint32_t* P);

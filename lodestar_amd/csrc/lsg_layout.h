@@ -12,6 +12,7 @@
 namespace lsgl {
 constexpr size_t W_FP = 14;          // u32 words per item: one Fp
 constexpr size_t W_G1A = 2 * W_FP;   // affine G1 (x, y)
+constexpr size_t W_TAB = 32;         // a pubkey-table row: affine G1 padded to one 128-byte line
 constexpr size_t W_G1P = 3 * W_FP;   // projective G1 (X : Y : Z)
 constexpr size_t W_G2A = 4 * W_FP;   // affine G2 over Fp2
 constexpr size_t W_G2P = 6 * W_FP;   // projective G2

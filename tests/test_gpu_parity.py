@@ -461,13 +461,26 @@ def test_batch_partial_bit_exact_vs_oracle(ab_ctx, monkeypatch):
 
 # ---- validator pubkey table resident in HBM, sets naming keys by index
 # (index2pubkey, state-transition/src/cache/pubkeyCache.ts:60-75, epochContext.ts:701-704)
-@pytest.fixture(scope="module")
-def table_ctx():
+def _table_context(lib=None):
     from lodestar_amd._native import Context
-    c = Context(0)
+    c = Context(0, lib=lib)
     # indices 0..23 uncompressed, 24..39 compressed (two loads, the second one past the end)
     assert c.pubkey_table_set(0, [bd.pk_bytes(i) for i in range(24)]) == [0] * 24
     assert c.pubkey_table_set(24, [bd.pk_bytes(i, compressed=True) for i in range(24, 40)]) == [0] * 16
+    return c
+
+
+@pytest.fixture(scope="module")
+def table_ctx():
+    c = _table_context()
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def table_ab_ctx():
+    from lodestar_amd._native import AB_LIB_PATH
+    c = _table_context(AB_LIB_PATH)
     yield c
     c.close()
 
@@ -484,15 +497,20 @@ def test_pubkey_table_aggregation_by_index(table_ctx):
     assert c.aggregate_pubkeys(PkIndices([]))[1] == 101  # EMPTY_AGGREGATE_ARRAY
 
 
-def test_aggregation_tree_edge_cases(table_ctx):
-    """The batch-affine aggregation tree (lsg_k_pk.hip k_agg_*, packages of >= 32768 keys)
-    against the oracle's PublicKey.aggregate, bit-exact, on the cases its affine additions must
-    route around: P + P (doubling), P + (-P) (infinity), infinity keys in the table, lone last
-    points, segments that skip the levels (<= 8 keys), a key list of period 40 whose higher
-    levels are full of equal pairs, bad indices and empty sets."""
+@pytest.mark.parametrize("form", ["fold", "tree"])
+def test_aggregation_tree_edge_cases(table_ctx, table_ab_ctx, monkeypatch, form):
+    """PublicKey.aggregate of large packages (>= 32768 keys) against the oracle, bit-exact, in
+    both forms: the shipped fused gather + mixed-addition fold (lsg_k_pk.hip k_pk_agg_seg) and
+    the batch-affine tree (k_agg_*, A/B build with LSG_AGG_TREE=1), on the cases the tree's
+    affine additions must route around: P + P (doubling), P + (-P) (infinity), infinity keys in
+    the table, lone last points, sets summed directly (few keys), a key list of period 40 whose
+    higher levels are full of equal pairs, bad indices and empty sets."""
     from lodestar_amd._native import PkIndices, LSG_ERR_BAD_INDEX
     from oracle.curves import E1, G1_GEN
     c = table_ctx
+    if form == "tree":
+        c = table_ab_ctx
+        monkeypatch.setenv("LSG_AGG_TREE", "1")
     # rows 40 = -pk(3), 41 = the infinity key (uncompressed encoding)
     neg3 = g1_serialize(E1.neg(bd.pk_point(3)))
     assert c.pubkey_table_set(40, [neg3, bytes([0x40]) + bytes(95)]) == [0, 0]
