@@ -341,7 +341,7 @@ def main():
                     default="jobs")
     ap.add_argument("--sets-per-step", type=int, default=32768, help="sets per package (jobs / adversarial)")
     ap.add_argument("--depth", type=int, default=None, help="packages in flight per GPU")
-    ap.add_argument("--blocks", type=int, default=64, help="block workload: blocks (128-set jobs) per package")
+    ap.add_argument("--blocks", type=int, default=128, help="block workload: blocks (128-set jobs) per package")
     ap.add_argument("--validators", type=int, default=N_VALIDATORS,
                     help="block workload: pubkey table rows (validator v holds key v mod 1024)")
     ap.add_argument("--packages", type=int, default=None, help="distinct packages cycled through")

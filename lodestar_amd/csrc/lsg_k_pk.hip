@@ -69,13 +69,19 @@ __global__ void LSG_KERNEL_ATTR k_pk_agg_seg(int n_chunks, int ips_log2, const i
   if (active) {
     const int off = chunks[3 * c], len = chunks[3 * c + 1];
     out = chunks[3 * c + 2];
+    // software-pipelined: the next key's row is in flight while this one is added (the
+    // gathers are scattered over the table; unhidden, their latency bounds the fold)
+    g1a_t a;
+    bool is_inf = true;
+    int e = 0;
+    if (j < len) e = pk_fetch_aff((size_t)(off + j), pk, stride, pk_len, tab, tab_ok, tab_n, a, is_inf);
 #pragma unroll 1
     for (int k = j; k < len; k += ips) {
-      g1a_t a;
-      bool is_inf;
-      const int e = pk_fetch_aff((size_t)(off + k), pk, stride, pk_len, tab, tab_ok, tab_n, a, is_inf);
+      const g1a_t cur = a;
+      const bool cur_inf = is_inf;
       if (lead) err[off + k] = e;
-      if (!is_inf) acc = proj_is_inf(acc) ? proj_from_aff(a) : g1_add_mixed(acc, a);
+      if (k + ips < len) e = pk_fetch_aff((size_t)(off + k + ips), pk, stride, pk_len, tab, tab_ok, tab_n, a, is_inf);
+      if (!cur_inf) acc = proj_is_inf(acc) ? proj_from_aff(cur) : g1_add_mixed(acc, cur);
     }
   }
   // every lane runs the butterfly: a chunk never straddles a wave (ips <= 32 pairs)
