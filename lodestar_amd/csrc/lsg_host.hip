@@ -2167,6 +2167,8 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
   std::vector<Grp> chk;       // chunks checked on their own (phase B)
   std::vector<std::pair<size_t, size_t>> chk_jobs;
   std::vector<std::pair<int32_t, int32_t>> chk_items;  // their resident phase-A items
+  std::vector<uint8_t> chk_threw;                      // the chunk threw (its retry is counted)
+  std::vector<uint8_t> job_err(nj, 0);                 // the job's result is its decode error
   bool any_err_chunk = false;
   std::vector<uint8_t> chunk_err(chunks.size(), 0);
   for (size_t c = 0; c < chunks.size(); c++) {
@@ -2214,18 +2216,49 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         chk.push_back(g);
         chk_jobs.push_back(chunks[c]);
         chk_items.push_back(c < s->chunk_items.size() ? s->chunk_items[c] : std::make_pair(-1, -1));
+        chk_threw.push_back(0);
       }
     } else {  // the chunk throws (worker.ts:79-85): every job is verified on its own
       retry_inc(chunks[c].first);
+      // A job's own verdict is its validity alone, so the chunk's jobs that do not throw are
+      // checked as ONE group first -- the throwing sets are the identity in the chunk's items
+      // and signature sums (the kernels' err rule) -- and localised only if it fails: a chunk
+      // with one undecodable signature costs one group check instead of 16 per-job checks.
+      // Verdicts and the batch counters are the reference's (the retry counted above, no
+      // batch success for a chunk that threw).
+      bool live = false;
       for (size_t q = chunks[c].first; q < chunks[c].second; q++) {
         const size_t j = s->batch_order[q];
         const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
-        if (e)
+        if (e) {
           s->results[j] = {LSG_ERROR, e};
-        else if (big_ok && !s->chunk_mode)  // its sets are in the passing package group
-          s->results[j] = {LSG_VALID, 0};
-        else
-          retry.push_back(j);
+          job_err[j] = 1;
+        } else {
+          live = true;
+        }
+      }
+      if (!live) continue;
+      if (big_ok && !s->chunk_mode) {  // its sets are in the passing package group
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++)
+          if (!job_err[s->batch_order[q]]) s->results[s->batch_order[q]] = {LSG_VALID, 0};
+      } else if (s->chunk_mode) {  // the chunk's own phase-A group (throwing sets as identity)
+        const bool ok = vA[(size_t)s->chunk_group[c]] != 0;
+        for (size_t q = chunks[c].first; q < chunks[c].second; q++) {
+          const size_t j = s->batch_order[q];
+          if (job_err[j]) continue;
+          if (ok)
+            s->results[j] = {LSG_VALID, 0};
+          else
+            retry.push_back(j);
+        }
+      } else {
+        Grp g;
+        g.first = first;
+        g.len = len;
+        chk.push_back(g);
+        chk_jobs.push_back(chunks[c]);
+        chk_items.push_back(c < s->chunk_items.size() ? s->chunk_items[c] : std::make_pair(-1, -1));
+        chk_threw.push_back(1);
       }
     }
   }
@@ -2237,14 +2270,16 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     LSG_RC(run_fallback_phase(s, lk, chk, reuse ? &chk_items : nullptr, v));
     for (size_t c = 0; c < chk.size(); c++) {
       if (v[c]) {
-        for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
-        succ_add(chk_jobs[c].first, chk[c].len);
+        for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++)
+          if (!job_err[s->batch_order[q]]) s->results[s->batch_order[q]] = {LSG_VALID, 0};
+        if (!chk_threw[c]) succ_add(chk_jobs[c].first, chk[c].len);
       } else {
-        retry_inc(chk_jobs[c].first);
+        if (!chk_threw[c]) retry_inc(chk_jobs[c].first);
         if (reuse) {
           fail_chunks.push_back(c);
         } else {
-          for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++) retry.push_back(s->batch_order[q]);
+          for (size_t q = chk_jobs[c].first; q < chk_jobs[c].second; q++)
+            if (!job_err[s->batch_order[q]]) retry.push_back(s->batch_order[q]);
         }
       }
     }
@@ -2285,12 +2320,14 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     }
     LSG_RC(run_fallback_phase(s, lk, g1, &g1_items, v));
     for (size_t g = 0; g < g1.size(); g++) {
-      const size_t nj = g1_jobs[g].second - g1_jobs[g].first;
+      size_t nlive = 0;  // (a thrown job keeps its error; its sets are the identity here)
+      for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) nlive += job_err[s->batch_order[q]] ? 0 : 1;
       for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) {
         const size_t j = s->batch_order[q];
+        if (job_err[j]) continue;
         if (v[g])
           s->results[j] = {LSG_VALID, 0};
-        else if (nj == 1)
+        else if (nlive == 1)
           s->results[j] = {LSG_INVALID, 0};
         else
           retry.push_back(j);
