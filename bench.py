@@ -364,7 +364,7 @@ def main():
     if args.workload == "node":
         return run_node_workload(args)
     if args.depth is None:
-        args.depth = {"jobs": 6, "adversarial": 6, "block": 4, "sync": 32, "gossip": 64, "single": 1,
+        args.depth = {"jobs": 6, "adversarial": 5, "block": 4, "sync": 32, "gossip": 64, "single": 1,
                       "committees": 6}[args.workload]
     if args.coalesce is None:
         args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
@@ -374,12 +374,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LSG_BENCH_REHEARSE=1: a multi-rank rehearsal on a one-GPU box -- every rank on device 0,
+    # the partials exchanged over gloo through host memory (RCCL refuses two ranks on one GPU).
+    # The rank protocol, data split, barriers and max-over-ranks timing are the real ones.
+    rehearse = os.environ.get("LSG_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            # the per-package all-gather of 576-byte partials must not queue behind the
+            # package kernels in flight: RCCL on a high-priority stream
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
 
     from lodestar_amd._native import Context, PreparedJobs
     n_dev = max(args.devices, 1)
@@ -420,7 +433,13 @@ def main():
         send = torch.empty(576, dtype=torch.uint8, device=f"cuda:{local}")
         recv = torch.empty(world * 576, dtype=torch.uint8, device=f"cuda:{local}")
         ctx.jobs_partial_device(t, send.data_ptr())
-        dist.all_gather_into_tensor(recv, send)
+        if rehearse:  # gloo: through host memory
+            torch.cuda.synchronize()
+            parts = [torch.empty(576, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, send.cpu())
+            recv.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(recv, send)
         torch.cuda.current_stream().synchronize()  # the gathered bytes are complete
         ft = ctx.final_submit_device(recv.data_ptr(), world)
         if ft is None:
@@ -532,7 +551,7 @@ def main():
     allocs = ctx.allocation_count() - allocs0
     if dist is not None:
         import torch
-        te = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        te = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
     # unloaded latency: one package at a time, each alone on the GPU

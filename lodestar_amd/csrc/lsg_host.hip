@@ -2320,14 +2320,21 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     }
     LSG_RC(run_fallback_phase(s, lk, g1, &g1_items, v));
     for (size_t g = 0; g < g1.size(); g++) {
-      size_t nlive = 0;  // (a thrown job keeps its error; its sets are the identity here)
-      for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) nlive += job_err[s->batch_order[q]] ? 0 : 1;
+      // A thrown job keeps its error.  Only its throwing sets are the identity in the group:
+      // its other sets take part, so a failing group with one live job localises that job on
+      // its own (C2) unless every other job of the group is live too.
+      size_t nlive = 0;
+      bool thrown = false;
+      for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) {
+        nlive += job_err[s->batch_order[q]] ? 0 : 1;
+        thrown = thrown || job_err[s->batch_order[q]];
+      }
       for (size_t q = g1_jobs[g].first; q < g1_jobs[g].second; q++) {
         const size_t j = s->batch_order[q];
         if (job_err[j]) continue;
         if (v[g])
           s->results[j] = {LSG_VALID, 0};
-        else if (nlive == 1)
+        else if (nlive == 1 && !thrown)
           s->results[j] = {LSG_INVALID, 0};
         else
           retry.push_back(j);
@@ -2833,7 +2840,13 @@ int dev_create(lsg_ctx* c, int ord, int device, Dev** out) {
   // pipeline slots are created on first use (slot_ready): 64 x 2 streams per device up front
   // would cost init time nobody needs below a few packages in flight
   if (ord == 0) {
-    for (int i = 0; i < LSG_FE_STREAMS; i++) LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_fe[i], hipStreamNonBlocking));
+    // the node checks' final exponentiations (lsg_final_submit*) at the greatest stream
+    // priority: one small program that the node's next verdicts wait on must not queue behind
+    // the packages in flight
+    int least = 0, greatest = 0;
+    LSG_HIPC(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (int i = 0; i < LSG_FE_STREAMS; i++)
+      LSG_HIPC(c, hipStreamCreateWithPriority(&d->s_fe[i], hipStreamNonBlocking, greatest));
     for (int i = 0; i < LSG_FINALS; i++) LSG_RC(slot_create(d, &d->finals[i], i, d->s_fe[i % LSG_FE_STREAMS]));
   }
   return slot_create(d, &d->util, 0, d->s_util);
