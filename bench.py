@@ -290,7 +290,7 @@ def run_node_workload(args):
         raise SystemExit("--workload node runs one Node process per node (use --gpus 1)")
     # at least 150 timed steps (~2.5 s): over a 30-step window (~0.6 s) the JIT, the heap
     # growth and single collections moved the rate by +-25 % between runs
-    args.steps = max(args.steps, 150)
+    args.steps = max(args.steps or 0, 150)
     # 40 untimed steps: the first Node process on a fresh box ran its first ~10-20 packages
     # 20-30 % slower (1.35-1.53M against 1.86-1.97M for a second run in the same call)
     args.warmup = max(args.warmup, 40)
@@ -335,7 +335,9 @@ def run_node_workload(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30, help="timed packages per GPU")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed packages per GPU (default 30; 10 x depth for the deep small-package workloads, "
+                         "so that the timed region is the steady state, not one burst of the pipeline)")
     ap.add_argument("--warmup", type=int, default=5, help="untimed packages per GPU (at least --depth are run)")
     ap.add_argument("--workload", choices=["jobs", "block", "sync", "gossip", "adversarial", "node", "single", "committees"],
                     default="jobs")
@@ -366,6 +368,8 @@ def main():
     if args.depth is None:
         args.depth = {"jobs": 6, "adversarial": 5, "block": 4, "sync": 32, "gossip": 64, "single": 1,
                       "committees": 6}[args.workload]
+    if args.steps is None:
+        args.steps = 10 * args.depth if args.workload in ("gossip", "sync") else 30
     if args.coalesce is None:
         args.coalesce = 4096 if args.workload in ("gossip", "sync") else 0
     if args.packages is None:  # distinct packages cycled (the aggregate workloads are costly to build)
@@ -381,7 +385,7 @@ def main():
     if rehearse:
         local = 0
     dist = None
-    if world > 1:
+    if world > 1 or rehearse:  # (a one-rank rehearsal runs the node protocol too)
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -395,6 +399,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
 
     from lodestar_amd._native import Context, PreparedJobs
+    NODE_LAG = 2  # multi-rank: node verdicts awaited this many exchanges late (run())
     n_dev = max(args.devices, 1)
     if args.devices:
         if world > 1:
@@ -409,7 +414,8 @@ def main():
     max_pks = int(n_sets * wl.pks_per_set) + 1
     # coalesced launches hold up to `depth` packages: slots sized for that
     co = args.depth if args.coalesce and n_sets <= args.coalesce else 1
-    ctx.reserve(n_sets * co, max_pks * co, 32 * n_sets * co, n_slots=args.depth + 1)
+    # (multi-rank: NODE_LAG more packages wait for their node verdicts with their GPU work done)
+    ctx.reserve(n_sets * co, max_pks * co, 32 * n_sets * co, n_slots=args.depth + 1 + (NODE_LAG if world > 1 or rehearse else 0))
     if args.coalesce:
         ctx.set_coalesce(args.coalesce, args.coalesce_inflight)
 
@@ -432,21 +438,26 @@ def main():
         import torch
         send = torch.empty(576, dtype=torch.uint8, device=f"cuda:{local}")
         recv = torch.empty(world * 576, dtype=torch.uint8, device=f"cuda:{local}")
+        c0 = time.perf_counter()
         ctx.jobs_partial_device(t, send.data_ptr())
-        if rehearse:  # gloo: through host memory
-            torch.cuda.synchronize()
+        c1 = time.perf_counter()
+        if rehearse:  # gloo: through host memory (the export above is complete; no device sync)
             parts = [torch.empty(576, dtype=torch.uint8) for _ in range(world)]
             dist.all_gather(parts, send.cpu())
             recv.copy_(torch.cat(parts))
         else:
             dist.all_gather_into_tensor(recv, send)
         torch.cuda.current_stream().synchronize()  # the gathered bytes are complete
+        node_ms["partial"] += (c1 - c0) * 1e3
+        node_ms["gather"] += (time.perf_counter() - c1) * 1e3
+        node_ms["n"] += 1
         ft = ctx.final_submit_device(recv.data_ptr(), world)
         if ft is None:
             raise SystemExit("final-exponentiation entries exhausted")
         return ft
 
     stats_acc = collections.Counter()
+    node_ms = collections.Counter()  # host time per node check: partial ready, all-gather, node FE + wait
     submit_wall = []  # wall time of each lsg_submit_jobs call (lock wait + staging + enqueue)
 
     def run(n_pkgs, depth, capture=False, seq0=0):
@@ -454,6 +465,8 @@ def main():
         (capture) per-package HIP-event kernel times"""
         if dist is None and args.waits == "thread":
             return run_threaded(n_pkgs, depth, capture)
+        if dist is not None:
+            return run_node(n_pkgs, depth, capture)
         lat, times = [], []
         pend = collections.deque()
         done = 0
@@ -470,15 +483,8 @@ def main():
             pend.append((t, k, time.perf_counter()))
             seq += 1
 
-        while len(pend) < min(depth, n_pkgs):
-            submit()
-        while pend:
-            t, k, t_sub = pend.popleft()
-            if dist is not None:  # node check of SURVEY.md 8e
-                node_ok = ctx.final_wait(gather_node(t))
-                res, st = ctx.wait_jobs_node(t, 1 if node_ok else 0, raw=True)
-            else:
-                res, st = ctx.wait_jobs(t, raw=True)
+        def finish(t, k, t_sub, res, st):
+            nonlocal done
             lat.append(time.perf_counter() - t_sub)
             if not verdict_ok(k, res, t[1]):
                 raise SystemExit(f"rank {rank}: package {k} verdicts differ from the expected ones")
@@ -487,8 +493,111 @@ def main():
             if capture:
                 times.append(ctx.last_kernel_times())
             done += 1
-            if done + len(pend) < n_pkgs:
+
+        # node checks are pipelined: package k's partial is exchanged and its node
+        # final exponentiation launched, then package k+1's, ...; a node verdict is awaited
+        # NODE_LAG exchanges later, so the host never idles on one final exponentiation while
+        # the GPU runs the packages behind it.  Every rank exchanges in submission order.
+        fins = collections.deque()
+
+        def resolve_node():
+            t, k, t_sub, ft = fins.popleft()
+            c2 = time.perf_counter()
+            node_ok = ctx.final_wait(ft)
+            c3 = time.perf_counter()
+            res, st = ctx.wait_jobs_node(t, 1 if node_ok else 0, raw=True)
+            node_ms["final"] += (c3 - c2) * 1e3
+            node_ms["resolve"] += (time.perf_counter() - c3) * 1e3
+            finish(t, k, t_sub, res, st)
+
+        while len(pend) < min(depth, n_pkgs):
+            submit()
+        while pend or fins:
+            if pend:
+                t, k, t_sub = pend.popleft()
+                if dist is not None:
+                    fins.append((t, k, t_sub, gather_node(t)))
+                    if len(fins) > NODE_LAG or not pend:
+                        resolve_node()
+                else:
+                    res, st = ctx.wait_jobs(t, raw=True)
+                    finish(t, k, t_sub, res, st)
+            else:
+                resolve_node()
+            while seq - seq0 < n_pkgs and len(pend) < depth and len(pend) + len(fins) < depth + NODE_LAG:
                 submit()
+        return lat, times
+
+    def run_node(n_pkgs, depth, capture):
+        """Multi-rank: the main thread submits, an exchange thread takes the
+        packages in submission order (every rank alike: the collectives' order) through partial
+        -> RCCL all-gather -> node final exponentiation, and a resolver thread waits each node
+        verdict and resolves the package -- host work overlaps the GPU as in the one-GPU
+        threaded path.  depth packages execute; NODE_LAG more may wait for their verdicts."""
+        import queue
+        import threading
+        import torch
+        lat, times = [], []
+        room = threading.Semaphore(depth + NODE_LAG)
+        exq, rq = queue.Queue(), queue.Queue()
+        failed = []
+
+        def guard(fn):
+            def body():
+                try:
+                    torch.cuda.set_device(local)
+                    fn()
+                except BaseException as e:  # surface in the main thread, never hang it
+                    failed.append(e)
+                    for _ in range(n_pkgs + depth + NODE_LAG):
+                        room.release()
+                        rq.put(None)
+            return body
+
+        def exchanger():
+            for _ in range(n_pkgs):
+                t, k, t_sub = exq.get()
+                rq.put((t, k, t_sub, gather_node(t)))
+
+        def resolver():
+            for _ in range(n_pkgs):
+                item = rq.get()
+                if item is None:
+                    return
+                t, k, t_sub, ft = item
+                c2 = time.perf_counter()
+                node_ok = ctx.final_wait(ft)
+                c3 = time.perf_counter()
+                res, st = ctx.wait_jobs_node(t, 1 if node_ok else 0, raw=True)
+                node_ms["final"] += (c3 - c2) * 1e3
+                node_ms["resolve"] += (time.perf_counter() - c3) * 1e3
+                lat.append(time.perf_counter() - t_sub)
+                if not verdict_ok(k, res, t[1]):
+                    raise SystemExit(f"rank {rank}: package {k} verdicts differ from the expected ones")
+                stats_acc.update({"batch_retries": st["batch_retries"], "n_final_exps": st["n_final_exps"],
+                                  "submit_us": st["submit_us"], "packages": 1})
+                if capture:
+                    times.append(ctx.last_kernel_times())
+                room.release()
+
+        threads = [threading.Thread(target=guard(f), daemon=True) for f in (exchanger, resolver)]
+        for th in threads:
+            th.start()
+        for seq in range(n_pkgs):
+            room.acquire()
+            if failed:
+                break
+            k = seq % len(prepared)
+            t0 = time.perf_counter()
+            t = ctx.submit_jobs(prepared[k])
+            submit_wall.append(time.perf_counter() - t0)
+            if t is None:
+                raise SystemExit("pipeline slots exhausted: lower --depth")
+            exq.put((t, k, time.perf_counter()))
+        for th in threads:
+            th.join()
+        if failed:
+            raise failed[0]
         return lat, times
 
     def run_threaded(n_pkgs, depth, capture):
@@ -659,6 +768,8 @@ def main():
             "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),
             "submit_call_ms_p50_max": [round(1e3 * statistics.median(submit_wall_timed), 3),
                                        round(1e3 * submit_wall_timed[-1], 3)],
+            "node_check_host_ms_per_package": ({k: round(v / node_ms["n"], 3) for k, v in node_ms.items() if k != "n"}
+                                               if node_ms["n"] else None),
             "roofline": roof,
             "whole_path_mad_frac": round(node_mads / (peak_mad * world * n_dev), 4),
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},

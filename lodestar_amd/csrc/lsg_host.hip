@@ -407,6 +407,7 @@ struct Dev {
   int ord = 0;  // position in the context's device list
   hipStream_t s_util = nullptr;
   hipStream_t s_fe[LSG_FE_STREAMS] = {};
+  hipStream_t s_xp = nullptr;  // partial exports (lsg_jobs_partial_device), high priority
   Slot slots[LSG_SLOTS];
   Slot finals[LSG_FINALS];
   Slot util;
@@ -2847,6 +2848,7 @@ int dev_create(lsg_ctx* c, int ord, int device, Dev** out) {
     LSG_HIPC(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
     for (int i = 0; i < LSG_FE_STREAMS; i++)
       LSG_HIPC(c, hipStreamCreateWithPriority(&d->s_fe[i], hipStreamNonBlocking, greatest));
+    LSG_HIPC(c, hipStreamCreateWithPriority(&d->s_xp, hipStreamNonBlocking, greatest));
     for (int i = 0; i < LSG_FINALS; i++) LSG_RC(slot_create(d, &d->finals[i], i, d->s_fe[i % LSG_FE_STREAMS]));
   }
   return slot_create(d, &d->util, 0, d->s_util);
@@ -2863,6 +2865,7 @@ void dev_destroy(Dev* d) {
   if (d->s_util) (void)hipStreamDestroy(d->s_util);
   for (hipStream_t st : d->s_fe)
     if (st) (void)hipStreamDestroy(st);
+  if (d->s_xp) (void)hipStreamDestroy(d->s_xp);
   delete d;
 }
 
@@ -3132,14 +3135,22 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
   if (p < 0) return LSG_ERR_INVALID_ARG;
   Slot* s = &c->dev[0]->slots[p];
   const bool has = !s->phA.groups.empty() && s->big_g >= 0;
+  // the copy goes out on a high-priority stream (the node final exponentiations'): on the
+  // package's own stream it would queue behind other packages' kernels sharing its hardware
+  // queue, and the node's next verdicts wait on it (ev_part is complete: presync_pkg)
+  hipStream_t xs = c->dev[0]->s_xp;
   if (has) {
     const uint8_t* src;
     LSG_RC(export_partial_dev(s, &src));
-    LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, s->st[0]));
+    if (s->lone_unscaled) {  // f^r was launched on the package's stream
+      LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[0]));
+      LSG_HIP(s, hipStreamWaitEvent(xs, s->ev_grp, 0));
+    }
+    LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, xs));
   } else {
-    LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, s->st[0]));
+    LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, xs));
   }
-  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(xs));
   if (has_batch) *has_batch = has ? 1 : 0;
   return LSG_OK;
 }
