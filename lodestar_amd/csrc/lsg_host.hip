@@ -373,6 +373,7 @@ struct Slot {
   std::vector<std::pair<int32_t, int32_t>> chunk_items;  // package mode: per chunk, its phase-A items
   bool chunk_mode = false;          // phase A ran one group per 16-job chunk (LSG_PACKAGE_GROUP=0)
   std::vector<int> chunk_group;     // chunk mode: per chunk of batch_order, its phase-A group
+  std::vector<int> sub_big;         // a coalesced launch: per sub-package, its package group (-1: none)
   std::vector<int> job_group;       // per job: its phase-A group (non-batchable), else -1
   std::vector<lsg_job_result> results;
   lsg_stats stats;
@@ -720,6 +721,9 @@ int msm_window_bits(size_t n) { return n >= 256 ? 8 : (n >= 48 ? 4 : 2); }
 // Phase A as the reference batches it: one RLC group per 16-job chunk instead of one package
 // group (env LSG_PACKAGE_GROUP=0; A/B and the equivalence test of the two modes)
 bool package_group_mode() { return lsg_ab_long("LSG_PACKAGE_GROUP", 1) != 0; }
+// A coalesced launch with one package group per sub-package (A/B build: LSG_SUB_GROUPS=0 gives
+// round 3's one group per 16-job chunk)
+bool sub_groups_on() { return lsg_ab_long("LSG_SUB_GROUPS", 1) != 0; }
 
 void binv_sizes(size_t n, size_t* lv, size_t* iv);
 size_t binv_lv_words(size_t n) {
@@ -1739,6 +1743,15 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     // (non-batchable jobs below: their groups never enter the package partial)
   } else if (package_group_mode() && !subs) {
     if (s->nb_sets == 1) noscale[0] = s->lone_unscaled = true;
+  } else if (package_group_mode() && sub_groups_on()) {  // a coalesced launch: one package group per sub-package
+    for (int k = 0; k < s->n_sub; k++) {
+      size_t len = 0, first = 0;
+      for (size_t q = s->bpos_first[(size_t)k]; q < s->bpos_first[(size_t)k + 1]; q++) {
+        if (!len) first = s->jobs[s->batch_order[q]].first;
+        len += s->jobs[s->batch_order[q]].count;
+      }
+      if (len == 1) noscale[first] = 1;
+    }
   } else {
     const auto ch = slot_chunks(s);
     for (auto& c : ch) {
@@ -1765,8 +1778,11 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     (g.msm ? gm : gs).push_back(g);
     (g.msm ? om : os).push_back(owner);
   };
-  s->chunk_mode = !package_group_mode() || subs;  // a coalesced launch checks every chunk on its own
+  // one RLC group per package; a coalesced launch: one per sub-package (each keeps its own
+  // verdicts, chunks and fallback: pkg_resolve)
+  s->chunk_mode = !package_group_mode() || (subs && !sub_groups_on());
   s->chunk_group.clear();
+  s->sub_big.assign((size_t)s->n_sub, -1);
   std::vector<std::pair<size_t, size_t>> chunks;
   if (s->chunk_mode) {
     chunks = slot_chunks(s);
@@ -1776,6 +1792,15 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
       if (len) add(s->jobs[s->batch_order[chunks[c].first]].first, len, -3 - (int)c);
     }
     s->chunk_group.assign(chunks.size(), -1);
+  } else if (s->n_sub) {
+    for (int k = 0; k < s->n_sub; k++) {
+      size_t len = 0, first = 0;
+      for (size_t q = s->bpos_first[(size_t)k]; q < s->bpos_first[(size_t)k + 1]; q++) {
+        if (!len) first = s->jobs[s->batch_order[q]].first;
+        len += s->jobs[s->batch_order[q]].count;
+      }
+      if (len) add(first, len, -1000 - k);
+    }
   } else if (s->nb_sets) {
     add(0, s->nb_sets, -2);
   }
@@ -1795,8 +1820,10 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     chunks = slot_chunks(s);
     A.sub.assign(om.size(), {});
     for (size_t g = 0; g < om.size(); g++) {
-      if (om[g] != -2) continue;
+      if (om[g] != -2 && om[g] > -1000) continue;
+      const int sub = om[g] <= -1000 ? -1000 - om[g] : -1;
       for (size_t c = 0; c < chunks.size(); c++) {
+        if (sub >= 0 && sub_of_pos(s, chunks[c].first) != sub) continue;
         const size_t first = s->jobs[s->batch_order[chunks[c].first]].first;
         size_t len = 0;
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) len += s->jobs[s->batch_order[q]].count;
@@ -1810,6 +1837,8 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   for (size_t g = 0; g < om.size(); g++) {
     if (om[g] == -2)
       s->big_g = (int)g;
+    else if (om[g] <= -1000)
+      s->sub_big[(size_t)(-1000 - om[g])] = (int)g;
     else if (om[g] <= -3)
       s->chunk_group[(size_t)(-3 - om[g])] = (int)g;
     else
@@ -1851,8 +1880,9 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     size_t r = 0;
     for (size_t g = 0; g < om.size(); g++) {
       const size_t ns = g < A.sub.size() && !A.sub[g].empty() ? A.sub[g].size() : 1;
-      if (om[g] == -2)
+      if (om[g] == -2 || om[g] <= -1000)
         for (size_t k = 0; k < ns; k++) s->chunk_items[chunk_sub[k]] = A.sub_items[r + k];
+      if (om[g] == -2 || om[g] <= -1000) chunk_sub.erase(chunk_sub.begin(), chunk_sub.begin() + (long)ns);
       r += ns;
     }
   }
@@ -2162,8 +2192,12 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
   // whose all-gather missed a rank) localises like a failing one instead of
   // accepting the package.
   (void)node_valid;
-  const bool big_ok = s->big_g < 0 || vA[(size_t)s->big_g] != 0;
   auto chunks = slot_chunks(s);
+  // the package group covering chunk c passed (a coalesced launch: its sub-package's group)
+  auto pkg_ok = [&](size_t c) {
+    const int g = s->n_sub ? s->sub_big[(size_t)sub_of_pos(s, chunks[c].first)] : s->big_g;
+    return g < 0 || vA[(size_t)g] != 0;
+  };
   std::vector<size_t> retry;  // jobs verified individually (phase C)
   std::vector<Grp> chk;       // chunks checked on their own (phase B)
   std::vector<std::pair<size_t, size_t>> chk_jobs;
@@ -2203,10 +2237,10 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
       }
     } else if (!chunk_err[c]) {
-      if (big_ok) {
+      if (pkg_ok(c)) {
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
         succ_add(chunks[c].first, len);
-      } else if (chunks.size() == 1 && !any_err_chunk) {
+      } else if (chunks.size() == 1 && !any_err_chunk && !s->n_sub) {
         // the package group is exactly this chunk: its verdict is the chunk's
         retry_inc(chunks[c].first);
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
@@ -2239,7 +2273,7 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         }
       }
       if (!live) continue;
-      if (big_ok && !s->chunk_mode) {  // its sets are in the passing package group
+      if (!s->chunk_mode && pkg_ok(c)) {  // its sets are in the passing package group
         for (size_t q = chunks[c].first; q < chunks[c].second; q++)
           if (!job_err[s->batch_order[q]]) s->results[s->batch_order[q]] = {LSG_VALID, 0};
       } else if (s->chunk_mode) {  // the chunk's own phase-A group (throwing sets as identity)
