@@ -33,7 +33,9 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <string>
 #include <vector>
@@ -408,7 +410,10 @@ struct Dev {
   int ord = 0;  // position in the context's device list
   hipStream_t s_util = nullptr;
   hipStream_t s_fe[LSG_FE_STREAMS] = {};
-  hipStream_t s_xp = nullptr;  // partial exports (lsg_jobs_partial_device), high priority
+  // the node protocol's streams at the greatest priority, created on first use (idle
+  // high-priority streams cost the packages hardware-queue concurrency: firehose 2.87M ->
+  // ~2.4M sets/s with nine of them created up front): partial exports, node final exps
+  hipStream_t s_xp = nullptr, s_nfe = nullptr;
   Slot slots[LSG_SLOTS];
   Slot finals[LSG_FINALS];
   Slot util;
@@ -557,6 +562,31 @@ void keep_times(Slot* s) {
     float t = 0;
     if (hipEventElapsedTime(&t, s->timers[i].a, s->timers[i].b) != hipSuccess) t = -1;
     v.push_back({s->timers[i].name, t});
+  }
+}
+
+// a greatest-priority stream of the device, created on first use
+int prio_stream(lsg_ctx* c, Dev* d, hipStream_t* st) {
+  if (!*st) {
+    int least = 0, greatest = 0;
+    LSG_HIPC(c, hipSetDevice(d->device));
+    LSG_HIPC(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    LSG_HIPC(c, hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest));
+  }
+  return LSG_OK;
+}
+
+// Host wait for a completion event without holding a core: hipEventSynchronize spins on this
+// stack (with hipEventBlockingSync too: the gossip bench's 64 waiter threads kept 16 cores
+// busy, tools/thread_cpu.py), so poll -- back to back for the first 20 us, then with 30 us
+// sleeps; the added latency is well under 0.1 ms per wait.
+hipError_t event_wait(hipEvent_t e) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(20))
+      std::this_thread::sleep_for(std::chrono::microseconds(30));
   }
 }
 
@@ -2076,7 +2106,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   LSG_RC(launch_readback(s, false));
   const int dev = s->d->device;
   if (lk) lk->unlock();
-  hipError_t e = hipEventSynchronize(s->ev_done);
+  hipError_t e = event_wait(s->ev_done);
   if (lk) {
     lk->lock();
     (void)hipSetDevice(dev);
@@ -2094,7 +2124,7 @@ int run_big_fe(Slot* s, CtxLock* lk) {
   LSG_HIP(s, hipEventRecord(s->ev_done, s->st[0]));
   const int dev = s->d->device;
   if (lk) lk->unlock();
-  hipError_t e = hipEventSynchronize(s->ev_done);
+  hipError_t e = event_wait(s->ev_done);
   if (lk) {
     lk->lock();
     (void)hipSetDevice(dev);
@@ -2540,7 +2570,7 @@ int wait_pkg(lsg_ctx* c, CtxLock* lk, int p, int node_valid, lsg_job_result* res
   for (int d = 0; d < n && !rc; d++) {
     Slot* s = &c->dev[d]->slots[p];
     (void)hipSetDevice(c->dev[d]->device);
-    if (hipEventSynchronize(s->ev_done) != hipSuccess) rc = fail(s, "hipEventSynchronize", hipGetLastError());
+    if (event_wait(s->ev_done) != hipSuccess) rc = fail(s, "hipEventSynchronize", hipGetLastError());
   }
   Slot* s0 = &c->dev[0]->slots[p];
   // the ticket's own node check (lsg_init_devices) decides the package groups: 2 = passed
@@ -2730,7 +2760,7 @@ int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* st
     k = it->second.sub;
     ev = c->dev[0]->slots[p].ev_done;
   }
-  if (hipEventSynchronize(ev) != hipSuccess) return fail_c(c, "hipEventSynchronize", hipGetLastError());
+  if (event_wait(ev) != hipSuccess) return fail_c(c, "hipEventSynchronize", hipGetLastError());
   CtxLock lk(c->mu);
   LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
   Slot* s = &c->dev[0]->slots[p];
@@ -2785,7 +2815,7 @@ int presync_pkg(lsg_ctx* c, lsg_ticket t, bool partial_only) {
   }
   for (auto& e : evs) {
     (void)hipSetDevice(e.first);
-    hipError_t r = hipEventSynchronize(e.second);
+    hipError_t r = event_wait(e.second);
     if (r != hipSuccess) return fail_c(c, "hipEventSynchronize", r);
   }
   return LSG_OK;
@@ -2875,14 +2905,7 @@ int dev_create(lsg_ctx* c, int ord, int device, Dev** out) {
   // pipeline slots are created on first use (slot_ready): 64 x 2 streams per device up front
   // would cost init time nobody needs below a few packages in flight
   if (ord == 0) {
-    // the node checks' final exponentiations (lsg_final_submit*) at the greatest stream
-    // priority: one small program that the node's next verdicts wait on must not queue behind
-    // the packages in flight
-    int least = 0, greatest = 0;
-    LSG_HIPC(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (int i = 0; i < LSG_FE_STREAMS; i++)
-      LSG_HIPC(c, hipStreamCreateWithPriority(&d->s_fe[i], hipStreamNonBlocking, greatest));
-    LSG_HIPC(c, hipStreamCreateWithPriority(&d->s_xp, hipStreamNonBlocking, greatest));
+    for (int i = 0; i < LSG_FE_STREAMS; i++) LSG_HIPC(c, hipStreamCreateWithFlags(&d->s_fe[i], hipStreamNonBlocking));
     for (int i = 0; i < LSG_FINALS; i++) LSG_RC(slot_create(d, &d->finals[i], i, d->s_fe[i % LSG_FE_STREAMS]));
   }
   return slot_create(d, &d->util, 0, d->s_util);
@@ -2900,6 +2923,7 @@ void dev_destroy(Dev* d) {
   for (hipStream_t st : d->s_fe)
     if (st) (void)hipStreamDestroy(st);
   if (d->s_xp) (void)hipStreamDestroy(d->s_xp);
+  if (d->s_nfe) (void)hipStreamDestroy(d->s_nfe);
   delete d;
 }
 
@@ -3172,6 +3196,7 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
   // the copy goes out on a high-priority stream (the node final exponentiations'): on the
   // package's own stream it would queue behind other packages' kernels sharing its hardware
   // queue, and the node's next verdicts wait on it (ev_part is complete: presync_pkg)
+  LSG_RC(prio_stream(c, c->dev[0], &c->dev[0]->s_xp));
   hipStream_t xs = c->dev[0]->s_xp;
   if (has) {
     const uint8_t* src;
@@ -3310,6 +3335,9 @@ int lsg_final_submit_groups(lsg_ctx* c, const uint8_t* partials576, size_t n_gro
     c->err = "all final-exponentiation entries are busy";
     return LSG_ERR_BUSY;
   }
+  // a node verdict waits on this one program: the greatest stream priority (the entry is free)
+  LSG_RC(prio_stream(c, c->dev[0], &c->dev[0]->s_nfe));
+  s->st[0] = s->st[1] = c->dev[0]->s_nfe;
   int rc = submit_final(s, partials576, n_groups, per_group);
   if (rc) {
     sync_slot(s);
@@ -3332,6 +3360,8 @@ int lsg_final_submit_device(lsg_ctx* c, const void* dev_partials576, size_t n_pa
     c->err = "all final-exponentiation entries are busy";
     return LSG_ERR_BUSY;
   }
+  LSG_RC(prio_stream(c, c->dev[0], &c->dev[0]->s_nfe));
+  s->st[0] = s->st[1] = c->dev[0]->s_nfe;
   int rc = submit_final(s, (const uint8_t*)dev_partials576, n_partials ? 1 : 0, n_partials, true);
   if (rc) {
     sync_slot(s);
@@ -3359,7 +3389,7 @@ static int final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid, bool single
     ev = s->ev_done;
   }
   (void)hipSetDevice(c->dev[0]->device);
-  hipError_t e = hipEventSynchronize(ev);
+  hipError_t e = event_wait(ev);
   if (e != hipSuccess) return fail_c(c, "hipEventSynchronize", e);
   LSG_ENTER(c);
   Slot* s = ticket_final(c, ticket);
