@@ -414,6 +414,7 @@ struct Dev {
   // high-priority streams cost the packages hardware-queue concurrency: firehose 2.87M ->
   // ~2.4M sets/s with nine of them created up front): partial exports, node final exps
   hipStream_t s_xp = nullptr, s_nfe = nullptr;
+  hipStream_t s_pp[2] = {nullptr, nullptr};  // priority packages (slot_streams), on first use
   Slot slots[LSG_SLOTS];
   Slot finals[LSG_FINALS];
   Slot util;
@@ -655,7 +656,7 @@ void slot_destroy(Slot* s) {
     }
     for (int k = 0; k < 2; k++) {
       if (s->st_norm[k]) (void)hipStreamDestroy(s->st_norm[k]);
-      if (s->st_prio[k]) (void)hipStreamDestroy(s->st_prio[k]);
+      // (st_prio: the device's shared pair, destroyed with the device)
       s->st_norm[k] = s->st_prio[k] = s->st[k] = nullptr;
     }
   }
@@ -666,11 +667,14 @@ void slot_destroy(Slot* s) {
 // earlier package is in flight on either pair)
 int slot_streams(Slot* s, bool prio) {
   if (!s->own_streams) return LSG_OK;
+  // priority packages share one pair of greatest-priority streams per device, created on
+  // first use: a pair per slot would leave idle high-priority streams behind that take
+  // hardware-queue concurrency from every later package
   if (prio && !s->st_prio[0]) {
-    int least = 0, greatest = 0;
-    LSG_HIP(s, hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (int k = 0; k < 2; k++)
-      LSG_HIP(s, hipStreamCreateWithPriority(&s->st_prio[k], hipStreamNonBlocking, greatest));
+    Dev* d = s->d;
+    for (int k = 0; k < 2; k++) LSG_RC(prio_stream(d->c, d, &d->s_pp[k]));
+    s->st_prio[0] = d->s_pp[0];
+    s->st_prio[1] = d->s_pp[1];
   }
   hipStream_t* p = prio ? s->st_prio : s->st_norm;
   s->st[0] = p[0];
@@ -2924,6 +2928,8 @@ void dev_destroy(Dev* d) {
     if (st) (void)hipStreamDestroy(st);
   if (d->s_xp) (void)hipStreamDestroy(d->s_xp);
   if (d->s_nfe) (void)hipStreamDestroy(d->s_nfe);
+  for (hipStream_t st : d->s_pp)
+    if (st) (void)hipStreamDestroy(st);
   delete d;
 }
 
