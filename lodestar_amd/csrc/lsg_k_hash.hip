@@ -16,21 +16,97 @@
 #define LSG_H2C_WAVES 2
 #endif
 
-// expand_message_xmd(msg_i, DST, 256): one thread per set (byte-serial SHA-256)
+// expand_message_xmd(msg_i, DST, 256) (RFC 9380 5.3.1; oracle/hash_to_curve.py), one thread
+// per message.  Each thread's SHA-256 block buffer lives in LDS, byte k of thread t at word
+// (k / 4) * 64 + t (consecutive threads, consecutive banks): a byte appended is one LDS byte
+// store, where a register array indexed by the byte count went to scratch (a read-modify-
+// write per byte).  The Z_pad block is compressed without being written; b_i's 32-byte prefix
+// is stored as words; the output goes to global memory as words.
+struct ShaLds {
+  uint32_t st[8];
+  uint32_t n, total;
+  uint8_t* blk;  // this thread's byte 0; byte k at blk[(k >> 2) * 256 + (k & 3)]
+};
+LSG_DEVI void shal_init(ShaLds& c) {
+  const uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+#pragma unroll
+  for (int i = 0; i < 8; i++) c.st[i] = iv[i];
+  c.n = 0;
+  c.total = 0;
+}
+LSG_DEVI void shal_flush(ShaLds& c) {
+  uint32_t w[16];
+  const uint32_t* wl = (const uint32_t*)c.blk;
+#pragma unroll
+  for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(wl[k * 64]);
+  sha256_compress(c.st, w);
+  c.n = 0;
+}
+LSG_DEVI void shal_byte(ShaLds& c, uint8_t v) {
+  c.blk[(c.n >> 2) * 256 + (c.n & 3)] = v;
+  c.n++;
+  c.total++;
+  if (c.n == 64) shal_flush(c);
+}
+// a big-endian word at a word-aligned position (c.n % 4 == 0)
+LSG_DEVI void shal_word(ShaLds& c, uint32_t v) {
+  ((uint32_t*)c.blk)[(c.n >> 2) * 64] = __builtin_bswap32(v);
+  c.n += 4;
+  c.total += 4;
+  if (c.n == 64) shal_flush(c);
+}
+LSG_DEVI void shal_final(ShaLds& c, uint32_t* out8) {
+  const uint32_t bits = c.total * 8;  // (messages < 2^29 bytes)
+  shal_byte(c, 0x80);
+  while (c.n & 3) shal_byte(c, 0);
+  if (c.n > 56)
+    while (c.n) shal_word(c, 0);
+  while (c.n < 60) shal_word(c, 0);
+  shal_word(c, bits);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out8[i] = c.st[i];
+}
+
 __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restrict__ msg,
                                                     const uint32_t* __restrict__ msg_off,
                                                     const uint32_t* __restrict__ msg_len,
                                                     const uint8_t* __restrict__ dst, uint32_t dst_len,
                                                     uint8_t* __restrict__ ub) {
-  size_t i = gtid();
+  __shared__ uint32_t lds[16 * 64];
+  const size_t i = gtid();
   if (i >= (size_t)n) return;
-  uint8_t out[256];
-  expand_message_xmd_256(out, msg + msg_off[i], msg_len[i], dst, dst_len);
+  ShaLds c;
+  c.blk = (uint8_t*)(lds + threadIdx.x);
+  shal_init(c);
+  {  // Z_pad: one all-zero block
+    uint32_t z[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) z[k] = 0;
+    sha256_compress(c.st, z);
+    c.total = 64;
+  }
+  const uint8_t* m = msg + msg_off[i];
+  const uint32_t ml = msg_len[i];
+  for (uint32_t k = 0; k < ml; k++) shal_byte(c, m[k]);
+  shal_byte(c, 1);  // l_i_b_str = 256 (2 bytes, big endian)
+  shal_byte(c, 0);
+  shal_byte(c, 0);  // I2OSP(0, 1)
+  for (uint32_t k = 0; k < dst_len; k++) shal_byte(c, dst[k]);
+  shal_byte(c, (uint8_t)dst_len);
+  uint32_t b0[8], bi[8];
+  shal_final(c, b0);
   uint32_t* o = (uint32_t*)(ub + 256 * i);
-  for (int k = 0; k < 64; k++) {
-    uint32_t w;
-    __builtin_memcpy(&w, out + 4 * k, 4);
-    o[k] = w;
+  for (int r = 1; r <= 8; r++) {
+    shal_init(c);
+#pragma unroll
+    for (int k = 0; k < 8; k++) shal_word(c, r == 1 ? b0[k] : (b0[k] ^ bi[k]));
+    shal_byte(c, (uint8_t)r);
+    for (uint32_t k = 0; k < dst_len; k++) shal_byte(c, dst[k]);
+    shal_byte(c, (uint8_t)dst_len);
+    shal_final(c, bi);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[8 * (r - 1) + k] = __builtin_bswap32(bi[k]);
   }
 }
 

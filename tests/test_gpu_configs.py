@@ -203,6 +203,37 @@ def test_config_e_adversarial_4096(ctx, keys):
     check_against_oracle(ctx, jobs, per[:pos])
 
 
+def test_thrown_chunk_localises_its_live_jobs(ctx, keys):
+    """A chunk whose batch throws (an undecodable signature) is checked as one group of its
+    other jobs; a thrown job's remaining sets still take part, so a failing Miller-item group
+    whose only live job shares it with a thrown job must not convict that job (found by the
+    10^7 soak, pkg_resolve phase C1).  The package has more than 8192 distinct messages (so its
+    group keeps per-set Miller items) and more than 2048 sets (four-set items, k_miller_fused):
+    sets 0-3 = job [truncated, wrong message, valid] + job [valid] form one item.  Verdicts and
+    batch counters against the oracle's worker.ts rules (multithread/worker.ts:51-96); the
+    untouched sets are valid by construction (GPU-signed), the corrupted ones by the oracle."""
+    n = 8400
+    sets = single_sets(ctx, keys, b"thrown", n)
+    s = list(sets)
+    starts = (0, 64, 640, 5200)
+    for base in starts:
+        s[base] = bd.corrupt_truncate(s[base])
+        s[base + 1] = bd.corrupt_wrong_message(s[base + 1])
+    lone = (300, 301, 7800)
+    for i in lone:
+        s[i] = bd.corrupt_wrong_message(s[i])
+    per = [1] * n
+    touched = sorted(set(lone) | {b + k for b in starts for k in (0, 1)})
+    for i, v in zip(touched, oracle_each([s[i] for i in touched])):
+        per[i] = v
+    jobs, pos = [], 0
+    while pos < n:
+        k = 3 if pos in starts else 1
+        jobs.append((s[pos:pos + k], 1))
+        pos += k
+    check_against_oracle(ctx, jobs, per)
+
+
 def test_package_group_matches_chunk_mode(ab_ctx, keys, monkeypatch):
     """The one-group phase A (default) and the reference's chunk-16 phase A
     (LSG_PACKAGE_GROUP=0, A/B build) give identical per-job verdicts AND batch_retries /
