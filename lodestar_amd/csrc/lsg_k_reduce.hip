@@ -75,25 +75,24 @@ __global__ void LSG_KERNEL_ATTR_W(OP == 2 ? 1 : LSG_WAVES_PER_EU)
 // ---- batched field inversion (Montgomery's trick, chunked): every field inversion of a
 // stage -- 1/Z of the scaled pubkeys, 1/N(tv1) of the SSWU maps, 1/N(Z) of the hashed points
 // -- shares one exponentiation per batch instead of one per set.  A level folds chunks of
-// LSG_BINV_T values per lane pair (prefix products, one chunk product each); the chunk
-// products are the next level's values, up to one value, whose inverse unfolds back down (two
-// products per value).  log_T(n) launches each way instead of log_2(n).  Chunk c holds the
-// values c, c + n_c, c + 2 n_c, ... (n_c chunks): at every step adjacent lane pairs touch
-// adjacent values, so a wave's loads and stores are contiguous instead of T values apart.
-// Zero inputs (points at infinity, the SSWU exceptional case) are carried as 1 and come out as
-// 0, the value fp_inv(0) gives.
+// LSG_BINV_T consecutive values per lane pair (prefix products, one chunk product each); the
+// chunk products are the next level's values, up to one value, whose inverse unfolds back
+// down (two products per value).  log_T(n) launches each way instead of log_2(n).  Zero
+// inputs (points at infinity, the SSWU exceptional case) are carried as 1 and come out as 0,
+// the value fp_inv(0) gives.
 __global__ void LSG_KERNEL_ATTR k_binv_fold(int n, int zero_to_one, const uint32_t* __restrict__ in,
                                             uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
   const int n_chunks = (n + LSG_BINV_T - 1) / LSG_BINV_T;
   LANE_ITEM(n_chunks);
   (void)lead;
   const fp_t one = fp_one();
+  const int first = (int)item * LSG_BINV_T, last = min(n, first + LSG_BINV_T);
   fp_t acc = one;
 #pragma unroll 1
-  for (int k = (int)item, j = 0; k < n; k += n_chunks, j++) {
+  for (int k = first; k < last; k++) {
     fp_t x = lane_load<fp_t>(in, k);
     if (zero_to_one) x = fp_select(fp_is_zero(x), one, x);
-    acc = j == 0 ? x : fp_mul(acc, x);
+    acc = k == first ? x : fp_mul(acc, x);
     lane_store(pre, k, acc);
   }
   lane_store(tot, item, acc);
@@ -113,17 +112,16 @@ __global__ void LSG_KERNEL_ATTR k_binv_unfold(int n, int zero_to_one, const uint
   const int n_chunks = (n + LSG_BINV_T - 1) / LSG_BINV_T;
   LANE_ITEM(n_chunks);
   (void)lead;
-  fp_t acc = lane_load<fp_t>(tinv, item);  // 1 / (product of the chunk's values)
-  int k = (int)item;  // the chunk's last value
-  while (k + n_chunks < n) k += n_chunks;
+  const fp_t one = fp_one();
+  const int first = (int)item * LSG_BINV_T, last = min(n, first + LSG_BINV_T);
+  fp_t acc = lane_load<fp_t>(tinv, item);  // 1 / (in[first] * ... * in[last-1])
 #pragma unroll 1
-  for (; k >= (int)item; k -= n_chunks) {
+  for (int k = last - 1; k >= first; k--) {
     fp_t x = lane_load<fp_t>(in, k);
     const bool z = zero_to_one && fp_is_zero(x);
-    const bool first = k == (int)item;
-    fp_t r = first ? acc : fp_mul(acc, lane_load<fp_t>(pre, k - n_chunks));
+    fp_t r = k > first ? fp_mul(acc, lane_load<fp_t>(pre, k - 1)) : acc;
     lane_store(out, k, z ? fp_zero() : r);
-    if (!first && !z) acc = fp_mul(acc, x);
+    if (k > first && !z) acc = fp_mul(acc, x);
   }
 }
 
