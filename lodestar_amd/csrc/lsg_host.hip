@@ -188,10 +188,11 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
     // and every butterfly level costs each lane pair one operation, so use as few pairs per
     // chunk as keep the chip full, folding up to SEG_FOLD_WIDE terms each
     if (op != 2 && (cur.size() << 5) >= SEG_WIDE_PAIRS) {
+      const int wide = (int)lsg_ab_long("LSG_SEG_FOLD_WIDE", SEG_FOLD_WIDE);  // (A/B build)
       int l = 0;
-      while (l < pass.ips_log2 && (int32_t)(SEG_FOLD_WIDE << l) < max_len) l++;
+      while (l < pass.ips_log2 && (int32_t)(wide << l) < max_len) l++;
       pass.ips_log2 = l;
-      fold = SEG_FOLD_WIDE;
+      fold = wide;
     }
     pass.src = src;
     pass.tmp_out = tmp_out;
