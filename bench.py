@@ -132,15 +132,16 @@ class Workload:
                 raise SystemExit("pubkey table load failed")
             contributions, size = 256, 512
             for p in range(n_packages):
-                jobs = []
+                ixs, aggs, ms = [], [], []
                 for c in range(contributions):
                     g = (rank * n_packages + p) * contributions + c
                     start = (g * 131) % N_KEYS
                     ix = [(start + j) % N_KEYS for j in range(size)]
-                    m = msg(tag, g)
-                    sig = ctx.sign([sum(sks[k] for k in ix) % R_ORDER], [m])[0]
-                    jobs.append(([(PkIndices(ix), m, sig)], 1))
-                self.packages.append((jobs, None))
+                    ixs.append(ix)
+                    aggs.append(sum(sks[k] for k in ix) % R_ORDER)
+                    ms.append(msg(tag, g))
+                sigs = ctx.sign(aggs, ms)  # one signing launch per package
+                self.packages.append(([([(PkIndices(ixs[c]), ms[c], sigs[c])], 1) for c in range(contributions)], None))
             self.sets_per_package = contributions
             self.pks_per_set = float(size)
         else:
