@@ -46,9 +46,14 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# pipeline slots x 2 streams + the final-exponentiation streams: give each its own hardware
-# queue instead of HIP's default 4 shared ones
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
+# Hardware queues: the library itself takes GPU_MAX_HW_QUEUES=16 when the process has not set
+# it and HIP is not yet initialised (lsg_init_devices, as in a Node process).  One GPU: nothing
+# is set here, so the run measures the library's own default.  Several ranks: torch initialises
+# HIP before the library, so the same default is set here.  LSG_HW_QUEUES overrides (A/B runs).
+if "LSG_HW_QUEUES" in os.environ:
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LSG_HW_QUEUES"]
+elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -331,6 +336,24 @@ def run_node_workload(args):
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
+
+
+def _build_record():
+    """provenance of the library this run loaded: its manifest (lodestar_amd/build.py) and whether
+    the sources in this tree still hash to what it was built from"""
+    from lodestar_amd import build as b
+    from lodestar_amd import _native
+    lib = _native.LIB_PATH
+    man = b.read_manifest(lib)
+    if man is None:
+        return {"lib": os.path.basename(lib), "manifest": None}
+    srcs = b.SOURCES + (b.AB_SOURCES if lib == b.AB_OUT else [])
+    with open(lib, "rb") as fh:
+        so16 = hashlib.sha256(fh.read()).hexdigest()[:16]
+    return {"lib": man["lib"], "src_sha256_16": man["src_sha256"][:16], "so_sha256_16": man["so_sha256_16"],
+            "so_matches_manifest": so16 == man["so_sha256_16"],
+            "tree_matches_manifest": b.source_hash(srcs) == man["src_sha256"], "compiler": man["compiler"],
+            "built_utc": man["built_utc"]}
 
 
 def main():
@@ -720,8 +743,10 @@ def main():
     sf = opc["stage_fp_muls"]
     per_set_muls += (sf["miller_fused_per_set"] if fused else sf["miller_lines"] + sf[accum_key]) \
         - sf["miller_multi2_per_set"]
-    # extra signers: the batch-affine tree for packages of >= 32768 keys, else the serial fold
-    tree = wl.pks_per_set * n_sets >= 32768
+    # extra signers: the shipped library's fused gather + mixed-addition fold (k_pk_agg_seg,
+    # 12 M per key); the batch-affine tree only in the A/B build with LSG_AGG_TREE=1
+    tree = (os.environ.get("LSG_AGG_TREE") == "1" and "_ab" in os.environ.get("LSG_LIB", "")
+            and wl.pks_per_set * n_sets >= 32768)
     per_set_muls += (wl.pks_per_set - 1) * opc["aggregate_tree_extra_per_pubkey_fp_muls" if tree else
                                                 "aggregate_extra_per_pubkey_fp_muls"]
     per_set_muls -= (1.0 - wl.msgs_per_set) * sf["hash_map"]  # hash_to_G2 once per distinct message
@@ -783,6 +808,7 @@ def main():
             "kernel_ms": {k: round(v, 3) for k, v in agg.items()},
             "probe_lane_fp_mul_per_s": probe_fp,
             "cpu_baseline": cpu,
+            "build": _build_record(),
         }
         print(json.dumps(line), flush=True)
     ctx.close()

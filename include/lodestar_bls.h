@@ -220,8 +220,9 @@ int lsg_aggregate_pubkeys(lsg_ctx* ctx, const uint8_t* pks, uint32_t pk_len, siz
  * a block's aggregate sets, indexedAttestation.ts:21-47): set i's keys are sets[i].pks /
  * pk_len / n_pks (bytes or table indices; msg and sig are ignored).  out96[96 i..] = set i's
  * uncompressed sum; err[i] = its first bad key's BLST_* / LSG_ERR_BAD_INDEX, or
- * LSG_ERR_EMPTY_AGGREGATE for no keys.  Large inputs (>= 32768 keys) run the batch-affine
- * aggregation tree of the jobs path, smaller ones its serial fold. */
+ * LSG_ERR_EMPTY_AGGREGATE for no keys.  Every input size runs the jobs path's fused gather +
+ * mixed-addition fold (k_pk_agg_seg); the batch-affine aggregation tree exists only in the
+ * A/B build (liblodestar_bls_ab.so, LSG_AGG_TREE=1), where it was measured slower. */
 int lsg_aggregate_pubkeys_multi(lsg_ctx* ctx, const lsg_set* sets, size_t n_sets, uint8_t* out96, int32_t* err);
 
 /* hash_to_G2(msg_i, DST) for n messages of msg_len bytes each -> n x 192-byte uncompressed points. */

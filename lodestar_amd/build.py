@@ -93,6 +93,8 @@ def build(force=False, verbose=True, extra=None, out=None):
     extra = list(extra or [])
     out = out or OUT
     if not force and not extra and out == OUT and not needs_rebuild():
+        if read_manifest(OUT) is None:
+            write_manifest(OUT, SOURCES, [])
         return OUT
     odir = _obj_dir(extra)
     os.makedirs(odir, exist_ok=True)
@@ -103,7 +105,54 @@ def build(force=False, verbose=True, extra=None, out=None):
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose, extra), SOURCES))
     _link(objs, out, verbose)
+    write_manifest(out, SOURCES, extra)
     return out
+
+
+def source_hash(sources=SOURCES):
+    """sha256 over the library's sources, headers and the public header (sorted by name)"""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(set([os.path.join(CSRC, f) for f in list(sources) + HEADERS] +
+                       [os.path.join(ROOT, "include", "lodestar_bls.h")]))
+    for f in files:
+        if os.path.exists(f):
+            h.update(os.path.basename(f).encode() + b"\0")
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
+def _compiler_version():
+    try:
+        out = subprocess.run([hipcc(), "--version"], capture_output=True, text=True, timeout=60).stdout
+        return next((ln.strip() for ln in out.splitlines() if "clang version" in ln), out.splitlines()[0].strip())
+    except Exception as e:  # noqa: BLE001 (the manifest still records the rest)
+        return "unknown (%s)" % e
+
+
+def write_manifest(out, sources, extra):
+    """one-line JSON manifest beside the .so: compiler, flags, source hash, build time"""
+    import hashlib
+    import json
+    import time
+    with open(out, "rb") as fh:
+        so_sha = hashlib.sha256(fh.read()).hexdigest()
+    rec = {"lib": os.path.basename(out), "so_sha256_16": so_sha[:16], "src_sha256": source_hash(sources),
+           "compiler": _compiler_version(), "flags": CFLAGS + list(extra),
+           "built_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+    with open(out + ".manifest.json", "w") as fh:
+        fh.write(json.dumps(rec, sort_keys=True) + "\n")
+    return rec
+
+
+def read_manifest(out=None):
+    import json
+    try:
+        with open((out or OUT) + ".manifest.json") as fh:
+            return json.loads(fh.read())
+    except (OSError, ValueError):
+        return None
 
 
 def _link(objs, out, verbose):
@@ -128,6 +177,7 @@ def build_ab(verbose=True):
     objs = [ab.get(s) or os.path.join(OBJ, os.path.splitext(s)[0] + ".o") for s in SOURCES]
     objs += [ab[s] for s in AB_SOURCES if s not in SOURCES]
     _link(objs, AB_OUT, verbose)
+    write_manifest(AB_OUT, SOURCES + AB_SOURCES, AB_FLAGS)
     return AB_OUT
 
 

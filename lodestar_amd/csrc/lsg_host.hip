@@ -53,6 +53,9 @@ namespace {
 const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
 const uint32_t DST_POP_LEN = 43;
 constexpr int LSG_SLOTS = 64;      // packages in flight per device (created on first use)
+#ifndef LSG_DEFAULT_HW_QUEUES
+#define LSG_DEFAULT_HW_QUEUES "16"  // GPU_MAX_HW_QUEUES when the process sets none (lsg_init_devices)
+#endif
 constexpr int LSG_FINALS = 64;     // final-exponentiation entries in flight (lsg_final_*)
 constexpr int LSG_FE_STREAMS = 8;  // streams the final-exponentiation entries share
 constexpr int LSG_MAX_DEVICES = 16;
@@ -1961,7 +1964,8 @@ const uint8_t* pkg_partial_dev(Slot* s) {
 // The package group's partial as it may leave the slot (lsg_jobs_partial*), on the main stream:
 // a lone unscaled set's f is raised to a fresh nonzero 64-bit randomizer (two
 // one-set shards holding sig_a + D and sig_b - D must not pass a product check together).
-int export_partial_dev(Slot* s, const uint8_t** src) {
+// xs: launch the power there instead of on the slot's stream (the partial is complete)
+int export_partial_dev(Slot* s, const uint8_t** src, hipStream_t xs = nullptr) {
   *src = pkg_partial_dev(s);
   if (!s->lone_unscaled) return LSG_OK;
   uint64_t r = 0;
@@ -1979,7 +1983,12 @@ int export_partial_dev(Slot* s, const uint8_t** src) {
   }
   LSG_RC(ensure(s, s->d_xport, 576));
   s->cur = 0;
-  KL(s, "k_fp12_pow", lsgk::fp12_pow_u64(S_(s), *src, r, P_<uint8_t>(s->d_xport)));
+  if (xs) {
+    const hipError_t e = lsgk::fp12_pow_u64(xs, *src, r, P_<uint8_t>(s->d_xport));
+    if (e != hipSuccess) return fail(s, "k_fp12_pow", e);
+  } else {
+    KL(s, "k_fp12_pow", lsgk::fp12_pow_u64(S_(s), *src, r, P_<uint8_t>(s->d_xport)));
+  }
   *src = P_<uint8_t>(s->d_xport);
   return LSG_OK;
 }
@@ -2252,6 +2261,13 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
     }
     any_err_chunk = any_err_chunk || chunk_err[c];
   }
+  // a coalesced sub-package of exactly one chunk: its group has the chunk's sets and r_i
+  std::vector<int> sub_nchunks((size_t)s->n_sub, 0);
+  for (size_t c = 0; c < chunks.size() && s->n_sub; c++) sub_nchunks[(size_t)sub_of_pos(s, chunks[c].first)]++;
+  auto group_is_chunk = [&](size_t c) {
+    if (!s->n_sub) return chunks.size() == 1 && !any_err_chunk;
+    return sub_nchunks[(size_t)sub_of_pos(s, chunks[c].first)] == 1;  // (chunk c has no decode error)
+  };
   for (size_t c = 0; c < chunks.size(); c++) {
     if (job_dead[s->batch_order[chunks[c].first]]) continue;  // its sub-package has a bad key
     const size_t first = s->jobs[s->batch_order[chunks[c].first]].first;
@@ -2275,8 +2291,8 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
       if (pkg_ok(c)) {
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) s->results[s->batch_order[q]] = {LSG_VALID, 0};
         succ_add(chunks[c].first, len);
-      } else if (chunks.size() == 1 && !any_err_chunk && !s->n_sub) {
-        // the package group is exactly this chunk: its verdict is the chunk's
+      } else if (group_is_chunk(c)) {
+        // the package (or sub-package) group is exactly this chunk: its verdict is the chunk's
         retry_inc(chunks[c].first);
         for (size_t q = chunks[c].first; q < chunks[c].second; q++) retry.push_back(s->batch_order[q]);
       } else {
@@ -2751,9 +2767,13 @@ int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* st
     LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
     auto it = c->merged.find(serial);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
-    if (it->second.slot < 0 && !it->second.rc) (void)flush_pending(c);  // the waiter wants it now
+    int frc = LSG_OK;
+    if (it->second.slot < 0 && !it->second.rc) frc = flush_pending(c);  // the waiter wants it now
     it = c->merged.find(serial);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
+    // still held (every slot busy: LSG_ERR_BUSY, c->err says so): the ticket stays live and a
+    // later wait -- after the caller has waited on another ticket -- launches it
+    if (frc && it->second.slot < 0 && !it->second.rc) return frc;
     if (it->second.rc) {  // its coalesced launch failed
       const int frc = it->second.rc;
       c->err = it->second.err;
@@ -2997,6 +3017,15 @@ extern "C" {
 int lsg_init_devices(const int* device_ids, int n_devices, lsg_ctx** out) {
   if (!out || !device_ids || n_devices < 1 || n_devices > LSG_MAX_DEVICES) return LSG_ERR_INVALID_ARG;
   *out = nullptr;
+  // A package keeps two streams busy and up to LSG_SLOTS packages are in flight: HIP's default
+  // of 4 hardware queues per process serialises them.  When the embedding process has not
+  // chosen (the variable unset) and HIP is not yet initialised -- the first lsg_init of a Node
+  // process, before any other HIP call -- take LSG_DEFAULT_HW_QUEUES.  An explicit setting
+  // (GPU_MAX_HW_QUEUES in the environment) always wins; INTEGRATION.md documents both.
+  static std::once_flag hwq_once;
+  std::call_once(hwq_once, [] {
+    if (!getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", LSG_DEFAULT_HW_QUEUES, 0);
+  });
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return LSG_ERR_NO_DEVICE;
   bool distinct = true;
@@ -3207,11 +3236,7 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
   hipStream_t xs = c->dev[0]->s_xp;
   if (has) {
     const uint8_t* src;
-    LSG_RC(export_partial_dev(s, &src));
-    if (s->lone_unscaled) {  // f^r was launched on the package's stream
-      LSG_HIP(s, hipEventRecord(s->ev_grp, s->st[0]));
-      LSG_HIP(s, hipStreamWaitEvent(xs, s->ev_grp, 0));
-    }
+    LSG_RC(export_partial_dev(s, &src, xs));  // f^r (a lone unscaled set) runs on xs too
     LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, xs));
   } else {
     LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, xs));

@@ -415,8 +415,9 @@ static void* engine_main(void* arg) {
     lsg_job* jobs = NULL;
     r->rc = build_jobs(r, &sets, &jobs);
     if (r->rc == LSG_OK) {
-      /* at most LSG_NAPI_THREADS <= lsg_pipeline_slots packages are outstanding per context,
-       * so BUSY only means another host thread of this process shares the context: back off */
+      /* at most n_threads (the package threads plus the priority thread) <= lsg_pipeline_slots
+       * packages are outstanding per context (engine_start), so BUSY only means another host
+       * thread of this process shares the context: back off */
       for (int tries = 0;; tries++) {
         r->rc = lsg_submit_jobs(a->c, jobs, r->n_jobs, r->seed, &r->ticket);
         if (r->rc != LSG_ERR_BUSY || tries > 100000) break;
@@ -485,7 +486,11 @@ static int engine_start(napi_env env, addon_ctx* a) {
   pthread_cond_init(&a->cv, NULL);
   int32_t slots = LSG_NAPI_THREADS;
   lsg_pipeline_slots(a->c, &slots);
-  a->n_threads = (slots < LSG_NAPI_THREADS ? slots : LSG_NAPI_THREADS) + 1;
+  /* package threads: min(slots - 1, LSG_NAPI_THREADS), so that the priority thread always finds
+   * a free slot (with fewer slots than threads it would spin on BUSY behind the packages) */
+  int pkg_threads = slots - 1 < LSG_NAPI_THREADS ? slots - 1 : LSG_NAPI_THREADS;
+  if (pkg_threads < 1) pkg_threads = 1;
+  a->n_threads = pkg_threads + 1;
   a->started = 1;
   for (int i = 0; i < a->n_threads; i++) {
     a->targ[i].a = a;

@@ -159,8 +159,8 @@ def test_config_c_block_128x450(table_ctx, keys):
     got, _ = c.verify_jobs([(wrong[:64], 0), (wrong[64:], 0)])
     assert got == [(1, 0), (0, 0)]
     # the aggregated keys themselves, bit-exact against the oracle's (sum sk) G1: all 128 sets
-    # in one pass of the jobs path's batch-affine aggregation tree (57k keys), and a few through
-    # the single-set serial fold
+    # (57k keys) in one pass of the shipped library's fused gather + mixed-addition fold
+    # (k_pk_agg_seg; the batch-affine tree is A/B-build only), and a few one set at a time
     assert c.aggregate_pubkeys_multi([PkIndices(ix) for ix in idx]) == [(agg_pks[g], 0) for g in range(n)]
     for g in (0, 77, 127):
         assert c.aggregate_pubkeys(PkIndices(idx[g])) == (agg_pks[g], 0)
@@ -489,3 +489,73 @@ def test_coalesced_packages_match_separate_launches(keys):
     finally:
         c.close()
         ref.close()
+
+
+def test_held_merged_ticket_reports_busy(keys):
+    """A coalesced package held while every pipeline slot is taken by un-waited tickets: its
+    wait returns LSG_ERR_BUSY (the ticket stays live), and after another ticket's wait frees a
+    slot the same wait launches and resolves it (the waiter used to get
+    LSG_ERR_INVALID_ARG for a ticket that was still pending)."""
+    from lodestar_amd._native import Context, LSG_ERR_BUSY
+    c = Context(0)
+    try:
+        sets = single_sets(c, keys, b"busy", 6)
+        c.set_coalesce(4, c.pipeline_slots())  # packages of > 4 sets launch on their own
+        direct = []
+        while True:
+            t = c.submit_jobs([([s], 1) for s in sets[:5]])
+            if t is None:
+                break
+            direct.append(t)
+            assert len(direct) <= c.pipeline_slots()
+        assert len(direct) == c.pipeline_slots()
+        held = c.submit_jobs([([sets[5]], 1)])  # coalesced: held, no slot for it
+        assert held is not None
+        with pytest.raises(RuntimeError, match=r"\(%d\)" % LSG_ERR_BUSY):
+            c.wait_jobs(held)
+        assert c.wait_jobs(direct[0])[0] == [(1, 0)] * 5
+        assert c.wait_jobs(held)[0] == [(1, 0)]
+        for t in direct[1:]:
+            assert c.wait_jobs(t)[0] == [(1, 0)] * 5
+    finally:
+        c.close()
+
+
+def _splitmix(seed, n):
+    M = (1 << 64) - 1
+    s, out = seed, []
+    while len(out) < n:
+        s = (s + 0x9E3779B97F4A7C15) & M
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        if z:
+            out.append(z)
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 7, 264])
+def test_shipped_jobs_partial_bit_exact_vs_oracle(ctx, keys, n):
+    """The 576 bytes the SHIPPED library exports for the node exchange (lsg_jobs_partial, what
+    crosses RCCL in SURVEY.md 8e) equal the oracle's partial byte for byte under the seeded
+    splitmix randomizers: 264 sets take the bucket-MSM signature sum (groups >= 256), 7 the
+    per-set scaling, and a lone set is exported unscaled then raised to its own randomizer
+    (lsg_host.hip export_partial_dev)."""
+    from oracle import verifier as ov
+    from oracle.fields import f12_coeffs, f12_pow
+    sets = single_sets(ctx, keys, b"xport%d" % n, n)
+    seed = 0x5eed0000 + n
+    t = ctx.submit_jobs([([s], 1) for s in sets], seed=seed)
+    part, has = ctx.jobs_partial(t)
+    assert has
+    flat = [(p[0], m, s) for p, m, s in sets]
+    if n == 1:
+        exp, errs = ov.batch_partial(flat, [1])
+        exp = f12_pow(exp, _splitmix(seed ^ 0x5851F42D4C957F2D, 1)[0])
+    else:
+        exp, errs = ov.batch_partial(flat, _splitmix(seed, n))
+    assert errs == [0] * n
+    want = b"".join(int(c[0]).to_bytes(48, "big") + int(c[1]).to_bytes(48, "big") for c in f12_coeffs(exp))
+    assert part == want
+    assert ctx.wait_jobs_node(t, 1)[0] == [(1, 0)] * n
