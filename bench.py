@@ -46,14 +46,12 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# Hardware queues: the library itself takes GPU_MAX_HW_QUEUES=16 when the process has not set
-# it and HIP is not yet initialised (lsg_init_devices, as in a Node process).  One GPU: nothing
-# is set here, so the run measures the library's own default.  Several ranks: torch initialises
-# HIP before the library, so the same default is set here.  LSG_HW_QUEUES overrides (A/B runs).
-if "LSG_HW_QUEUES" in os.environ:
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LSG_HW_QUEUES"]
-elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# Hardware queues: the library sets GPU_MAX_HW_QUEUES itself (LSG_HW_QUEUES, default 16) before
+# its first HIP call (lsg_init_devices, as in a Node process).  One GPU: nothing is set here,
+# so the run measures the library's own setting.  Several ranks: torch initialises HIP before
+# the library, so the same value is set here first.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001

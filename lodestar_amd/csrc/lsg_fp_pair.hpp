@@ -172,6 +172,41 @@ extern unsigned long long lsg_mul_count;
 #define LSG_COUNT_MUL() ((void)0)
 #endif
 
+// The end of a CIOS reduction: the 14 accumulators (64-bit, value-preserving) -> limbs in
+// [0, 2^29) and the signed top limb, the pair's cross-lane carry included.
+LSG_PFN void pair_redc_tail(int64_t* t, fp_t& r, bool top) {
+#pragma unroll
+  for (int j = 0; j < LSG_PL - 1; j++) {
+    t[j + 1] += t[j] >> 29;
+    t[j] &= (int64_t)LSG_M29;
+  }
+#if LSG_PAIR_G == 2
+  const int64_t ct = t[LSG_PL - 1] >> 29;
+  const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
+  if (!top) t[LSG_PL - 1] &= (int64_t)LSG_M29;
+  t[0] += (int64_t)(((uint64_t)chi << 32) | clo);
+  // second pass: only limb 0 (lane 1's, plus lane 0's carry of < 2^35) can exceed 32 bits;
+  // limbs 1.. are < 2^29 (the top limb small and signed) and the carries from limb 1 on are
+  // a few units, so the rest runs on 32-bit words (same value, same unique limbs)
+  int32_t c = (int32_t)(t[0] >> 29);
+  r.l[0] = (uint32_t)t[0] & LSG_M29;
+#pragma unroll
+  for (int j = 1; j < LSG_PL; j++) {
+    const int32_t v = (int32_t)(uint32_t)t[j] + c;
+    if (j < LSG_PL - 1) {
+      c = v >> 29;
+      r.l[j] = (uint32_t)v & LSG_M29;
+    } else {
+      r.l[j] = (uint32_t)v;
+    }
+  }
+#else
+  (void)top;
+#pragma unroll
+  for (int j = 0; j < LSG_PL; j++) r.l[j] = (uint32_t)t[j];
+#endif
+}
+
 // ---- Montgomery product (CIOS over the 14 radix-2^29 limbs, i-loop over time)
 // N independent products advance step by step together: in-order issue stalls a lone
 // product on its serial chain (t0 mad -> m -> DPP broadcast -> m*p mads -> retire) at the
@@ -219,44 +254,109 @@ LSG_PFN void pair_mont_mul_n(fp_t* r, const fp_t* a, const fp_t* b) {
     }
   }
 #pragma unroll
-  for (int n = 0; n < N; n++) {
+  for (int n = 0; n < N; n++) pair_redc_tail(t[n], r[n], top);
+}
+#ifndef LSG_SOP_STEP_FENCE
+#define LSG_SOP_STEP_FENCE 0
+#endif
+// ---- sums of two products with one Montgomery reduction (fp_sop)
+//   r_n = REDC(xa_n ya_n + xb_n yb_n)
+// ONE CIOS pass with two partial products per step.  The Fp2 product is two of them,
+//   c0 = REDC(a0 b0 + (-a1) b1),  c1 = REDC(a0 b1 + a1 b0)        (u^2 = -1),
+// the same 588 mads per lane as Karatsuba's three full products, without its third
+// reduction's overhead, its two additions and three subtractions (~330 other instructions per
+// lane instead of ~560).  Bounds: in the pair layout an accumulator lives at most 7 steps on
+// each lane (lane 1 hands only its low 29 bits down, the carry stays behind), so it sums at
+// most 7 x 3 terms of < 2^58.1: |t| < 2^62.6.  The one-lane host build (LSG_PAIR_G = 1) keeps
+// a column for 14 steps and carries once at mid-loop instead.  For inputs |x|, |y| < 2^12.6 p
+// the outputs satisfy |r| < 3p.
+template <int N, bool NEG0 = false>  // NEG0: output 0 takes xa ya - xb yb
+LSG_PFN void pair_sop2_n(fp_t* r, const fp_t* xa, const fp_t* ya, const fp_t* xb, const fp_t* yb) {
+  const bool top = pair_top();
+  uint32_t p[LSG_PL];
 #pragma unroll
-    for (int j = 0; j < LSG_PL - 1; j++) {
-      t[n][j + 1] += t[n][j] >> 29;
-      t[n][j] &= (int64_t)LSG_M29;
-    }
-  }
-#if LSG_PAIR_G == 2
-#pragma unroll
-  for (int n = 0; n < N; n++) {
-    const int64_t ct = t[n][LSG_PL - 1] >> 29;
-    const uint32_t clo = pup((uint32_t)ct), chi = pup((uint32_t)((uint64_t)ct >> 32));
-    if (!top) t[n][LSG_PL - 1] &= (int64_t)LSG_M29;
-    t[n][0] += (int64_t)(((uint64_t)chi << 32) | clo);
-    // second pass: only limb 0 (lane 1's, plus lane 0's carry of < 2^35) can exceed 32 bits;
-    // limbs 1.. are < 2^29 (the top limb small and signed) and the carries from limb 1 on are
-    // a few units, so the rest runs on 32-bit words (same value, same unique limbs)
-    int32_t c = (int32_t)(t[n][0] >> 29);
-    r[n].l[0] = (uint32_t)t[n][0] & LSG_M29;
-#pragma unroll
-    for (int j = 1; j < LSG_PL; j++) {
-      const int32_t v = (int32_t)(uint32_t)t[n][j] + c;
-      if (j < LSG_PL - 1) {
-        c = v >> 29;
-        r[n].l[j] = (uint32_t)v & LSG_M29;
-      } else {
-        r[n].l[j] = (uint32_t)v;
-      }
-    }
-  }
-#else
-  (void)top;
+  for (int j = 0; j < LSG_PL; j++) p[j] = pair_pick(LSG_P, j);
+  int64_t t[N][LSG_PL];
 #pragma unroll
   for (int n = 0; n < N; n++)
 #pragma unroll
-    for (int j = 0; j < LSG_PL; j++) r[n].l[j] = (uint32_t)t[n][j];
+    for (int j = 0; j < LSG_PL; j++) t[n][j] = 0;
+  uint32_t m29 = LSG_M29, lmask = top ? 0u : LSG_M29;
+#if LSG_PAIR_G == 2
+  asm volatile("" : "+v"(m29), "+v"(lmask));  // register operands: the DPP moves fold into the ands
+#endif
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const uint32_t sa = ya[n].l[i % LSG_PL], sb = yb[n].l[i % LSG_PL];
+      const int32_t ba = (int32_t)(i / LSG_PL == 0 ? pbcast<0>(sa) : pbcast<LSG_GROUP - 1>(sa));
+      int32_t bb = (int32_t)(i / LSG_PL == 0 ? pbcast<0>(sb) : pbcast<LSG_GROUP - 1>(sb));
+      if (NEG0 && n == 0) bb = -bb;
+#pragma unroll
+      for (int j = 0; j < LSG_PL; j++) {
+        t[n][j] += (int64_t)(int32_t)xa[n].l[j] * ba;
+        t[n][j] += (int64_t)(int32_t)xb[n].l[j] * bb;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const uint32_t m = pbcast0_and((uint32_t)t[n][0] * LSG_N0P, m29);
+#pragma unroll
+      for (int j = 0; j < LSG_PL; j++) t[n][j] += (int64_t)(int32_t)m * (int32_t)p[j];
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const int64_t c = t[n][0] >> 29;
+      const uint32_t mv = pdown_and((uint32_t)t[n][0], lmask);
+#pragma unroll
+      for (int j = 0; j < LSG_PL - 1; j++) t[n][j] = t[n][j + 1];
+      t[n][0] += c;
+      t[n][LSG_PL - 1] = (int64_t)mv;
+    }
+#if LSG_PAIR_G == 2 && LSG_SOP_STEP_FENCE
+    __builtin_amdgcn_sched_barrier(0);  // no step's broadcasts hoisted into an earlier one
+#endif
+#if LSG_PAIR_G == 1
+    if (i == 6) {  // one lane holds every column for 14 steps: carry once (value-preserving)
+#pragma unroll
+      for (int n = 0; n < N; n++)
+#pragma unroll
+        for (int j = 0; j < LSG_PL - 1; j++) {
+          t[n][j + 1] += t[n][j] >> 29;
+          t[n][j] &= (int64_t)LSG_M29;
+        }
+    }
+#endif
+  }
+#pragma unroll
+  for (int n = 0; n < N; n++) pair_redc_tail(t[n], r[n], top);
+}
+LSG_PFN fp_t pair_neg_limbs(const fp_t& a) {  // -a limb by limb (no carry: SOP operands are signed)
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < LSG_PL; k++) r.l[k] = 0u - a.l[k];
+  return r;
+}
+#ifndef LSG_SOP_INTERLEAVE  // A/B: 1 = the two outputs of an Fp2 product in one pass
+#define LSG_SOP_INTERLEAVE 0
+#endif
+LSG_PFN void pair_fp2_mul_sop(fp_t& c0, fp_t& c1, const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
+#if LSG_SOP_INTERLEAVE
+  const fp_t xa[2] = {a0, a0}, ya[2] = {b0, b1}, xb[2] = {a1, a1}, yb[2] = {b1, b0};
+  fp_t r[2];
+  pair_sop2_n<2, true>(r, xa, ya, xb, yb);
+  c0 = r[0];
+  c1 = r[1];
+#else
+  pair_sop2_n<1, true>(&c0, &a0, &b0, &a1, &b1);
+#if LSG_PAIR_G == 2
+  __builtin_amdgcn_sched_barrier(0);  // one pass after the other: half the live accumulators
+#endif
+  pair_sop2_n<1>(&c1, &a0, &b1, &a1, &b0);
 #endif
 }
+
 LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
   LSG_COUNT_MUL();
   fp_t r;
@@ -270,6 +370,9 @@ LSG_PLEAF fp_t pair_mont_mul(fp_t a, fp_t b) {
 // leaves below with their products one after another (default), 2 = interleaved
 #ifndef LSG_LEAF_MODE
 #define LSG_LEAF_MODE 1
+#endif
+#ifndef LSG_FP2_SOP  // A/B builds: 0 = the Karatsuba Fp2 leaf (three full products)
+#define LSG_FP2_SOP 1
 #endif
 #if LSG_PAIR_G == 2 && LSG_LEAF_MODE == 1
 #define LSG_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -420,6 +523,11 @@ LSG_PLEAF fp_duo pair_fp2_mul_v(fp_arg_t va0, fp_arg_t va1, fp_arg_t vb0, LSG_TA
   LSG_COUNT_MUL();
   LSG_COUNT_MUL();
   const fp_t a0 = fp_unpack(va0), a1 = fp_unpack(va1), b0 = fp_unpack(vb0), b1 = LSG_TAIL_UNPACK(vb1);
+#if LSG_FP2_SOP
+  fp_duo d;
+  pair_fp2_mul_sop(d.x, d.y, a0, a1, b0, b1);
+  return d;
+#endif
   // the three products run one after another (sched_barrier): interleaved, the leaf needed
   // ~180 VGPRs, and every caller had to spill around it what the call clobbers
   fp_t t[3];

@@ -3018,13 +3018,16 @@ int lsg_init_devices(const int* device_ids, int n_devices, lsg_ctx** out) {
   if (!out || !device_ids || n_devices < 1 || n_devices > LSG_MAX_DEVICES) return LSG_ERR_INVALID_ARG;
   *out = nullptr;
   // A package keeps two streams busy and up to LSG_SLOTS packages are in flight: HIP's default
-  // of 4 hardware queues per process serialises them.  When the embedding process has not
-  // chosen (the variable unset) and HIP is not yet initialised -- the first lsg_init of a Node
-  // process, before any other HIP call -- take LSG_DEFAULT_HW_QUEUES.  An explicit setting
-  // (GPU_MAX_HW_QUEUES in the environment) always wins; INTEGRATION.md documents both.
+  // of 4 hardware queues per process serialises them (profiles/r05_hwq_ab.txt).  The library
+  // owns this setting: before its first HIP call it sets GPU_MAX_HW_QUEUES to LSG_HW_QUEUES
+  // (1..32, default LSG_DEFAULT_HW_QUEUES), overriding a process-wide default such as the
+  // GPU_MAX_HW_QUEUES=4 some hosts export.  It takes effect when HIP is not yet initialised --
+  // the first lsg_init of a Node process; INTEGRATION.md section 5.
   static std::once_flag hwq_once;
   std::call_once(hwq_once, [] {
-    if (!getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", LSG_DEFAULT_HW_QUEUES, 0);
+    const char* want = getenv("LSG_HW_QUEUES");
+    const int q = want ? atoi(want) : 0;
+    setenv("GPU_MAX_HW_QUEUES", (q >= 1 && q <= 32) ? want : LSG_DEFAULT_HW_QUEUES, 1);
   });
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return LSG_ERR_NO_DEVICE;

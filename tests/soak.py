@@ -28,8 +28,6 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if "LSG_HW_QUEUES" in os.environ:  # (otherwise the library's own default, lsg_init_devices)
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LSG_HW_QUEUES"]
 sys.path.insert(0, ROOT)
 
 from lodestar_amd import _native as N  # noqa: E402

@@ -1,17 +1,18 @@
 #!/bin/bash
-# GPU-box A/B of the hardware-queue count: the library's own default
-# (GPU_MAX_HW_QUEUES unset: lsg_init_devices sets 16 before its first HIP call) against an
-# explicit 4 (HIP's default) and 16, interleaved, for the jobs, gossip and Node workloads.
+# GPU-box A/B of the hardware-queue count: the library's own setting
+# (lsg_init_devices sets GPU_MAX_HW_QUEUES=16 before its first HIP call) against LSG_HW_QUEUES=4
+# (HIP's default) and 16, interleaved, for the jobs, gossip and Node workloads.
 #   bash tools/gpu_hwq_ab.sh      -> gpurun_out/r05_hwq_<workload>_<setting>.json
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-unset GPU_MAX_HW_QUEUES LSG_HW_QUEUES
+echo "box environment: GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-<unset>}"
+unset LSG_HW_QUEUES
 one() {  # setting workload
   local q=$1 w=$2 out="gpurun_out/r05_hwq_${2}_${1}"
   echo "== hwq=$q $w ($(date +%T))"
-  if [ "$q" = lib ]; then
+  if [ "$q" = lib ]; then  # the library's own setting, over whatever the box exports
     timeout -k 10 300 python -u bench.py --workload "$w" --no-cpu-baseline > "$out.json" 2> "$out.err"
   else
     LSG_HW_QUEUES=$q timeout -k 10 300 python -u bench.py --workload "$w" --no-cpu-baseline > "$out.json" 2> "$out.err"
