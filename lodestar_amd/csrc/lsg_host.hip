@@ -915,6 +915,10 @@ int run_pk_seg(Slot* s, const SegPlan& P, uint32_t* dst) {
   return LSG_OK;
 }
 
+// batched inversions in one launch per call (k_binv_block); LSG_BINV_BLOCK=0 (A/B build): the
+// multi-level fold / root / unfold launches
+static bool binv_block_on() { return lsg_ab_long("LSG_BINV_BLOCK", 1) != 0; }
+
 // Words (per Fp of W_FP) of the two scratch arrays a batched inversion of n values needs:
 // lv = every level's prefix products plus levels >= 1's values, iv = levels >= 1's inverses
 void binv_sizes(size_t n, size_t* lv, size_t* iv) {
@@ -939,6 +943,11 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
   LSG_RC(ensure(s, s->binv_iv[ws], 4 * W_FP * ivw));
   uint32_t* lv = P_<uint32_t>(s->binv_lv[ws]);
   uint32_t* iv = P_<uint32_t>(s->binv_iv[ws]);
+  if (binv_block_on()) {  // one launch: a divstep root per block of 128 x T values
+    const int T = (int)std::max<size_t>(1, (n + 128 * 1024 - 1) / (128 * 1024));  // >= 1024 blocks before T grows
+    KL(s, name, lsgk::binv_block(S_(s), (int)n, T, 1, v, lv, out));
+    return LSG_OK;
+  }
   // level l: values val[l] (val[0] = v), prefix products pre[l], inverses inv[l] (inv[0] = out)
   std::vector<size_t> cnt{n};
   std::vector<uint32_t*> val{(uint32_t*)v}, pre, inv{out};

@@ -190,46 +190,6 @@ LSG_DEVI fp_t agg_redo(const uint32_t* __restrict__ pts, const uint8_t* __restri
   return acc;
 }
 
-// The LDS heap of a fold group of G leaves (nodes G..2G-1; node 1 = the product of all):
-// lane pair `leaf` (< 0: none) contributes v.  Every thread of the block calls it.
-template <int G>
-LSG_DEVI void heap_up(uint32_t* Hg, int leaf, const fp_t& v) {
-  if (leaf >= 0) lane_store(Hg, G + leaf, v);
-#pragma unroll 1
-  for (int w = G / 2; w >= 1; w >>= 1) {
-    __syncthreads();
-    if (leaf >= 0 && leaf < w)
-      lane_store(Hg, w + leaf, fp_mul(lane_load<fp_t>(Hg, 2 * (w + leaf)), lane_load<fp_t>(Hg, 2 * (w + leaf) + 1)));
-  }
-  __syncthreads();
-}
-// ... and down: Ig[1] (set by the caller) = 1 / Hg[1]; leaves' inverses in Ig[G..2G-1]
-template <int G>
-LSG_DEVI void heap_down(const uint32_t* Hg, uint32_t* Ig, int leaf) {
-#pragma unroll 1
-  for (int w = 2; w <= G; w <<= 1) {
-    __syncthreads();
-    if (leaf < w) {
-      const int i = w + leaf;
-      lane_store(Ig, i, fp_mul(lane_load<fp_t>(Ig, i >> 1), lane_load<fp_t>(Hg, i ^ 1)));
-    }
-  }
-  __syncthreads();
-}
-
-// every participating lane pair's 1 / v: heap up, the root inverted (lane pair 0, divsteps),
-// heap down.  G leaves; every thread of the block calls it; H, I: 2G-node LDS heaps.
-template <int G>
-LSG_DEVI fp_t block_inv(uint32_t* H, uint32_t* I, int leaf, const fp_t& v) {
-  heap_up<G>(H, leaf, v);
-  if (leaf == 0) {
-    const fp_t d = pair_inv_gcd(pair_canon(lane_load<fp_t>(H, 1)));  // (x R)^-1 as an integer
-    lane_store(I, 1, pair_mont_mul(d, fp_t(FP_RCUBE)));                // x^-1 R
-  }
-  heap_down<G>(H, I, leaf < 0 ? G : leaf);
-  return leaf >= 0 ? lane_load<fp_t>(I, G + leaf) : v;
-}
-
 // level 0: gather each item's two keys, fold the chunk, invert the block's chunk products
 __global__ void LSG_KERNEL_ATTR k_agg_leaf(lsgk::AggTreeArgs a) {
   __shared__ uint32_t H[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP], I[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP];

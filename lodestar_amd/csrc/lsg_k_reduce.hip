@@ -125,6 +125,40 @@ __global__ void LSG_KERNEL_ATTR k_binv_unfold(int n, int zero_to_one, const uint
   }
 }
 
+// One-launch batched inversion: every workgroup inverts its own share --
+// lane pair l of block b folds the T consecutive values from (b * 128 + l) * T into prefix
+// products, the block's 128 chunk products go through an LDS heap with ONE divstep inversion
+// at its root (block_inv), and each lane pair unfolds its chunk.  No level crosses a block,
+// so the fold / root / unfold launches of the multi-level form (2 log16 n + 1 of them, each a
+// latency-bound stub between real kernels) become one.  zero_to_one: zeros fold as one and
+// come out as zero (fp_inv(0) = 0).
+__global__ void LSG_KERNEL_ATTR k_binv_block(int n, int T, int zero_to_one, const uint32_t* __restrict__ in,
+                                             uint32_t* __restrict__ pre, uint32_t* __restrict__ out) {
+  __shared__ uint32_t H[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP], I[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP];
+  lsg_lane_setup();
+  const int l = (int)(threadIdx.x / LSG_GROUP);
+  const int64_t first = ((int64_t)blockIdx.x * LSG_ITEMS_PER_BLOCK + l) * T;
+  const int64_t last = first + T < (int64_t)n ? first + T : (int64_t)n;
+  const fp_t one = fp_one();
+  fp_t acc = one;
+#pragma unroll 1
+  for (int64_t k = first; k < last; k++) {
+    fp_t x = lane_load<fp_t>(in, (size_t)k);
+    if (zero_to_one) x = fp_select(fp_is_zero(x), one, x);
+    acc = k == first ? x : fp_mul(acc, x);
+    if (T > 1) lane_store(pre, (size_t)k, acc);
+  }
+  fp_t inv = block_inv<LSG_ITEMS_PER_BLOCK>(H, I, l, acc);  // every lane pair is a leaf (one when idle)
+#pragma unroll 1
+  for (int64_t k = last - 1; k >= first; k--) {
+    const fp_t x = lane_load<fp_t>(in, (size_t)k);
+    const bool z = zero_to_one && fp_is_zero(x);
+    const fp_t r = k > first ? fp_mul(inv, lane_load<fp_t>(pre, (size_t)k - 1)) : inv;
+    lane_store(out, (size_t)k, z ? fp_zero() : r);
+    if (k > first && !z) inv = fp_mul(inv, x);
+  }
+}
+
 // partials: canonical big-endian 576-byte Fp12 blobs <-> lane form (one item each)
 __global__ void LSG_KERNEL_ATTR k_blobs_to_fp12(int n, const uint8_t* __restrict__ blobs, uint32_t* __restrict__ out) {
   LANE_ITEM(n);
@@ -201,6 +235,12 @@ hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const 
 }
 hipError_t binv_fold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* tot) {
   LSG_LAUNCH_ITEMS(k_binv_fold, (n + LSG_BINV_T - 1) / LSG_BINV_T, st, n, zero_to_one, in, pre, tot);
+}
+hipError_t binv_block(hipStream_t st, int n, int T, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* out) {
+  if (n <= 0) return hipSuccess;
+  const size_t chunks = ((size_t)n + T - 1) / T;
+  hipLaunchKernelGGL(k_binv_block, dim3(lane_blocks(chunks)), dim3(LSG_TPB), 0, st, n, T, zero_to_one, in, pre, out);
+  return hipGetLastError();
 }
 hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv) {
   LSG_LAUNCH_ITEMS(k_binv_root, 1, st, top, inv);

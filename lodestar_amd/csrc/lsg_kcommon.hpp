@@ -16,6 +16,7 @@ namespace {
 #include "lsg_fp_pair.hpp"
 #include "lsg_h2c.hpp"
 #include "lsg_io.hpp"
+#include "lsg_inv.hpp"  // block_inv's divstep root (below)
 
 static_assert(lane_words<fp_t>() == lsgl::W_FP, "layout: Fp");
 static_assert(lane_words<g1a_t>() == lsgl::W_G1A, "layout: G1 affine");
@@ -80,6 +81,46 @@ static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * bl
   const size_t item = gtid() / LSG_GROUP;   \
   if (item >= (size_t)(n)) return;          \
   const bool lead = (threadIdx.x % LSG_GROUP) == 0
+
+// The LDS heap of a fold group of G leaves (nodes G..2G-1; node 1 = the product of all):
+// lane pair `leaf` (< 0: none) contributes v.  Every thread of the block calls it.
+template <int G>
+static __device__ __forceinline__ void heap_up(uint32_t* Hg, int leaf, const fp_t& v) {
+  if (leaf >= 0) lane_store(Hg, G + leaf, v);
+#pragma unroll 1
+  for (int w = G / 2; w >= 1; w >>= 1) {
+    __syncthreads();
+    if (leaf >= 0 && leaf < w)
+      lane_store(Hg, w + leaf, fp_mul(lane_load<fp_t>(Hg, 2 * (w + leaf)), lane_load<fp_t>(Hg, 2 * (w + leaf) + 1)));
+  }
+  __syncthreads();
+}
+// ... and down: Ig[1] (set by the caller) = 1 / Hg[1]; leaves' inverses in Ig[G..2G-1]
+template <int G>
+static __device__ __forceinline__ void heap_down(const uint32_t* Hg, uint32_t* Ig, int leaf) {
+#pragma unroll 1
+  for (int w = 2; w <= G; w <<= 1) {
+    __syncthreads();
+    if (leaf < w) {
+      const int i = w + leaf;
+      lane_store(Ig, i, fp_mul(lane_load<fp_t>(Ig, i >> 1), lane_load<fp_t>(Hg, i ^ 1)));
+    }
+  }
+  __syncthreads();
+}
+
+// every participating lane pair's 1 / v: heap up, the root inverted (lane pair 0, divsteps),
+// heap down.  G leaves; every thread of the block calls it; H, I: 2G-node LDS heaps.
+template <int G>
+static __device__ __forceinline__ fp_t block_inv(uint32_t* H, uint32_t* I, int leaf, const fp_t& v) {
+  heap_up<G>(H, leaf, v);
+  if (leaf == 0) {
+    const fp_t d = pair_inv_gcd(pair_canon(lane_load<fp_t>(H, 1)));  // (x R)^-1 as an integer
+    lane_store(I, 1, pair_mont_mul(d, fp_t(FP_RCUBE)));                // x^-1 R
+  }
+  heap_down<G>(H, I, leaf < 0 ? G : leaf);
+  return leaf >= 0 ? lane_load<fp_t>(I, G + leaf) : v;
+}
 
 static inline int lane_blocks(size_t items) { return (int)((items + LSG_ITEMS_PER_BLOCK - 1) / LSG_ITEMS_PER_BLOCK); }
 

@@ -120,6 +120,8 @@ hipError_t seg_reduce(hipStream_t st, int op, int n_chunks, int ips_log2, const 
 // chunk products tot), root (one inversion), unfold (out = 1/in, 0 for zeros when zero_to_one)
 hipError_t binv_fold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* tot);
 hipError_t binv_root(hipStream_t st, const uint32_t* top, uint32_t* inv);
+// one-launch form: every block inverts its own 128 x T values (one divstep root per block)
+hipError_t binv_block(hipStream_t st, int n, int T, int zero_to_one, const uint32_t* in, uint32_t* pre, uint32_t* out);
 hipError_t binv_unfold(hipStream_t st, int n, int zero_to_one, const uint32_t* in, const uint32_t* pre,
                        const uint32_t* tinv, uint32_t* out);
 hipError_t blobs_to_fp12(hipStream_t st, int n, const uint8_t* blobs, uint32_t* out);
