@@ -381,6 +381,11 @@ struct Slot {
   std::vector<int> chunk_group;     // chunk mode: per chunk of batch_order, its phase-A group
   std::vector<int> sub_big;         // a coalesced launch: per sub-package, its package group (-1: none)
   std::vector<int> job_group;       // per job: its phase-A group (non-batchable), else -1
+  // the non-batchable jobs' merged group (-1: one group per job) and, per job, its phase-A
+  // items (the merged group's items never cross a job: a failing merged group is localised
+  // per job over them)
+  int nb_g = -1;
+  std::vector<std::pair<int32_t, int32_t>> nb_items;
   std::vector<lsg_job_result> results;
   lsg_stats stats;
   bool has_node = false;  // this slot computed the node check (device 0 of a multi-device ticket)
@@ -762,6 +767,11 @@ bool package_group_mode() { return lsg_ab_long("LSG_PACKAGE_GROUP", 1) != 0; }
 // A coalesced launch with one package group per sub-package (A/B build: LSG_SUB_GROUPS=0 gives
 // round 3's one group per 16-job chunk)
 bool sub_groups_on() { return lsg_ab_long("LSG_SUB_GROUPS", 1) != 0; }
+// A package's non-batchable jobs (>= 2 of them with sets) verified as ONE RLC group, localised
+// per job only when it fails (A/B build: LSG_NB_MERGE=0 gives one group per job).  Each job's
+// verdict is its own validity either way (worker.ts:88-96: such a job is verified alone), and
+// non-batchable jobs never enter the batch counters.
+bool nb_merge_on() { return lsg_ab_long("LSG_NB_MERGE", 1) != 0; }
 
 void binv_sizes(size_t n, size_t* lv, size_t* iv);
 size_t binv_lv_words(size_t n) {
@@ -1750,6 +1760,8 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   s->lone_unscaled = false;
   s->big_fe_pending = false;
   s->seed = seed;
+  s->nb_g = -1;
+  s->nb_items.clear();
   std::vector<const lsg_set*> flat;
   std::vector<size_t> nonb;
   for (int pass = 0; pass < 2; pass++)
@@ -1809,8 +1821,13 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
           if (s->jobs[s->batch_order[q]].count == 1) noscale[s->jobs[s->batch_order[q]].first] = 1;
     }
   }
+  // the merged non-batchable group (nb_merge_on): every one of its sets is randomised, so a
+  // one-set job in it is scaled too (its own check, if the group fails, stays exact: r_i != 0)
+  size_t nb_live = 0;
+  for (size_t k : nonb) nb_live += s->jobs[k].count ? 1 : 0;
+  const bool nb_merge = nb_merge_on() && nb_live >= 2 && !subs && package_group_mode();
   for (size_t k : nonb)
-    if (s->jobs[k].count == 1) noscale[s->jobs[k].first] = 1;
+    if (s->jobs[k].count == 1 && !nb_merge) noscale[s->jobs[k].first] = 1;
   LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true, &noscale, true));
   // phase-A groups, MSM groups first: the package group, then one per non-batchable job
   PhasePlan& A = s->phA;
@@ -1851,23 +1868,35 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   } else if (s->nb_sets) {
     add(0, s->nb_sets, -2);
   }
+  size_t nb_first = 0, nb_len = 0;
   for (size_t k : nonb) {
-    if (s->jobs[k].count == 0)
+    if (s->jobs[k].count == 0) {
       s->results[k] = {LSG_ERROR, LSG_ERR_EMPTY_SET};  // maybeBatch.ts:29-31
-    else
+    } else if (nb_merge) {  // staged contiguously after the batchable sets, in job order
+      if (!nb_len) nb_first = s->jobs[k].first;
+      nb_len += s->jobs[k].count;
+    } else {
       add(s->jobs[k].first, s->jobs[k].count, (int)k);
+    }
   }
+  constexpr int NB_OWNER = INT32_MIN;  // (chunk owners are -3 - c, sub-package owners -1000 - k)
+  if (nb_merge) add(nb_first, nb_len, NB_OWNER);
   A.groups = gm;
   A.groups.insert(A.groups.end(), gs.begin(), gs.end());
   om.insert(om.end(), os.begin(), os.end());
   // the package group's items never cross a 16-job chunk: if the group fails, each chunk's
   // check (phase B) reuses them instead of re-running the Miller accumulation
   std::vector<size_t> chunk_sub;  // chunks with sets, in order
+  if (nb_merge || (!s->chunk_mode && s->nb_sets)) A.sub.assign(om.size(), {});
+  if (nb_merge)  // the merged group's items never cross a job
+    for (size_t g = 0; g < om.size(); g++)
+      if (om[g] == NB_OWNER)
+        for (size_t k : nonb)
+          if (s->jobs[k].count) A.sub[g].push_back({s->jobs[k].first, s->jobs[k].first + s->jobs[k].count});
   if (!s->chunk_mode && s->nb_sets) {
     chunks = slot_chunks(s);
-    A.sub.assign(om.size(), {});
     for (size_t g = 0; g < om.size(); g++) {
-      if (om[g] != -2 && om[g] > -1000) continue;
+      if ((om[g] != -2 && om[g] > -1000) || om[g] == NB_OWNER) continue;
       const int sub = om[g] <= -1000 ? -1000 - om[g] : -1;
       for (size_t c = 0; c < chunks.size(); c++) {
         if (sub >= 0 && sub_of_pos(s, chunks[c].first) != sub) continue;
@@ -1884,10 +1913,12 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   for (size_t g = 0; g < om.size(); g++) {
     if (om[g] == -2)
       s->big_g = (int)g;
+    else if (om[g] == NB_OWNER)
+      s->nb_g = (int)g;
+    else if (om[g] <= -3 && s->chunk_mode)  // (chunk mode has no sub-package owners)
+      s->chunk_group[(size_t)(-3 - om[g])] = (int)g;
     else if (om[g] <= -1000)
       s->sub_big[(size_t)(-1000 - om[g])] = (int)g;
-    else if (om[g] <= -3)
-      s->chunk_group[(size_t)(-3 - om[g])] = (int)g;
     else
       s->job_group[(size_t)om[g]] = (int)g;
   }
@@ -1922,14 +1953,31 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     A.n_magg = s->n_msgs;
   }
   LSG_RC(plan_phase(s, A));
+  if (s->nb_g >= 0) {  // per non-batchable job, its items among the merged group's
+    s->nb_items.assign(nj, {-1, -1});
+    size_t r = 0;
+    for (size_t g = 0; g < om.size(); g++) {
+      if ((int)g == A.agg_g) continue;  // (message items: no sub_items entries)
+      const size_t ns = g < A.sub.size() && !A.sub[g].empty() ? A.sub[g].size() : 1;
+      if ((int)g == s->nb_g) {
+        size_t q = r;
+        for (size_t k : nonb)
+          if (s->jobs[k].count) s->nb_items[k] = A.sub_items[q++];
+      }
+      r += ns;
+    }
+    for (size_t k : nonb)
+      if (s->jobs[k].count) s->job_group[k] = s->nb_g;
+  }
   s->chunk_items.assign(chunks.size(), {-1, -1});
   if (!chunk_sub.empty() && A.agg_g < 0) {  // sub_items of the package group, in chunk order
     size_t r = 0;
     for (size_t g = 0; g < om.size(); g++) {
       const size_t ns = g < A.sub.size() && !A.sub[g].empty() ? A.sub[g].size() : 1;
-      if (om[g] == -2 || om[g] <= -1000)
+      const bool pkg = om[g] == -2 || (om[g] <= -1000 && om[g] != NB_OWNER);
+      if (pkg)
         for (size_t k = 0; k < ns; k++) s->chunk_items[chunk_sub[k]] = A.sub_items[r + k];
-      if (om[g] == -2 || om[g] <= -1000) chunk_sub.erase(chunk_sub.begin(), chunk_sub.begin() + (long)ns);
+      if (pkg) chunk_sub.erase(chunk_sub.begin(), chunk_sub.begin() + (long)ns);
       r += ns;
     }
   }
@@ -2231,12 +2279,31 @@ int pkg_resolve(Slot* s, CtxLock* lk, int node_valid, int32_t pkfail) {
         job_dead[j] = 1;
       }
   }
-  // non-batchable jobs: their own group (worker.ts:88-96)
+  // non-batchable jobs: their own group (worker.ts:88-96), or the merged group (nb_g): a
+  // passing one answers every such job; a failing one is localised job by job over the jobs'
+  // resident phase-A items (a fallback phase), so each verdict is still the job's own
+  std::vector<Grp> nbg;
+  std::vector<size_t> nbj;
+  std::vector<std::pair<int32_t, int32_t>> nbi;
   for (size_t j = 0; j < nj; j++) {
     const int g = s->job_group[j];
     if (g < 0 || job_dead[j]) continue;
     const int32_t e = job_error(ss, s->jobs[j].first, s->jobs[j].count);
+    if (!e && g == s->nb_g && !vA[(size_t)g]) {
+      Grp q;
+      q.first = s->jobs[j].first;
+      q.len = s->jobs[j].count;
+      nbg.push_back(q);
+      nbj.push_back(j);
+      nbi.push_back(s->nb_items[j]);
+      continue;
+    }
     s->results[j] = e ? lsg_job_result{LSG_ERROR, e} : lsg_job_result{vA[(size_t)g] ? LSG_VALID : LSG_INVALID, 0};
+  }
+  if (!nbg.empty()) {
+    std::vector<int32_t> vn;
+    LSG_RC(run_fallback_phase(s, lk, nbg, &nbi, vn));
+    for (size_t k = 0; k < nbj.size(); k++) s->results[nbj[k]] = {vn[k] ? LSG_VALID : LSG_INVALID, 0};
   }
   if (s->batch_order.empty()) return LSG_OK;
   // batchable jobs: chunks of >= 16 jobs (worker.ts:51-86)

@@ -338,13 +338,14 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
   // LSG_MF_WAVES waves per SIMD instead of the one workgroup per CU the LDS allows, so the
   // other kernels of the pipeline can share the SIMDs while this one waits at its barriers
   extern __shared__ uint32_t lds[];
-  const int w = (int)(threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform: an SGPR
   const size_t it = (size_t)blockIdx.x * MF_ITEMS + ((threadIdx.x & 63) >> 1);
   const bool live = it < (size_t)n_items;  // lanes past the end run item 0's data and store nothing
   const size_t itc = live ? it : 0;
   const int first = item_first[itc], cnt = item_cnt[itc];
   const int si = first + (w < cnt ? w : cnt - 1);
-  const bool use = live && w < cnt && err[si] == 0 && !pinf[si] && !hinf[si];
+  // the lanes whose pair contributes, as a wave mask (SGPRs) rather than a live VGPR
+  const uint64_t use_mask = __ballot(live && w < cnt && err[si] == 0 && !pinf[si] && !hinf[si]);
   // nothing stays in registers across the loop: T lives in LDS, Q (addition steps) and P are
   // re-read from global memory (L2 hits)
   {
@@ -357,7 +358,7 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
     // w and si re-materialised per phase: hoisted out of the loop, the wave-dependent LDS
     // slot addresses and point pointers were spilled to scratch and reloaded every step
     int wl = w, sl = si;
-    asm volatile("" : "+v"(wl), "+v"(sl));
+    asm volatile("" : "+s"(wl), "+v"(sl));
     g2p_t T;  // this wave's own slots: no other wave touches them
     T.X = mf_get2(lds, MF_T + 6 * wl);
     T.Y = mf_get2(lds, MF_T + 6 * wl + 2);
@@ -368,6 +369,7 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
     mf_put2(lds, MF_T + 6 * wl + 4, T.Z);
     const g1a_t Pk = lane_load<g1a_t>(P, (size_t)sl);
     L = line_eval(L, Pk.x, Pk.y);
+    const bool use = (use_mask >> __lane_id()) & 1u;
     mf_put2(lds, MF_LC(wl, 0), fp2_select(use, L.l00, fp2_one()));
     mf_put2(lds, MF_LC(wl, 1), fp2_select(use, L.l01, fp2_zero()));
     mf_put2(lds, MF_LC(wl, 2), fp2_select(use, L.l11, fp2_zero()));

@@ -559,3 +559,45 @@ def test_shipped_jobs_partial_bit_exact_vs_oracle(ctx, keys, n):
     want = b"".join(int(c[0]).to_bytes(48, "big") + int(c[1]).to_bytes(48, "big") for c in f12_coeffs(exp))
     assert part == want
     assert ctx.wait_jobs_node(t, 1)[0] == [(1, 0)] * n
+
+
+def test_merged_nonbatchable_group_matches_per_job(ab_ctx, keys, monkeypatch):
+    """A package's non-batchable jobs verified as one RLC group (default) and one group per job
+    (LSG_NB_MERGE=0, A/B build) give identical per-job verdicts and counters, against the
+    oracle's worker.ts:88-96 rules: a valid package takes one final exponentiation for all of
+    its non-batchable jobs; a failing merged group is localised job by job (an invalid set, a
+    one-set invalid job, an undecodable signature, an empty job, 300 sets in one job so the
+    merged group takes the bucket MSM)."""
+    ctx = ab_ctx
+    sets = single_sets(ctx, keys, b"nbmerge", 340)
+    sizes = [1, 2, 5, 300, 3, 1, 4, 8, 16]
+    def jobs_of(ss):
+        out, pos = [], 0
+        for n in sizes:
+            out.append((ss[pos:pos + n], 0))
+            pos += n
+        return out
+    valid = jobs_of(sets)
+    bad = list(sets)
+    bad[3] = bd.corrupt_wrong_message(bad[3])      # job 2 (5 sets): invalid
+    bad[311] = bd.corrupt_wrong_message(bad[311])  # job 5 (one set): invalid
+    bad[320] = bd.corrupt_truncate(bad[320])       # job 7: undecodable -> LSG_ERROR
+    mixed = jobs_of(bad) + [([], 0)] + [([s], 1) for s in sets[330:340]]
+    for jobs, exp_fe in ((valid, 1), (mixed, None)):
+        out = {}
+        for merge in ("1", "0"):
+            monkeypatch.setenv("LSG_NB_MERGE", merge)
+            got, stats = ctx.verify_jobs(jobs, seed=23)
+            out[merge] = (got, stats["batch_retries"], stats["batch_sigs_success"])
+            if merge == "1" and exp_fe is not None:
+                assert stats["n_final_exps"] == exp_fe, stats
+        assert out["1"] == out["0"]
+        flat = [s for js, _ in jobs for s in js]
+        jsets, pos = [], 0
+        for js, _ in jobs:
+            jsets.append(list(range(pos, pos + len(js))))
+            pos += len(js)
+        exp, retries, success = co.expected_jobs(jsets, [bool(f & 1) for _, f in jobs], oracle_each(flat))
+        got = out["1"][0]
+        assert [(g[0], g[1] if g[0] == 2 else 0) for g in got] == exp
+        assert out["1"][1:] == (retries, success)
