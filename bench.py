@@ -734,10 +734,11 @@ def main():
     # whole-path work per set: the per-set stages with the bucket-MSM signature sum (groups of
     # >= 256 sets) plus the package group's share of its per-group stages, plus one G1
     # addition per extra signer of an aggregate set
-    # the RLC group a set is verified in: the package group; a block; a coalesced launch's
-    # 16-job chunks; a lone set
-    group = n_sets if args.workload in ("jobs", "adversarial", "committees") else \
-        (128 if args.workload == "block" else (16 if args.coalesce else 1))
+    # the RLC group a set is verified in: the package group (block bodies: the package's
+    # non-batchable jobs as one merged group, lsg_host.hip nb_merge_on); a coalesced launch's
+    # sub-package; a lone set
+    group = n_sets if args.workload in ("jobs", "adversarial", "committees", "block") else \
+        (n_sets if args.coalesce else 1)
     if group >= 256:  # bucket MSM, 8-bit windows (lsg_host.hip plan_phase, msm_window_bits)
         per_set_muls = opc["batched_single_set_msm_fp_muls"] + opc["per_batch_msm_fp_muls"] / group
     elif group >= 48:  # 4-bit windows
