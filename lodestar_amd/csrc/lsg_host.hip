@@ -92,6 +92,16 @@ bool os_random(void* buf, size_t len) {
 
 std::atomic<uint64_t> g_allocs{0};  // device + pinned allocations made (lsg_allocation_count)
 
+// env LSG_TRACE_HOST=1: one stderr line per phase-A submission with its host time per stage
+// (staging, planning, per-set launches, group launches), to find host-bound workloads
+bool trace_host() {
+  static const bool on = [] {
+    const char* e = getenv("LSG_TRACE_HOST");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // env LSG_TRACE_ALLOC=1: one stderr line per allocation (size and caller), for steady-state checks
 void trace_alloc(const char* kind, size_t bytes) {
   const char* e = getenv("LSG_TRACE_ALLOC");  // read per allocation: allocations are rare
@@ -954,7 +964,10 @@ int batch_inv(Slot* s, int ws, const char* name, const uint32_t* v, size_t n, ui
   uint32_t* lv = P_<uint32_t>(s->binv_lv[ws]);
   uint32_t* iv = P_<uint32_t>(s->binv_iv[ws]);
   if (binv_block_on()) {  // one launch: a divstep root per block of 128 x T values
-    const int T = (int)std::max<size_t>(1, (n + 128 * 1024 - 1) / (128 * 1024));  // >= 1024 blocks before T grows
+    // ~64 blocks: each holds its CU slot through one ~30 us divstep root (and the heap's
+    // barriers), so fewer, longer blocks cost the loaded GPU less than one block per 128 values
+    // (7 % of summed kernel time with T = 1, profiles/r05_rocprof_stats_a.csv)
+    const int T = (int)std::min<size_t>(64, std::max<size_t>(1, (n + 128 * 64 - 1) / (128 * 64)));
     KL(s, name, lsgk::binv_block(S_(s), (int)n, T, 1, v, lv, out));
     return LSG_OK;
   }
@@ -1828,7 +1841,9 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
   const bool nb_merge = nb_merge_on() && nb_live >= 2 && !subs && package_group_mode();
   for (size_t k : nonb)
     if (s->jobs[k].count == 1 && !nb_merge) noscale[s->jobs[k].first] = 1;
+  const uint64_t th0 = trace_host() ? now_ns() : 0;
   LSG_RC(stage_sets(s, flat.data(), flat.size(), seed, true, &noscale, true));
+  const uint64_t th1 = trace_host() ? now_ns() : 0;
   // phase-A groups, MSM groups first: the package group, then one per non-batchable job
   PhasePlan& A = s->phA;
   A = PhasePlan();
@@ -1987,7 +2002,9 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     node = plan_seg(s->plan, 2, off, len, false, 0, 0);
   }
   LSG_RC(upload_plan(s));
+  const uint64_t th2 = trace_host() ? now_ns() : 0;
   LSG_RC(launch_set_stages(s, &s->pkagg, A, P_<uint32_t>(s->d_fall)));
+  const uint64_t th3 = trace_host() ? now_ns() : 0;
   // signature points: unscaled for MSM groups, [r_i] sig_i for the rest
   s->rs_raw.assign(s->n_sets, 0);
   for (size_t g = 0; g < A.n_msm; g++) memset(s->rs_raw.data() + A.groups[g].first, 1, A.groups[g].len);
@@ -2009,6 +2026,12 @@ int pkg_part1(Slot* s, const lsg_job* jobs, const std::vector<size_t>& ids, uint
     LSG_HIP(s, hipEventRecord(s->ev_part, s->st[0]));
   }
   s->phA_node = node;
+  if (trace_host()) {
+    const uint64_t th4 = now_ns();
+    fprintf(stderr, "lsg host: sets %zu jobs %zu subs %d groups %zu | stage %.3f plan %.3f set-launch %.3f group-launch %.3f ms\n",
+            (size_t)s->n_sets, nj, s->n_sub, A.groups.size(), (th1 - th0) * 1e-6, (th2 - th1) * 1e-6, (th3 - th2) * 1e-6,
+            (th4 - th3) * 1e-6);
+  }
   return LSG_OK;
 }
 
@@ -2748,9 +2771,14 @@ PendingPkg copy_pkg(const lsg_job* jobs, size_t n_jobs, uint64_t seed) {
   return pk;
 }
 
+// launches still executing on the device (their completion event not reached): a launch
+// whose work is done no longer holds packages back, whether or not its tickets were waited on
 int launches_in_flight(lsg_ctx* c) {
   int n = 0;
-  for (int i = 0; i < LSG_SLOTS; i++) n += c->dev[0]->slots[i].kind == SLOT_JOBS ? 1 : 0;
+  for (int i = 0; i < LSG_SLOTS; i++) {
+    const Slot& s = c->dev[0]->slots[i];
+    n += s.kind == SLOT_JOBS && hipEventQuery(s.ev_done) == hipErrorNotReady ? 1 : 0;
+  }
   return n;
 }
 
@@ -2838,18 +2866,33 @@ int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* st
   const uint64_t serial = t >> 16;
   int p, k;
   hipEvent_t ev;
-  {
-    std::lock_guard<std::mutex> lk(c->mu);
+  for (int spin = 0;; spin++) {
+    std::unique_lock<std::mutex> lk(c->mu);
     LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
     auto it = c->merged.find(serial);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
-    int frc = LSG_OK;
-    if (it->second.slot < 0 && !it->second.rc) frc = flush_pending(c);  // the waiter wants it now
+    if (it->second.slot >= 0 || it->second.rc) break;  // launched (or its launch failed)
+    // still held: it goes out with whatever else is pending once fewer than co_inflight launches
+    // execute -- packages submitted meanwhile join it (a waiter forcing the flush at once left
+    // two packages per launch on the gossip bench) -- or at once if the device is idle
+    if (launches_in_flight(c) >= c->co_inflight) {
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::microseconds(spin < 20 ? 50 : 200));
+      continue;
+    }
+    const int frc = flush_pending(c);
     it = c->merged.find(serial);
     if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
     // still held (every slot busy: LSG_ERR_BUSY, c->err says so): the ticket stays live and a
     // later wait -- after the caller has waited on another ticket -- launches it
     if (frc && it->second.slot < 0 && !it->second.rc) return frc;
+    break;
+  }
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
+    auto it = c->merged.find(serial);
+    if (it == c->merged.end()) return LSG_ERR_INVALID_ARG;
     if (it->second.rc) {  // its coalesced launch failed
       const int frc = it->second.rc;
       c->err = it->second.err;
