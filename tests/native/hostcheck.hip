@@ -418,3 +418,24 @@ void hc_inv_gcd(const uint8_t* a48, uint8_t* out48) {
 }
 }
 #endif
+
+#ifdef LSG_HOSTCHECK_PAIR
+extern "C" {
+// the Fp2 product leaf on raw lazy limbs (14 signed words per component, the pair layout with
+// all limbs in one lane): a0, a1, b0, b1 in, (c0, c1) out -- for tests at the lazy bounds
+void hc_pair_fp2_mul_raw(const int32_t* a, const int32_t* b, int32_t* out) {
+  fp_t a0, a1, b0, b1, c0, c1;
+  for (int k = 0; k < 14; k++) {
+    a0.l[k] = (uint32_t)a[k];
+    a1.l[k] = (uint32_t)a[14 + k];
+    b0.l[k] = (uint32_t)b[k];
+    b1.l[k] = (uint32_t)b[14 + k];
+  }
+  pair_fp2_mul_sop(c0, c1, a0, a1, b0, b1);
+  for (int k = 0; k < 14; k++) {
+    out[k] = (int32_t)c0.l[k];
+    out[14 + k] = (int32_t)c1.l[k];
+  }
+}
+}
+#endif

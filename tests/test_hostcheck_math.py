@@ -398,3 +398,48 @@ def test_inv_gcd_matches_pow(hc):
     for x in vals:
         hc.hc_inv_gcd(be(x), o)
         assert int.from_bytes(o.raw, "big") == (pow(x, -1, P) if x else 0), x
+
+
+def _limbs_value(limbs):
+    return sum(int(v) << (29 * k) for k, v in enumerate(limbs))
+
+
+def test_fp2_sop_bound_limits(hc):
+    """The Fp2 product as two sums of products (lsg_fp_pair.hpp pair_fp2_mul_sop) at the lazy
+    bounds of its inputs: limbs at the edges of [-8, 2^29 + 8), signed top limbs with
+    |v| < 2^12.6 p, against the exact integers: out = (a0 b0 - a1 b1, a0 b1 + a1 b0) / R mod p,
+    |out| < 3p, limbs 0..12 normalised.  (Host build: one lane holds every column for 14 steps
+    and carries at mid-loop; on gfx950 a column lives 7 steps per lane)"""
+    if hc.backend != "pair":
+        pytest.skip("pair backend only")
+    import itertools
+    R = 1 << 406
+    Rinv = pow(R, -1, P)
+    top_max = (int(2 ** 12.6 * P) >> (29 * 13))  # the largest top limb of a value < 2^12.6 p
+    lo_hi, lo_lo = (1 << 29) + 7, -8
+    bound = int(2 ** 12.6 * P)
+
+    def clamp(limbs):  # the top limb's magnitude lowered until |value| < 2^12.6 p
+        while abs(_limbs_value(limbs)) >= bound:
+            limbs[13] += -1 if limbs[13] > 0 else 1
+        return limbs
+    patterns = []
+    for lo, top in itertools.product((lo_hi, lo_lo, 0, (1 << 29) - 1), (top_max, -top_max, 0, 1)):
+        patterns.append(clamp([lo] * 13 + [top]))
+    r = random.Random(77)
+    for _ in range(40):  # random limbs anywhere in the lazy range
+        patterns.append(clamp([r.randrange(-8, (1 << 29) + 8) for _ in range(13)] + [r.randrange(-top_max, top_max + 1)]))
+    I32 = ctypes.c_int32 * 28
+    for k in range(len(patterns) * 2):
+        a0, a1 = patterns[k % len(patterns)], patterns[(3 * k + 1) % len(patterns)]
+        b0, b1 = patterns[(5 * k + 2) % len(patterns)], patterns[(7 * k + 3) % len(patterns)]
+        va0, va1, vb0, vb1 = map(_limbs_value, (a0, a1, b0, b1))
+        assert max(abs(v) for v in (va0, va1, vb0, vb1)) < 2 ** 12.6 * P
+        out = I32()
+        hc.hc_pair_fp2_mul_raw(I32(*(a0 + a1)), I32(*(b0 + b1)), out)
+        c0, c1 = list(out[:14]), list(out[14:])
+        v0, v1 = _limbs_value(c0), _limbs_value(c1)
+        assert (v0 - (va0 * vb0 - va1 * vb1) * Rinv) % P == 0
+        assert (v1 - (va0 * vb1 + va1 * vb0) * Rinv) % P == 0
+        assert abs(v0) < 3 * P and abs(v1) < 3 * P
+        assert all(0 <= c < (1 << 29) for c in c0[:13] + c1[:13])
