@@ -421,7 +421,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
 
     from lodestar_amd._native import Context, PreparedJobs
-    NODE_LAG = 2  # multi-rank: node verdicts awaited this many exchanges late (run())
+    # multi-rank: node verdicts awaited this many exchanges late (run()); the threaded loop lets
+    # NODE_LAG more packages than --depth wait for their node verdicts
+    NODE_LAG = int(os.environ.get("LSG_BENCH_NODE_LAG", "2"))
     # packages whose per-kernel HIP-event times are read back in the timed region (the
     # reading costs host time: a sample, not every package of a 640-step small-package run)
     KT_SAMPLE = 30

@@ -331,6 +331,7 @@ struct Slot {
   // flight (verifyOnMainThread's latency under load)
   hipStream_t st_norm[2] = {nullptr, nullptr}, st_prio[2] = {nullptr, nullptr};
   int cur = 0;
+  hipEvent_t ev_xp = nullptr;  // the exported partial's copy is complete (lsg_jobs_partial*)
   hipEvent_t ev_in = nullptr, ev_sig = nullptr, ev_grp = nullptr, ev_part = nullptr, ev_done = nullptr,
              ev_node = nullptr;
   // inputs (device copies of the pinned staging arena)
@@ -627,7 +628,7 @@ int slot_create(Dev* d, Slot* s, int index, hipStream_t shared) {
     s->st[0] = s->st_norm[0];
     s->st[1] = s->st_norm[1];
   }
-  hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_part, &s->ev_done, &s->ev_node};
+  hipEvent_t* evs[] = {&s->ev_in, &s->ev_sig, &s->ev_grp, &s->ev_part, &s->ev_done, &s->ev_node, &s->ev_xp};
   for (hipEvent_t* e : evs) LSG_HIP(s, hipEventCreateWithFlags(e, hipEventDisableTiming));
   if (blocking_waits()) {  // the events a waiter blocks on: sleep instead of spinning
     for (hipEvent_t* e : {&s->ev_part, &s->ev_done}) {
@@ -665,7 +666,7 @@ void slot_destroy(Slot* s) {
     (void)hipEventDestroy(t.b);
   }
   s->timers.clear();
-  hipEvent_t evs[] = {s->ev_in, s->ev_sig, s->ev_grp, s->ev_part, s->ev_done, s->ev_node};
+  hipEvent_t evs[] = {s->ev_in, s->ev_sig, s->ev_grp, s->ev_part, s->ev_done, s->ev_node, s->ev_xp};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
   if (s->own_streams) {
@@ -3346,24 +3347,33 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
     return LSG_ERR_INVALID_ARG;
   }
   if (int prc = presync_pkg(c, ticket, true)) return prc;
-  LSG_ENTER(c);
-  const int p = ticket_pkg(c, ticket);
-  if (p < 0) return LSG_ERR_INVALID_ARG;
-  Slot* s = &c->dev[0]->slots[p];
-  const bool has = !s->phA.groups.empty() && s->big_g >= 0;
-  // the copy goes out on a high-priority stream (the node final exponentiations'): on the
-  // package's own stream it would queue behind other packages' kernels sharing its hardware
-  // queue, and the node's next verdicts wait on it (ev_part is complete: presync_pkg)
-  LSG_RC(prio_stream(c, c->dev[0], &c->dev[0]->s_xp));
-  hipStream_t xs = c->dev[0]->s_xp;
-  if (has) {
-    const uint8_t* src;
-    LSG_RC(export_partial_dev(s, &src, xs));  // f^r (a lone unscaled set) runs on xs too
-    LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, xs));
-  } else {
-    LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, xs));
+  hipEvent_t xev;
+  bool has;
+  {
+    LSG_ENTER(c);
+    const int p = ticket_pkg(c, ticket);
+    if (p < 0) return LSG_ERR_INVALID_ARG;
+    Slot* s = &c->dev[0]->slots[p];
+    has = !s->phA.groups.empty() && s->big_g >= 0;
+    // the copy goes out on a high-priority stream (the node final exponentiations'): on the
+    // package's own stream it would queue behind other packages' kernels sharing its hardware
+    // queue, and the node's next verdicts wait on it (ev_part is complete: presync_pkg)
+    LSG_RC(prio_stream(c, c->dev[0], &c->dev[0]->s_xp));
+    hipStream_t xs = c->dev[0]->s_xp;
+    if (has) {
+      const uint8_t* src;
+      LSG_RC(export_partial_dev(s, &src, xs));  // f^r (a lone unscaled set) runs on xs too
+      LSG_HIP(s, hipMemcpyAsync(dev_out576, src, 576, hipMemcpyDeviceToDevice, xs));
+    } else {
+      LSG_HIP(s, hipMemcpyAsync(dev_out576, fp12_one_blob(), 576, hipMemcpyHostToDevice, xs));
+    }
+    LSG_HIP(s, hipEventRecord(s->ev_xp, xs));
+    xev = s->ev_xp;  // (the slot stays this ticket's until it is waited on)
   }
-  LSG_HIP(s, hipStreamSynchronize(xs));
+  // the copy completes without the context lock held: submissions and resolutions of other
+  // packages go on meanwhile
+  (void)hipSetDevice(c->dev[0]->device);
+  if (hipError_t e = event_wait(xev)) return fail_c(c, "hipEventSynchronize", e);
   if (has_batch) *has_batch = has ? 1 : 0;
   return LSG_OK;
 }

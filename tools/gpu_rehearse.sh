@@ -25,4 +25,5 @@ plain() {
 plain
 one rank1 1
 for extra in ${REH_EXTRA:-}; do one "rank1_$extra" 1 --depth "$extra"; done
+for lag in ${REH_LAG:-}; do LSG_BENCH_NODE_LAG=$lag one "rank1_lag$lag" 1; done
 echo "== all ok"
