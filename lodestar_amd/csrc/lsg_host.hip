@@ -2119,6 +2119,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
                        const std::vector<std::pair<int32_t, int32_t>>* given, std::vector<int32_t>& v) {
   v.assign(groups.size(), 0);
   if (groups.empty()) return LSG_OK;
+  const uint64_t tf0 = trace_host() ? now_ns() : 0;
   // Signature sums: a group whose sets' unscaled points are resident (they were in a phase-A
   // bucket-MSM group: d_rs) and that is large enough sums them by its own bucket MSM (no
   // per-set scaling); the others sum [r_i] sig_i (d_rs2, scaled below).  MSM groups go first
@@ -2199,6 +2200,7 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
   LSG_RC(launch_phase(s, Ph, P_<uint32_t>(s->d_rs2), fall, false, P_<uint32_t>(s->d_rs)));
   LSG_RC(launch_fe(s, groups.size()));
   LSG_RC(launch_readback(s, false));
+  const uint64_t tf1 = trace_host() ? now_ns() : 0;
   const int dev = s->d->device;
   if (lk) lk->unlock();
   hipError_t e = event_wait(s->ev_done);
@@ -2207,6 +2209,9 @@ int run_fallback_phase(Slot* s, CtxLock* lk, const std::vector<Grp>& groups,
     (void)hipSetDevice(dev);
   }
   if (e != hipSuccess) return fail(s, "hipEventSynchronize", e);
+  if (trace_host())
+    fprintf(stderr, "lsg host: fallback groups %zu (msm %zu) given %d | plan+launch %.3f ms, device+lock %.3f ms\n",
+            groups.size(), n_msm, given ? 1 : 0, (tf1 - tf0) * 1e-6, (now_ns() - tf1) * 1e-6);
   s->stats.n_final_exps += (uint32_t)groups.size();
   for (size_t k = 0; k < order.size(); k++) v[order[k]] = H_<int32_t>(s->h_verdict)[k];
   return LSG_OK;
