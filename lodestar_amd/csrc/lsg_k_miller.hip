@@ -190,7 +190,10 @@ LSG_DEVI void mf_sqr(uint32_t* lds, int w) {
   } else {  // c0.c2 = u2 - t2 - t1
     o0 = fp2_sub(fp2_sub(fin(6, 2), fin(0, 2)), fin(0, 1));
   }
-  __syncthreads();  // every wave has read the products it needs before f is overwritten
+  // No barrier before or after the writes: f was last read in the product half (before the
+  // barrier above) and the combination reads only the products; the next reader of f (the M
+  // phase) and the next writer of the product slots (the P phase) both come after the L
+  // phase's barrier.  (Round 4 kept two more barriers here.)
   if (w == 0) {
     mf_put2(lds, MF_FC(3), fp2_add(o0, o0));
     mf_put2(lds, MF_FC(4), fp2_add(o1, o1));
@@ -198,7 +201,6 @@ LSG_DEVI void mf_sqr(uint32_t* lds, int w) {
   } else {
     mf_put2(lds, MF_FC(w - 1), o0);
   }
-  __syncthreads();
 }
 
 // P phase: M01 = l0 l1 into the slots of lines 0 and 1, M23 = l2 l3 into those of 2 and 3.
