@@ -68,12 +68,29 @@ LSG_DEVI void shal_final(ShaLds& c, uint32_t* out8) {
   for (int i = 0; i < 8; i++) out8[i] = c.st[i];
 }
 
+// append len bytes from src (global memory or LDS): the loads of 16 bytes are issued before
+// the first append, so a lone message pays one memory round trip per 16 bytes, not per byte
+LSG_DEVI void shal_bytes(ShaLds& c, const uint8_t* src, uint32_t len) {
+  uint32_t k = 0;
+  for (; k + 16 <= len; k += 16) {
+    uint8_t b[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) b[j] = src[k + j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) shal_byte(c, b[j]);
+  }
+  for (; k < len; k++) shal_byte(c, src[k]);
+}
+
 __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restrict__ msg,
                                                     const uint32_t* __restrict__ msg_off,
                                                     const uint32_t* __restrict__ msg_len,
                                                     const uint8_t* __restrict__ dst, uint32_t dst_len,
                                                     uint8_t* __restrict__ ub) {
   __shared__ uint32_t lds[16 * 64];
+  __shared__ uint8_t s_dst[256];  // the DST (< 256 bytes, RFC 9380), appended nine times
+  for (uint32_t k = threadIdx.x; k < dst_len; k += 64) s_dst[k] = dst[k];
+  __syncthreads();
   const size_t i = gtid();
   if (i >= (size_t)n) return;
   ShaLds c;
@@ -88,11 +105,11 @@ __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restr
   }
   const uint8_t* m = msg + msg_off[i];
   const uint32_t ml = msg_len[i];
-  for (uint32_t k = 0; k < ml; k++) shal_byte(c, m[k]);
+  shal_bytes(c, m, ml);
   shal_byte(c, 1);  // l_i_b_str = 256 (2 bytes, big endian)
   shal_byte(c, 0);
   shal_byte(c, 0);  // I2OSP(0, 1)
-  for (uint32_t k = 0; k < dst_len; k++) shal_byte(c, dst[k]);
+  shal_bytes(c, s_dst, dst_len);
   shal_byte(c, (uint8_t)dst_len);
   uint32_t b0[8], bi[8];
   shal_final(c, b0);
@@ -102,7 +119,7 @@ __global__ void __launch_bounds__(64) k_expand_msg(int n, const uint8_t* __restr
 #pragma unroll
     for (int k = 0; k < 8; k++) shal_word(c, r == 1 ? b0[k] : (b0[k] ^ bi[k]));
     shal_byte(c, (uint8_t)r);
-    for (uint32_t k = 0; k < dst_len; k++) shal_byte(c, dst[k]);
+    shal_bytes(c, s_dst, dst_len);
     shal_byte(c, (uint8_t)dst_len);
     shal_final(c, bi);
 #pragma unroll

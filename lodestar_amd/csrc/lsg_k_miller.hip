@@ -329,6 +329,72 @@ LSG_DEVI void mf_mul_pair(uint32_t* lds, int w, int k) {
   __syncthreads();
 }
 
+// L phase steps with their values staged through LDS: ml_dbl_step_raw / ml_add_step_raw +
+// line_eval (lsg_pairing.hpp), the same formulas in the same order, but each line
+// coefficient is evaluated at P and written to its slot as soon as it exists, and T's
+// coordinates go back to their slots as soon as they are final.  Computed first and written
+// last (the generic step), the line's three Fp2 values were live across the remaining point
+// products and went to scratch (176 B per lane).
+#ifndef LSG_MF_STAGED
+#define LSG_MF_STAGED 1
+#endif
+LSG_DEVI void mf_put_line(uint32_t* lds, int wl, bool use, const fp2_t& l00, const fp2_t& l01P, const fp2_t& l11P) {
+  mf_put2(lds, MF_LC(wl, 0), fp2_select(use, l00, fp2_one()));
+  mf_put2(lds, MF_LC(wl, 1), fp2_select(use, l01P, fp2_zero()));
+  mf_put2(lds, MF_LC(wl, 2), fp2_select(use, l11P, fp2_zero()));
+}
+LSG_DEVI void mf_dbl_line(uint32_t* lds, int wl, bool use, const uint32_t* __restrict__ P, size_t sl) {
+  const int tb = MF_T + 6 * wl;
+  fp2_t t0, t1, t2, v1;
+  {
+    const fp2_t X = mf_get2(lds, tb), Y = mf_get2(lds, tb + 2), Z = mf_get2(lds, tb + 4);
+    t0 = fp2_sqr(Y);
+    t1 = fp2_mul(Y, Z);
+    t2 = fp2_mul_b3(fp2_sqr(Z));
+    const fp2_t XX = fp2_sqr(X);
+    v1 = fp2_mul(X, Y);
+    const g1a_t Pk = lane_load<g1a_t>(P, sl);
+    mf_put_line(lds, wl, use, fp2_sub(t2, t0), fp2_mul_fp(fp2_add(fp2_add(XX, XX), XX), Pk.x),
+                fp2_mul_fp(fp2_neg(fp2_add(t1, t1)), Pk.y));
+  }
+  fp2_t Z3 = fp2_add(t0, t0);
+  Z3 = fp2_add(Z3, Z3);
+  Z3 = fp2_add(Z3, Z3);
+  fp2_t X3 = fp2_mul(t2, Z3);
+  fp2_t Y3 = fp2_add(t0, t2);
+  mf_put2(lds, tb + 4, fp2_mul(t1, Z3));
+  const fp2_t u2 = fp2_add(fp2_add(t2, t2), t2);
+  const fp2_t s0 = fp2_sub(t0, u2);
+  Y3 = fp2_mul(s0, Y3);
+  mf_put2(lds, tb + 2, fp2_add(X3, Y3));
+  X3 = fp2_mul(s0, v1);
+  mf_put2(lds, tb, fp2_add(X3, X3));
+}
+LSG_DEVI void mf_add_line(uint32_t* lds, int wl, bool use, const uint32_t* __restrict__ P, const uint32_t* __restrict__ H,
+                          size_t sl) {
+  const int tb = MF_T + 6 * wl;
+  fp2_t theta, delta;
+  {
+    const g2a_t Q = lane_load<g2a_t>(H, sl);
+    const fp2_t Z = mf_get2(lds, tb + 4);
+    theta = fp2_sub(mf_get2(lds, tb + 2), fp2_mul(Q.y, Z));
+    delta = fp2_sub(mf_get2(lds, tb), fp2_mul(Q.x, Z));
+    const fp2_t l00 = fp2_sub(fp2_mul(delta, Q.y), fp2_mul(theta, Q.x));
+    const g1a_t Pk = lane_load<g1a_t>(P, sl);
+    mf_put_line(lds, wl, use, l00, fp2_mul_fp(theta, Pk.x), fp2_mul_fp(fp2_neg(delta), Pk.y));
+  }
+  const fp2_t C = fp2_sqr(theta);
+  const fp2_t D = fp2_sqr(delta);
+  const fp2_t E = fp2_mul(D, delta);
+  const fp2_t F = fp2_mul(mf_get2(lds, tb + 4), C);
+  const fp2_t G = fp2_mul(mf_get2(lds, tb), D);
+  const fp2_t Hs = fp2_sub(fp2_add(E, F), fp2_add(G, G));
+  mf_put2(lds, tb, fp2_mul(delta, Hs));
+  const fp2_t Y3 = fp2_sub(fp2_mul(theta, fp2_sub(G, Hs)), fp2_mul(E, mf_get2(lds, tb + 2)));
+  mf_put2(lds, tb + 2, Y3);
+  mf_put2(lds, tb + 4, fp2_mul(E, mf_get2(lds, tb + 4)));
+}
+
 #ifndef LSG_MF_WAVES
 #define LSG_MF_WAVES 2  // waves per SIMD the register budget is sized for (256 VGPR + AGPR)
 #endif
@@ -361,6 +427,13 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
     // slot addresses and point pointers were spilled to scratch and reloaded every step
     int wl = w, sl = si;
     asm volatile("" : "+s"(wl), "+v"(sl));
+#if LSG_MF_STAGED
+    const bool use = (use_mask >> __lane_id()) & 1u;
+    if (add)
+      mf_add_line(lds, wl, use, P, H, (size_t)sl);
+    else
+      mf_dbl_line(lds, wl, use, P, (size_t)sl);
+#else
     g2p_t T;  // this wave's own slots: no other wave touches them
     T.X = mf_get2(lds, MF_T + 6 * wl);
     T.Y = mf_get2(lds, MF_T + 6 * wl + 2);
@@ -375,6 +448,7 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
     mf_put2(lds, MF_LC(wl, 0), fp2_select(use, L.l00, fp2_one()));
     mf_put2(lds, MF_LC(wl, 1), fp2_select(use, L.l01, fp2_zero()));
     mf_put2(lds, MF_LC(wl, 2), fp2_select(use, L.l11, fp2_zero()));
+#endif
     __syncthreads();
     mf_pair_lines(lds, wl);
 #pragma unroll 1

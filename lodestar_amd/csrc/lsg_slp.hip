@@ -32,6 +32,9 @@ constexpr size_t lsgl_w_g1a = lsgl::W_G1A / 2, lsgl_w_g2a = lsgl::W_G2A / 2, lsg
 
 namespace {
 
+// s_waitcnt vmcnt(0) with expcnt and lgkmcnt left at their maxima (gfx9 encoding)
+#define LSG_WAIT_VMCNT0 0x0F70
+
 enum { SLP_FE = 0, SLP_ML = 1, SLP_HORNER = 2, SLP_ITEM1 = 3, SLP_H2C_CLEAR = 4, SLP_G2_SUBGROUP = 5, SLP_G2_SCALE = 6 };
 
 template <int PROG, int W>
@@ -74,6 +77,10 @@ __device__ __forceinline__ void slp_steps(uint32_t* lds, const uint8_t* inp, uin
     e0 = e[0];
     e1 = e[1];
   }
+  // the first entry is complete before the loop: otherwise the wait-count pass merges the
+  // loop header's two predecessors and makes every step wait for its own prefetch of the
+  // next entry (vmcnt(0) at the top of the step), exposing one L2 round trip per step
+  __builtin_amdgcn_s_waitcnt(LSG_WAIT_VMCNT0);
 #pragma unroll 1
   for (int s = 0; s < PR::n_steps; s++) {
     const uint32_t dn = steps[s + 1];  // (a zero sentinel follows the last step)
