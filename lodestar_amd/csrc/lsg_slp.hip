@@ -353,10 +353,16 @@ hipError_t launch(hipStream_t st, int n, const uint8_t* in, uint32_t in_stride, 
 
 }  // namespace
 
-// Two waves per item (steps of 64 operations, each wave on its own SIMD) while the items fit
-// the chip one wave per SIMD; one wave per item beyond (a fallback phase's thousands of
-// groups: throughput).
-static int slp_waves(int n) { return n <= 512 ? 2 : 1; }
+// Two waves per item (steps of 64 operations, each wave on its own SIMD) for up to 128 items
+// (latency: a lone set, a few groups); one wave per item beyond, where the launch shares the
+// chip with other packages and throughput counts: a one-wave step fills 32 lane pairs with ~32
+// of the ~39 operations a two-wave step spreads over 64 (final exponentiation: 771 one-wave
+// steps against 630 two-wave steps, 39 % fewer wave-steps).  128 against 512:
+// profiles/r05_slp_w2max_ab.txt (gossip +4 %, block bodies +1.4 %, adversarial +1 %).
+#ifndef LSG_SLP_W2_MAX
+#define LSG_SLP_W2_MAX 128
+#endif
+static int slp_waves(int n) { return n <= LSG_SLP_W2_MAX ? 2 : 1; }
 hipError_t lsg_slp_final_exp(hipStream_t st, int ng, const uint8_t* F576, int32_t* verdict) {
   return slp_waves(ng) == 2 ? launch<SLP_FE, 2, 0>(st, ng, F576, 576, nullptr, verdict)
                             : launch<SLP_FE, 1, 0>(st, ng, F576, 576, nullptr, verdict);
