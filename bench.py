@@ -48,9 +48,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Hardware queues: the library sets GPU_MAX_HW_QUEUES itself (LSG_HW_QUEUES, default 16) before
 # its first HIP call (lsg_init_devices, as in a Node process).  One GPU: nothing is set here,
-# so the run measures the library's own setting.  Several ranks: torch initialises HIP before
-# the library, so the same value is set here first.
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+# so the run measures the library's own setting.  Several ranks, and the one-rank rehearsal of
+# the node protocol: torch initialises HIP before the library, so the same value is set here
+# first (without it the rehearsal ran at the box's 4 queues against the plain run's 16).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("LSG_BENCH_REHEARSE") == "1":
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LSG_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
