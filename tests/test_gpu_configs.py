@@ -234,6 +234,28 @@ def test_thrown_chunk_localises_its_live_jobs(ctx, keys):
     check_against_oracle(ctx, jobs, per)
 
 
+def test_phase_b0_runs_localise_like_chunks(ctx, keys):
+    """Phase B0 (lsg_host.hip pkg_resolve): a failing package of 2048 single-set jobs (128
+    chunks of 16) is first checked as 32 runs of four chunks; only the chunks of a failing run
+    are checked on their own.  An invalid set in chunk 5, an undecodable one in chunk 9 (its run
+    passes: the thrown set is the identity, as in the chunk's own group) and an invalid set at
+    the end of chunk 63 (the last chunk of run 15): per-job verdicts and batch counters equal
+    the oracle's worker.ts rules (multithread/worker.ts:51-96), with fewer final
+    exponentiations than the 1 + 128 chunk checks alone would take."""
+    n = 2048
+    s = list(single_sets(ctx, keys, b"b0runs", n))
+    touched = (5 * 16 + 3, 9 * 16 + 7, 63 * 16 + 15)
+    s[touched[0]] = bd.corrupt_wrong_message(s[touched[0]])
+    s[touched[1]] = bd.corrupt_truncate(s[touched[1]])
+    s[touched[2]] = bd.corrupt_wrong_message(s[touched[2]])
+    per = [1] * n
+    for i, v in zip(touched, oracle_each([s[i] for i in touched])):
+        per[i] = v
+    assert per[touched[0]] == 0 and per[touched[1]] < 0 and per[touched[2]] == 0
+    _, stats = check_against_oracle(ctx, [([x], 1) for x in s], per)
+    assert stats["n_final_exps"] < 1 + 128, stats
+
+
 def test_package_group_matches_chunk_mode(ab_ctx, keys, monkeypatch):
     """The one-group phase A (default) and the reference's chunk-16 phase A
     (LSG_PACKAGE_GROUP=0, A/B build) give identical per-job verdicts AND batch_retries /
