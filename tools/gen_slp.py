@@ -57,6 +57,18 @@ MAX_SLOTS = 1 << SLOT_BITS
 W_LAT = {"mul": 1.0, "loadmul": 1.0, "lin": 0.25, "inv": 20.0}  # step costs relative to one product
 COMBINE_TERMS = int(os.environ.get("LSG_SLP_COMBINE", "12"))  # a form built by +/- keeps up to this many terms
 COMBINE_KEEP = int(os.environ.get("LSG_SLP_KEEP", "7"))  # ... and is cut back to this many
+# Per program: the Miller-loop programs keep wider forms before cutting them back (their
+# line and point formulas then collapse fewer fresh terms into LIN chains on the critical
+# path: two-wave steps 330 -> 270 for a Miller item, 331 -> 273 for ML(-G1), 709 -> 651 for
+# Horner + ML); the final exponentiation's Granger-Scott chain is shortest at 12 (630 steps;
+# 643 at 14, 663 at 20, 1059 at 28).
+COMBINE_BY_PROGRAM = {"miller_neg_g1": 28, "horner_miller": 28, "miller_item1": 28}
+SPLIT_COLLAPSE = os.environ.get("LSG_SLP_SPLIT", "1") == "1"
+
+
+def _n_enc(items):
+    """encoded terms of a LIN over items (a coefficient outside [-32, 31] repeats its term)"""
+    return sum(-(-c // COEF_MAX) if c > 0 else -(c // -COEF_MIN) for _, c in items)
 
 
 # ----------------------------------------------------------------------------- engines
@@ -152,6 +164,7 @@ class Ctx:
         self.n_inputs = n_inputs
         self.load_inputs = load_inputs
         self.one = self._raw_const(R % P)  # Montgomery one (taming)
+        self.combine = COMBINE_TERMS if "LSG_SLP_COMBINE" in os.environ else COMBINE_BY_PROGRAM.get(name, COMBINE_TERMS)
 
     def _new(self, bound, prod, est=0.0):
         self.bound.append(bound)
@@ -261,12 +274,36 @@ class Ctx:
             tame = b_rest + b_old > max_bound or b_old > LIN_MAX
             if m == 1 and not tame and enc(old):
                 continue
+            if not tame and SPLIT_COLLAPSE and _n_enc(old) > 2 * MAX_TERMS:
+                split = self._split_collapse(items, m, max_terms, max_bound)
+                if split is not None:
+                    return split
             return [(self.mat_terms(old, tame), 1)] + rest
         return [(self.mat_terms(items, True), 1)]
 
+    def _split_collapse(self, items, m0, max_terms, max_bound):
+        """the oldest terms as several LIN values of <= 14 encoded terms each, computed side by
+        side, where one value would need a chain (a LIN of 14 terms, then a LIN over it and the
+        rest): the consumer takes the partial sums as separate terms.  None if no split fits."""
+        for m in range(m0, len(items) + 1):
+            old, rest = items[:m], items[m:]
+            chunks, cur = [], []
+            for it in old:
+                if cur and _n_enc(cur + [it]) > 2 * MAX_TERMS:
+                    chunks.append(cur)
+                    cur = []
+                cur.append(it)
+            chunks.append(cur)
+            if len(rest) + len(chunks) > max_terms:
+                continue
+            if self._fbound(rest) + self._fbound(old) > max_bound or self._fbound(old) > LIN_MAX:
+                return None
+            return [(self.mat_terms(ch, False), 1) for ch in chunks] + rest
+        return None
+
     def shape(self, t):
         """keep a combined form within the working size"""
-        if len(t) <= COMBINE_TERMS and self._fbound(t.items()) <= LIN_MAX // 64:
+        if len(t) <= self.combine and self._fbound(t.items()) <= LIN_MAX // 64:
             return t
         return dict(self.fit(t, COMBINE_KEEP, LIN_MAX // 64))
 
