@@ -299,6 +299,7 @@ namespace lsgk {
 hipError_t expand_msg(hipStream_t st, int n, const uint8_t* msg, const uint32_t* off, const uint32_t* len,
                       const uint8_t* dst, uint32_t dst_len, uint8_t* ub) {
   if (n <= 0) return hipSuccess;
+  if (dst_len > 255) return hipErrorInvalidValue;  // the kernel's LDS copy (RFC 9380: DST < 256 bytes)
   hipLaunchKernelGGL(k_expand_msg, dim3((n + 63) / 64), dim3(64), 0, st, n, msg, off, len, dst, dst_len, ub);
   return hipGetLastError();
 }
