@@ -977,8 +977,23 @@ def dce(cx):
     return [i for i in range(len(cx.ops)) if live[i]]
 
 
-def schedule(cx, W, earliest=None):
-    """list scheduling: steps of <= 32 W ops, longest remaining path first"""
+# One-wave programs run where a launch holds hundreds of groups (throughput): a step costs its
+# slowest lane, so a step with any product costs a product, while a step of linear combinations
+# alone skips the product (~1/3 of the cost).  Their steps are typed: a product step when at
+# least TYPED_ALPHA * 32 products are ready (its spare lanes take linear combinations), a
+# step of linear combinations otherwise.  Final exponentiation: 766 -> ~650 product-step
+# equivalents; ML(-G1) 437 -> ~340; a Miller item 436 -> ~345.
+# (The cofactor-clearing and [r] sig programs are product chains: typed steps only lengthen
+# them, and the clearing runs one wave per set for a lone set too.)
+TYPED_ALPHA = float(os.environ.get("LSG_SLP_TYPED", "0.5"))
+TYPED_PROGRAMS = ("final_exp", "miller_neg_g1", "miller_item1", "horner_miller", "g2_subgroup")
+
+
+def schedule(cx, W, earliest=None, typed=None):
+    """list scheduling: steps of <= 32 W ops, longest remaining path first (typed: see
+    TYPED_ALPHA)"""
+    if typed:
+        return _schedule_typed(cx, W, typed, earliest)
     cap = 32 * W
     ops = dce(cx)
     idx = {o: k for k, o in enumerate(ops)}
@@ -1032,6 +1047,65 @@ def schedule(cx, W, earliest=None):
     return [s for s in steps if s]
 
 
+def _schedule_typed(cx, W, alpha, earliest=None):
+    cap = 32 * W
+    ops = dce(cx)
+    idx = {o: k for k, o in enumerate(ops)}
+    n = len(ops)
+    preds = [[] for _ in range(n)]
+    succs = [[] for _ in range(n)]
+    for k, o in enumerate(ops):
+        seen = set()
+        for v, _ in cx.ops[o][2] + cx.ops[o][3]:
+            p = cx.prod[v]
+            if p >= 0 and p not in seen:
+                seen.add(p)
+                preds[k].append(idx[p])
+                succs[idx[p]].append(k)
+    islin = [cx.ops[o][0] == "lin" for o in ops]
+    lat = [W_LAT[cx.ops[o][0]] for o in ops]
+    prio = [0.0] * n
+    for k in range(n - 1, -1, -1):
+        prio[k] = lat[k] + max((prio[s] for s in succs[k]), default=0.0)
+    npred = [len(p) for p in preds]
+    hm, hl = [], []  # ready products, ready linear combinations
+    for k in range(n):
+        if npred[k] == 0:
+            heapq.heappush(hl if islin[k] else hm, (-prio[k], k))
+    steps = []
+    done = 0
+    t = 0
+
+    def take(h, cur):
+        deferred = []
+        while h and len(cur) < cap:
+            pr, k = heapq.heappop(h)
+            if earliest and earliest.get(ops[k], 0) > t:
+                deferred.append((pr, k))
+                continue
+            cur.append(k)
+        for x in deferred:
+            heapq.heappush(h, x)
+
+    while done < n:
+        cur = []
+        n_mul = sum(1 for _, k in hm if not (earliest and earliest.get(ops[k], 0) > t))
+        n_lin = sum(1 for _, k in hl if not (earliest and earliest.get(ops[k], 0) > t))
+        if n_mul >= alpha * cap or (n_mul and not n_lin):
+            take(hm, cur)
+        take(hl, cur)
+        if cur:
+            steps.append([ops[k] for k in cur])
+            done += len(cur)
+            for k in cur:
+                for s in succs[k]:
+                    npred[s] -= 1
+                    if npred[s] == 0:
+                        heapq.heappush(hl if islin[s] else hm, (-prio[s], s))
+        t += 1
+    return steps
+
+
 def _hold_back(cx, steps, pred, lead):
     """earliest steps holding every op selected by pred back to `lead` steps before its first
     consumer in `steps` (ops scheduled early only because capacity was free hold their results
@@ -1049,13 +1123,14 @@ def _hold_back(cx, steps, pred, lead):
 def schedule_loads(cx, W, passes=3, lead=4):
     """list schedule, then hold LOADMUL inputs and off-critical-path work back towards their
     consumers: a few passes, each kept only if it does not lengthen the program"""
-    steps = schedule(cx, W)
+    typed = TYPED_ALPHA if W == 1 and TYPED_ALPHA > 0 and cx.name in TYPED_PROGRAMS else None
+    steps = schedule(cx, W, typed=typed)
     if cx.load_inputs is True:
-        steps = schedule(cx, W, _hold_back(cx, steps, lambda p: cx.ops[p][0] == "loadmul", 3))
+        steps = schedule(cx, W, _hold_back(cx, steps, lambda p: cx.ops[p][0] == "loadmul", 3), typed=typed)
     best = steps
     _, best_slots = allocate(cx, best)
     for _ in range(passes):
-        cand = schedule(cx, W, _hold_back(cx, steps, lambda p: True, lead))
+        cand = schedule(cx, W, _hold_back(cx, steps, lambda p: True, lead), typed=typed)
         if len(cand) > len(best) * 1.01:
             break
         _, ns = allocate(cx, cand)
