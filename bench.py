@@ -808,7 +808,7 @@ def main():
             "coalesce": {"max_sets": args.coalesce, "inflight": args.coalesce_inflight} if args.coalesce else None,
             "allocations_in_timed_region": allocs, "timed_window_monotonic_ns": [w0, w1],
             "batch_retries": stats_acc["batch_retries"], "final_exps": stats_acc["n_final_exps"],
-            # (coalesced launches: every ticket reports its launch's count, lodestar_bls.h lsg_wait_merged;
+            # (coalesced launches: every ticket reports its launch's count, lodestar_bls.h lsg_set_coalesce;
             # the sum over tickets counts a launch once per sub-package)
             "final_exps_counting": "per launch, once per ticket" if args.coalesce else "per package",
             "host_submit_ms_per_package": round(stats_acc["submit_us"] / max(stats_acc["packages"], 1) / 1e3, 3),
