@@ -24,6 +24,7 @@ plain() {
 }
 plain
 one rank1 1
+for n in ${REH_RANKS:-}; do one "ranks$n" "$n"; done
 for extra in ${REH_EXTRA:-}; do one "rank1_$extra" 1 --depth "$extra"; done
 for lag in ${REH_LAG:-}; do LSG_BENCH_NODE_LAG=$lag one "rank1_lag$lag" 1; done
 echo "== all ok"
