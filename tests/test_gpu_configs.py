@@ -256,6 +256,25 @@ def test_phase_b0_runs_localise_like_chunks(ctx, keys):
     assert stats["n_final_exps"] < 1 + 128, stats
 
 
+def test_one_wave_programs_in_wide_fallback_phases(ctx, keys):
+    """Fallback phases of more than 128 groups run the one-wave straight-line programs with
+    typed steps (lsg_slp.hip slp_waves, tools/gen_slp.py TYPED_PROGRAMS).  One invalid set in
+    every run of four chunks of a 4096-job package: every B0 run fails, so phase B checks all
+    256 chunks, C1 256 item groups and C2 the 256 jobs of the failing items -- each a one-wave
+    launch.  Verdicts and batch counters against the oracle's worker.ts rules."""
+    n = 4096
+    s = list(single_sets(ctx, keys, b"w1progs", n))
+    bad = [64 * k + (k * 7) % 64 for k in range(n // 64)]
+    for i in bad:
+        s[i] = bd.corrupt_wrong_message(s[i])
+    per = [1] * n
+    for i, v in zip(bad, oracle_each([s[i] for i in bad])):
+        per[i] = v
+    assert all(per[i] == 0 for i in bad)
+    _, stats = check_against_oracle(ctx, [([x], 1) for x in s], per)
+    assert stats["n_final_exps"] > 1 + 64 + 128, stats  # B alone is 256 groups
+
+
 def test_package_group_matches_chunk_mode(ab_ctx, keys, monkeypatch):
     """The one-group phase A (default) and the reference's chunk-16 phase A
     (LSG_PACKAGE_GROUP=0, A/B build) give identical per-job verdicts AND batch_retries /
