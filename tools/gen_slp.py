@@ -992,6 +992,8 @@ TYPED_PROGRAMS = ("final_exp", "miller_neg_g1", "miller_item1", "horner_miller",
 def schedule(cx, W, earliest=None, typed=None):
     """list scheduling: steps of <= 32 W ops, longest remaining path first (typed: see
     TYPED_ALPHA)"""
+    if typed == "crit":
+        return _schedule_crit(cx, W, earliest)
     if typed:
         return _schedule_typed(cx, W, typed, earliest)
     cap = 32 * W
@@ -1106,6 +1108,79 @@ def _schedule_typed(cx, W, alpha, earliest=None):
     return steps
 
 
+# Two-wave programs run where a launch holds few groups (latency): a step of linear
+# combinations alone still skips the product, so a linear combination on the critical path is
+# cheaper in a step of its own than riding in a product step.  Priorities are remaining
+# critical-path costs with a LIN at CRIT_LIN of a product step; a step takes only linear
+# combinations when the most critical ready one outranks every ready product.  Final
+# exponentiation: 612 -> ~550 product-step equivalents (618 -> 636 steps, ~130 of them cheap).
+CRIT_LIN = 0.5
+
+
+def _schedule_crit(cx, W, earliest=None):
+    cap = 32 * W
+    ops = dce(cx)
+    idx = {o: k for k, o in enumerate(ops)}
+    n = len(ops)
+    preds = [[] for _ in range(n)]
+    succs = [[] for _ in range(n)]
+    for k, o in enumerate(ops):
+        seen = set()
+        for v, _ in cx.ops[o][2] + cx.ops[o][3]:
+            p = cx.prod[v]
+            if p >= 0 and p not in seen:
+                seen.add(p)
+                preds[k].append(idx[p])
+                succs[idx[p]].append(k)
+    islin = [cx.ops[o][0] == "lin" for o in ops]
+    lat = [CRIT_LIN if islin[k] else W_LAT[cx.ops[ops[k]][0]] for k in range(n)]
+    prio = [0.0] * n
+    for k in range(n - 1, -1, -1):
+        prio[k] = lat[k] + max((prio[s] for s in succs[k]), default=0.0)
+    npred = [len(p) for p in preds]
+    hm, hl = [], []
+    for k in range(n):
+        if npred[k] == 0:
+            heapq.heappush(hl if islin[k] else hm, (-prio[k], k))
+    steps = []
+    done = 0
+    t = 0
+
+    def ready(k):
+        return not (earliest and earliest.get(ops[k], 0) > t)
+
+    def top(h):
+        return max((-pr for pr, k in h if ready(k)), default=None)
+
+    def take(h, cur):
+        deferred = []
+        while h and len(cur) < cap:
+            pr, k = heapq.heappop(h)
+            if not ready(k):
+                deferred.append((pr, k))
+                continue
+            cur.append(k)
+        for x in deferred:
+            heapq.heappush(h, x)
+
+    while done < n:
+        cur = []
+        tm, tl = top(hm), top(hl)
+        if tm is not None and (tl is None or tl <= tm):
+            take(hm, cur)
+        take(hl, cur)
+        if cur:
+            steps.append([ops[k] for k in cur])
+            done += len(cur)
+            for k in cur:
+                for s2 in succs[k]:
+                    npred[s2] -= 1
+                    if npred[s2] == 0:
+                        heapq.heappush(hl if islin[s2] else hm, (-prio[s2], s2))
+        t += 1
+    return steps
+
+
 def _hold_back(cx, steps, pred, lead):
     """earliest steps holding every op selected by pred back to `lead` steps before its first
     consumer in `steps` (ops scheduled early only because capacity was free hold their results
@@ -1123,7 +1198,12 @@ def _hold_back(cx, steps, pred, lead):
 def schedule_loads(cx, W, passes=3, lead=4):
     """list schedule, then hold LOADMUL inputs and off-critical-path work back towards their
     consumers: a few passes, each kept only if it does not lengthen the program"""
-    typed = TYPED_ALPHA if W == 1 and TYPED_ALPHA > 0 and cx.name in TYPED_PROGRAMS else None
+    typed = None
+    if cx.name in TYPED_PROGRAMS:
+        if W == 1 and TYPED_ALPHA > 0:
+            typed = TYPED_ALPHA
+        elif W == 2 and CRIT_LIN > 0 and os.environ.get("LSG_SLP_CRIT", "1") == "1":
+            typed = "crit"
     steps = schedule(cx, W, typed=typed)
     if cx.load_inputs is True:
         steps = schedule(cx, W, _hold_back(cx, steps, lambda p: cx.ops[p][0] == "loadmul", 3), typed=typed)
