@@ -18,7 +18,8 @@
  */
 const crypto = require("crypto");
 const path = require("path");
-const V = require(path.join(__dirname, "..", "lodestar_amd", "js", "blsGpuVerifier.js"));
+// LSG_VERIFIER_JS: another build of the verifier (A/B runs on one box)
+const V = require(process.env.LSG_VERIFIER_JS || path.join(__dirname, "..", "lodestar_amd", "js", "blsGpuVerifier.js"));
 
 function arg(name, def) {
   const i = process.argv.indexOf("--" + name);

@@ -17,6 +17,10 @@ def test_js_host_queue_logic():
                        text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+    # a test whose promise never settles lets node exit early with status 0: insist on the summary
+    last = r.stdout.strip().splitlines()[-1]
+    done, total = last.split()[0].split("/")
+    assert last.endswith("passed") and done == total, r.stdout
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")

@@ -148,23 +148,6 @@ function serializeSet(set) {
 }
 
 /**
- * Every call's promise is made with this one executor, which hands the resolve function out
- * through a module variable: no closure per call.  A job keeps only that function in its page
- * (the reject function dies young) and is settled by calling it with its boolean verdict, or
- * with a rejected promise for an error -- one promise and one reaction job per call.  What
- * bounds the JS thread is the young-generation collector: node 12's nursery is 16 MB whatever
- * --max-semi-space-size says, so at ~1M calls per 100 ms every pending call survives several
- * scavenges and is copied twice; each retained object per call costs.  Measured in node 12
- * with a 5-package pipeline (tools/node_host_ceiling.js, profiles/r06_node_host_ceiling.txt):
- * `shared.then(pick[i])` (rounds 3-5: a second promise, a reaction and a second microtask per
- * call) 1.3 us per call, resolve + reject kept 0.95 us, resolve only 0.75 us.
- */
-let RES = null;
-function EXEC(resolve) {
-  RES = resolve;
-}
-
-/**
  * verifySignatureSetsMaybeBatch(sets) (maybeBatch.ts:16-39) as ONE non-batchable job sent
  * straight to the addon, outside the queue and ahead of it: verifyPacked's priority flag runs it
  * on the addon's priority thread (never behind the package threads' queue) and on the
@@ -173,17 +156,16 @@ function EXEC(resolve) {
  * with the verdict and the JS thread keeps running meanwhile.  No retry: one job is one
  * maybeBatch call; an error rejects with its BLST code (e.g. BLST_INVALID_SIZE).
  */
-function verifyDirect(addon, ctx, sets, seed) {
-  const page = new JobPage(false, true, null);
-  const p = page.push(sets);
-  const pkg = packJobs([page, 0, 1], sets.length, undefined, 0);
-  if (pkg.nJobs === 1) {
-    addon.verifyPacked(ctx, pkg.arena, pkg.setDesc, pkg.jobDesc, seed, true).then(
-      (r) => settleJobs(pkg.ranges, r.status, r.errCode),
-      (e) => page.fail(0, e)
-    );
+async function verifyDirect(addon, ctx, sets, seed) {
+  const block = new VerdictBlock(false, false);
+  block.add(sets, true);
+  block.seal();
+  const pkg = packBlocks([block], sets.length, undefined);
+  if (pkg.jobBlock.length === 1) {
+    const r = await addon.verifyPacked(ctx, pkg.arena, pkg.setDesc, pkg.jobDesc, seed, true);
+    block.settle(0, r.status[0], r.errCode[0]);
   }
-  return p;
+  return block.verdict(0);
 }
 
 /** utils.ts:19-26 */
@@ -198,7 +180,7 @@ function getAggregatedPubkeysCount(sets) {
 
 function loadAddon() {
   // eslint-disable-next-line global-require
-  return require("../napi/lsg_napi.node");
+  return require("../../lodestar_amd/napi/lsg_napi.node");
 }
 
 /** Reference set shape check done at call time, as serializeSet throws there (index.ts:177). */
@@ -216,9 +198,6 @@ class Fifo {
   }
   get length() {
     return this.items.length - this.head;
-  }
-  peek() {
-    return this.head < this.items.length ? this.items[this.head] : undefined;
   }
   push(x) {
     this.items.push(x);
@@ -242,100 +221,108 @@ class Fifo {
 }
 
 /**
- * Jobs live in pages: parallel arrays (a job's sets, its resolve and reject functions), no
- * object per job.  A page is the reference's buffer of batchable jobs (index.ts:255-302) or a
- * run of non-batchable jobs queued one after another, and it keeps accepting jobs while it
- * waits at the tail of the queue: a batchable job that arrives after its buffer was flushed to
- * the queue joins it there instead of opening a new buffer (it becomes eligible sooner, never
- * later, than in the reference; verdicts do not depend on it).  A package takes jobs from the
- * head page onwards one job at a time, as prepareWork does (index.ts:400-418), so a page can
- * be spread over several packages; a page a package has taken from accepts no more jobs.
+ * Jobs travel in blocks.  A block is the group of jobs queued together -- one buffered batch
+ * of batchable jobs (index.ts:255-302 flushes it to the queue as a whole), or one
+ * non-batchable job -- kept as parallel arrays (no object per job), and a job's promise is
+ * `block.promise.then(PICK[idx])` with PICK[idx] a shared function reading verdict idx: one
+ * promise per call, no executor, no per-call closure.  In node 12 `new Promise(executor)`
+ * costs ~0.75 us against ~0.2 us for a `then` on a shared promise, which decides whether the
+ * JS thread can feed the GPU at all (it has to issue >1M calls/s).  The block resolves when
+ * its last job is answered.
  */
-const PAGE_JOBS = 8192;
+const JOB_PENDING = -1;
+const JOB_FAILED = 3; // settled with a JS Error (queue aborted, serialisation)
+const MAX_JOBS_PER_BLOCK = 4096;
 
-class JobPage {
-  /** @param {number[]|null} added  per-job Date.now() at queueing (jobWaitTime metric) */
-  constructor(batchable, priority, added) {
+class VerdictBlock {
+  /** batchable: the block's jobs are batchable (a buffered block) or not (one job) */
+  constructor(batchable, withTimes) {
+    this.sets = []; // per job (queue order): its sets
     this.batchable = batchable;
-    this.priority = priority;
-    this.sets = []; // per job: its sets (dropped once packed)
-    this.res = []; // per job: its promise's resolve function (undefined once settled)
-    this.added = added;
-    this.n = 0; // jobs
+    this.nFront = 0; // jobs put in front (priority): queue positions 0 .. nFront-1
+    this.added = withTimes ? [] : null; // per job: Date.now() at queueing (jobWaitTime metric)
+    this.order = null; // queue position -> verdict index, once a priority job went in front
+    this.status = null; // per verdict index, allocated when the block is sealed
+    this.codes = null;
+    this.errors = null;
     this.nSigs = 0;
-    this.multi = false; // some job does not hold exactly one set
-    this.taken = 0; // jobs [0, taken) are in packages (or settled)
-    this.open = true; // accepts jobs
-    this.firstPush = 0; // buffered pages: Date.now() of the first job
+    this.remaining = 0;
+    this.sealed = false;
+    this.promise = new Promise((resolve) => {
+      this._resolve = resolve;
+    });
   }
-  push(sets) {
-    const p = new Promise(EXEC);
-    this.sets.push(sets);
-    this.res.push(RES);
-    if (this.added) this.added.push(Date.now());
-    this.n++;
-    this.nSigs += sets.length;
-    if (sets.length !== 1) this.multi = true;
-    if (this.n >= PAGE_JOBS) this.open = false;
-    return p;
-  }
-  fail(j, error) {
-    const r = this.res[j];
-    if (r === undefined) return;
-    this.res[j] = undefined;
-    this.sets[j] = undefined;
-    r(Promise.reject(error));
-  }
-  /** rejects every job not yet in a package */
-  failRest(error) {
-    for (let j = this.taken; j < this.n; j++) this.fail(j, error);
-    this.taken = this.n;
-    this.open = false;
-  }
-}
-
-/** Settles the jobs of a package's ranges ([page, start, end] triples) with the addon's
- * per-job results, in packing order; jobs settled while packing (unserialisable sets) were
- * left out of the package and are skipped here. */
-function settleJobs(ranges, status, codes) {
-  let i = 0;
-  for (let r = 0; r < ranges.length; r += 3) {
-    const page = ranges[r];
-    const res = page.res;
-    for (let j = ranges[r + 1], end = ranges[r + 2]; j < end; j++) {
-      const f = res[j];
-      if (f === undefined) continue;
-      const st = status[i];
-      const code = codes[i];
-      i++;
-      res[j] = undefined;
-      if (st === LSG_VALID) f(true);
-      else if (st === LSG_INVALID) f(false);
-      else f(Promise.reject(Error(errorMessage(code))));
+  /** appends a job; priority jobs of a buffer go to its head (index.ts:296 unshift).
+   * Returns the job's verdict index (the order of arrival). */
+  add(sets, front) {
+    const idx = this.sets.length;
+    if (front) {
+      if (!this.order) {
+        this.order = [];
+        for (let k = 0; k < idx; k++) this.order.push(k);
+      }
+      this.order.unshift(idx);
+      this.sets.unshift(sets);
+      this.nFront++;
+      if (this.added) this.added.unshift(Date.now());
+    } else {
+      if (this.order) this.order.push(idx);
+      this.sets.push(sets);
+      if (this.added) this.added.push(Date.now());
     }
+    this.nSigs += sets.length;
+    return idx;
+  }
+  /** verdict index of the job at queue position k */
+  at(k) {
+    return this.order ? this.order[k] : k;
+  }
+  /** no more jobs: verdict storage for all of them */
+  seal() {
+    if (this.sealed) return;
+    this.sealed = true;
+    const n = this.sets.length;
+    this.status = new Int8Array(n).fill(JOB_PENDING);
+    this.codes = new Int32Array(n);
+    this.remaining = n;
+    if (n === 0) this._resolve(this);
+  }
+  settle(idx, status, code, error) {
+    if (this.status[idx] !== JOB_PENDING) return;
+    this.status[idx] = status;
+    this.codes[idx] = code;
+    if (status === JOB_FAILED) {
+      if (!this.errors) this.errors = [];
+      this.errors[idx] = error;
+    }
+    if (--this.remaining === 0) this._resolve(this);
+  }
+  failAll(error) {
+    this.seal();
+    for (let k = 0; k < this.status.length; k++) this.settle(k, JOB_FAILED, 0, error);
+  }
+  verdict(idx) {
+    const st = this.status[idx];
+    if (st === LSG_ERROR) throw Error(errorMessage(this.codes[idx]));
+    if (st === JOB_FAILED) throw this.errors[idx];
+    return st === LSG_VALID;
   }
 }
 
-/** Rejects every still-pending job of a package's ranges (the addon's call failed). */
-function failJobs(ranges, error) {
-  for (let r = 0; r < ranges.length; r += 3) {
-    const page = ranges[r];
-    for (let j = ranges[r + 1], end = ranges[r + 2]; j < end; j++) page.fail(j, error);
-  }
-}
+const PICK = [];
+for (let i = 0; i < MAX_JOBS_PER_BLOCK; i++) PICK.push((b) => b.verdict(i));
 
 const SET_DESC_WORDS = 7; // pkOff, pkLen, nPks, msgOff, msgLen, sigOff, sigLen (lsg_napi.c verifyPacked)
 
 /**
- * A package's jobs in the addon's packed form: one byte arena with every key, message and
+ * A package of blocks in the addon's packed form: one byte arena with every key, message and
  * signature, 7 descriptor words per set and 2 per job -- the role of the structured clone of
  * BlsWorkReq[] in multithread/index.ts:335 (and of getAggregatedPubkey + toBytes,
- * index.ts:177, except that aggregate keys are summed on the GPU).  `ranges` are
- * [page, start, end] triples.  A job whose sets cannot be serialized is rejected on its own
- * and left out.  `into` (optional) is a previous package's buffers, reused when large enough
- * (fresh multi-MB typed arrays per package cost GC time).  Packed jobs drop their sets.
+ * index.ts:177, except that aggregate keys are summed on the GPU).  A job whose sets cannot
+ * be serialized fails on its own and is left out.  `into` (optional) is a previous package's
+ * buffers, reused when large enough (fresh multi-MB typed arrays per package cost GC time).
  */
-function packJobs(ranges, nSigs, into, minSigs = 0) {
+function packBlocks(blocks, nSigs, into, minSigs = 0) {
   let cap = Math.max(nSigs, minSigs) * 224 + 256;
   let arena = into && into.arenaBuf.length >= cap ? into.arenaBuf : new Uint8Array(cap);
   cap = arena.length;
@@ -356,19 +343,16 @@ function packJobs(ranges, nSigs, into, minSigs = 0) {
   const setDescBuf =
     into && into.setDescBuf.length >= SET_DESC_WORDS * nSigs ? into.setDescBuf : new Uint32Array(SET_DESC_WORDS * Math.max(nSigs, minSigs));
   let nJobs = 0;
-  for (let r = 0; r < ranges.length; r += 3) nJobs += ranges[r + 2] - ranges[r + 1];
+  for (const b of blocks) nJobs += b.sets.length;
   const jobDescBuf = into && into.jobDescBuf.length >= 2 * nJobs ? into.jobDescBuf : new Uint32Array(2 * Math.max(nJobs, minSigs));
+  const jobBlock = [];
+  const jobIdx = [];
   const sd = setDescBuf;
   let k = 0;
   let j = 0;
-  for (let r = 0; r < ranges.length; r += 3) {
-    const page = ranges[r];
-    const flags = (page.batchable ? JOB_BATCHABLE : 0) | (page.priority ? JOB_PRIORITY : 0);
-    const pageSets = page.sets;
-    for (let q = ranges[r + 1], qEnd = ranges[r + 2]; q < qEnd; q++) {
-      const sets = pageSets[q];
-      if (page.res[q] === undefined) continue; // already settled (close)
-      pageSets[q] = undefined;
+  for (const block of blocks) {
+    for (let q = 0; q < block.sets.length; q++) {
+      const sets = block.sets[q];
       const off0 = off;
       const k0 = k;
       try {
@@ -429,17 +413,19 @@ function packJobs(ranges, nSigs, into, minSigs = 0) {
       } catch (e) {
         off = off0;
         k = k0;
-        page.fail(q, e);
+        block.settle(block.at(q), JOB_FAILED, 0, e);
         continue;
       }
       jobDescBuf[2 * j] = sets.length;
-      jobDescBuf[2 * j + 1] = flags;
+      jobDescBuf[2 * j + 1] = (block.batchable ? JOB_BATCHABLE : 0) | (q < block.nFront ? JOB_PRIORITY : 0);
+      jobBlock.push(block);
+      jobIdx.push(block.at(q));
       j++;
     }
   }
   return {
-    ranges,
-    nJobs: j,
+    jobBlock,
+    jobIdx,
     arena: arena.subarray(0, off),
     setDesc: sd.subarray(0, SET_DESC_WORDS * k),
     jobDesc: jobDescBuf.subarray(0, 2 * j),
@@ -473,10 +459,9 @@ class BlsGpuVerifier {
    *     one launch filling all 256 CUs) and light load keeps the latency of small packages;
    *   - at most one package per pipeline slot / package thread (addon.slots) is in flight.
    * Back-pressure (canAcceptWork, index.ts:143-149) is on SETS: queued + buffered + in flight
-   * < `maxPendingSigs` (4 x maxSigsPerPackage: three to four packages on the GPU and one
-   * filling; 5 x adds latency, not throughput: profiles/r06_node_ab.txt).  Per-job verdicts do
-   * not depend on any of it: the GPU applies worker.ts's batch + retry rules to whatever
-   * package it gets.
+   * < `maxPendingSigs` (3 x maxSigsPerPackage: enough to keep the GPU pipelined, and every
+   * pending call is live JS state the young-generation collector copies).  Per-job verdicts do not depend on any of it:
+   * the GPU applies worker.ts's batch + retry rules to whatever package it gets.
    * The reference's policy is {maxSigsPerPackage: 128, eagerPackages: slots}.
    */
   constructor(options = {}, modules = {}) {
@@ -491,19 +476,18 @@ class BlsGpuVerifier {
     this.maxSigsPerPackage = options.maxSigsPerPackage || DEFAULT_MAX_SIGS_PER_PACKAGE;
     this.eagerPackages = options.eagerPackages === undefined ? DEFAULT_EAGER_PACKAGES : options.eagerPackages;
     this.minSigsWhenBusy = options.minSigsWhenBusy || Math.max(1, Math.floor(this.maxSigsPerPackage / 4));
-    this.maxPendingSigs = options.maxPendingSigs || 4 * this.maxSigsPerPackage;
+    this.maxPendingSigs = options.maxPendingSigs || 3 * this.maxSigsPerPackage;
     this.bufferWaitMs = options.bufferWaitMs === undefined ? MAX_BUFFER_WAIT_MS : options.bufferWaitMs;
     if (options.reserveSets && this.addon.reserve) {
       // preallocate every pipeline slot for packages of up to reserveSets sets (lsg_reserve)
       const pks = options.reservePubkeys || options.reserveSets;
       this.addon.reserve(this.ctx, options.reserveSets, pks, 32 * options.reserveSets, this.poolSize);
     }
-    this.jobs = new Fifo(); // queued pages (index.ts `jobs`)
-    this.priorityPages = []; // pages of priority jobs: a stack, drained first
-    this.tail = null; // the last queued page while it accepts jobs
-    this.buffer = null; // buffered batchable jobs (index.ts `bufferedJobs`), a page not yet queued
+    this.jobs = new Fifo(); // queued blocks (index.ts `jobs`, a block at a time)
+    this.priorityJobs = []; // blocks of non-batchable priority jobs: a stack, drained first
     this.queuedJobs = 0;
     this.queuedSigs = 0;
+    this.bufferedJobs = null;
     this.closed = false;
     this.workersBusy = 0; // packages in flight (the reference's busy workers)
     this.sigsInFlight = 0;
@@ -544,7 +528,7 @@ class BlsGpuVerifier {
 
   /** Sets not yet answered: queued, buffered and on the GPU. */
   pendingSigs() {
-    return this.queuedSigs + (this.buffer ? this.buffer.nSigs : 0) + this.sigsInFlight;
+    return this.queuedSigs + (this.bufferedJobs ? this.bufferedJobs.sigCount : 0) + this.sigsInFlight;
   }
 
   canAcceptWork() {
@@ -605,14 +589,13 @@ class BlsGpuVerifier {
       clearTimeout(this.bufferTimer);
       this.bufferTimer = null;
     }
-    if (this.buffer) {
-      this.buffer.failRest(aborted);
-      this.buffer = null;
+    if (this.bufferedJobs) {
+      this.bufferedJobs.block.failAll(aborted);
+      this.bufferedJobs = null;
     }
-    for (const pg of this.priorityPages) pg.failRest(aborted);
-    for (const pg of this.jobs.drain()) pg.failRest(aborted);
-    this.priorityPages = [];
-    this.tail = null;
+    for (const b of this.priorityJobs) b.failAll(aborted);
+    for (const b of this.jobs.drain()) b.failAll(aborted);
+    this.priorityJobs = [];
     this.queuedJobs = 0;
     this.queuedSigs = 0;
     this.closed = true;
@@ -628,49 +611,28 @@ class BlsGpuVerifier {
     if (this.closed) {
       return Promise.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
     }
-    const added = this.metrics !== null;
-    if (opts.priority === true) {
-      // north-star extension: the job goes to the head of the queue, not through the buffer
-      const page = new JobPage(opts.batchable === true, true, added ? [] : null);
-      const p = page.push(sets);
-      page.open = false;
-      this.priorityPages.push(page);
-      this.queuedJobs++;
-      this.queuedSigs += sets.length;
-      this._schedule();
-      return p;
-    }
+    const priority = opts.priority === true;
     if (opts.batchable === true) {
-      const tail = this.tail;
-      if (tail !== null && tail.batchable && tail.open) {
-        // the buffer was flushed and is still waiting in the queue: join it there
-        const p = tail.push(sets);
-        this.queuedJobs++;
-        this.queuedSigs += sets.length;
-        this._schedule();
-        return p;
-      }
-      let buf = this.buffer;
-      if (buf === null) {
-        buf = this.buffer = new JobPage(true, false, added ? [] : null);
-        buf.firstPush = Date.now();
+      let buf = this.bufferedJobs;
+      if (!buf) {
+        buf = this.bufferedJobs = {sigCount: 0, firstPush: Date.now(), block: new VerdictBlock(true, this.metrics !== null)};
         this._armBufferTimer();
       }
-      const p = buf.push(sets);
-      if (buf.nSigs > MAX_BUFFERED_SIGS || !buf.open) this._runBufferedJobs();
+      const idx = buf.block.add(sets, priority);
+      const p = buf.block.promise.then(PICK[idx]);
+      buf.sigCount += sets.length;
+      if (buf.sigCount > MAX_BUFFERED_SIGS || buf.block.sets.length >= MAX_JOBS_PER_BLOCK) this._runBufferedJobs();
       return p;
     }
-    let page = this.tail;
-    if (page === null || page.batchable || !page.open) {
-      page = new JobPage(false, false, added ? [] : null);
-      this.jobs.push(page);
-      this.tail = page;
-    }
-    const p = page.push(sets);
+    const block = new VerdictBlock(false, this.metrics !== null);
+    block.add(sets, priority);
+    block.seal();
+    if (priority) this.priorityJobs.push(block);
+    else this.jobs.push(block);
     this.queuedJobs++;
     this.queuedSigs += sets.length;
     this._schedule();
-    return p;
+    return block.promise.then(PICK[0]);
   }
 
   /** One timer for the buffer's 100 ms limit (index.ts:291-293 arms one per buffer; a buffer
@@ -682,7 +644,7 @@ class BlsGpuVerifier {
 
   _onBufferTimer() {
     this.bufferTimer = null;
-    const buf = this.buffer;
+    const buf = this.bufferedJobs;
     if (!buf) return;
     const age = Date.now() - buf.firstPush;
     if (age >= this.bufferWaitMs) this._runBufferedJobs();
@@ -705,24 +667,25 @@ class BlsGpuVerifier {
       // just completed (class comment)
       if (this.workersBusy >= this.eagerPackages && this.queuedSigs < this.minSigsWhenBusy && !this.kick) break;
       this.kick = false;
-      const work = this._prepareWork();
-      if (work.ranges.length === 0) break;
-      this._runPackage(work);
+      const blocks = this._prepareWork();
+      if (blocks.length === 0) break;
+      this._runPackage(blocks);
     }
   }
 
-  _runPackage(work) {
+  _runPackage(blocks) {
     const m = this.metrics && this.metrics.blsThreadPool;
-    const ranges = work.ranges;
-    const startedSigSets = work.nSigs;
+    let startedSigSets = 0;
+    let startedJobs = 0;
+    const now = m ? Date.now() : 0;
+    for (const b of blocks) {
+      startedSigSets += b.nSigs;
+      startedJobs += b.sets.length;
+      if (m) for (const t of b.added) m.jobWaitTime.observe((now - t) / 1000);
+    }
     if (m) {
-      const now = Date.now();
-      for (let r = 0; r < ranges.length; r += 3) {
-        const added = ranges[r].added;
-        for (let j = ranges[r + 1]; j < ranges[r + 2]; j++) m.jobWaitTime.observe((now - added[j]) / 1000);
-      }
       m.totalJobsGroupsStarted.inc(1);
-      m.totalJobsStarted.inc(work.nJobs);
+      m.totalJobsStarted.inc(startedJobs);
       m.totalSigSetsStarted.inc(startedSigSets);
     }
     this.workersBusy++;
@@ -733,16 +696,21 @@ class BlsGpuVerifier {
       let pkg = null;
       try {
         // buffers sized for a full package, so that every one can be reused
-        pkg = packJobs(ranges, startedSigSets, this.spare.pop(), this.maxSigsPerPackage);
-        if (pkg.nJobs === 0) return;
+        pkg = packBlocks(blocks, startedSigSets, this.spare.pop(), this.maxSigsPerPackage);
+        const n = pkg.jobBlock.length;
+        if (n === 0) return;
         const jobStartNs = process.hrtime.bigint();
         const workResult = await this.addon.verifyPacked(this.ctx, pkg.arena, pkg.setDesc, pkg.jobDesc, this.seed);
         const jobEndNs = process.hrtime.bigint();
+        const status = workResult.status;
+        const codes = workResult.errCode;
+        let errorCount = 0;
+        for (let i = 0; i < n; i++) {
+          if (status[i] === LSG_ERROR) errorCount += pkg.jobBlock[i].sets.length;
+          pkg.jobBlock[i].settle(pkg.jobIdx[i], status[i], codes[i]);
+        }
         if (m) {
           // index.ts:362-381, with the GPU package in the worker's place
-          let errorCount = 0;
-          const jd = pkg.jobDesc;
-          for (let i = 0; i < pkg.nJobs; i++) if (workResult.status[i] === LSG_ERROR) errorCount += jd[2 * i];
           const workerJobTimeSec = (workResult.endNs - workResult.startNs) / 1e9;
           const latencyToWorkerSec = (workResult.startNs - Number(jobStartNs)) / 1e9;
           const latencyFromWorkerSec = (Number(jobEndNs) - workResult.endNs) / 1e9;
@@ -755,11 +723,10 @@ class BlsGpuVerifier {
           m.batchRetries.inc(workResult.batchRetries);
           m.batchSigsSuccess.inc(workResult.batchSigsSuccess);
         }
-        settleJobs(ranges, workResult.status, workResult.errCode);
         if (this.spare.length < this.poolSize) this.spare.push(pkg);
       } catch (e) {
         if (!this.closed && this.logger) this.logger.error("BlsGpuVerifier error", {}, e);
-        failJobs(ranges, e);
+        for (const b of blocks) b.failAll(e);
       }
     })();
     this.inflight.add(run);
@@ -772,51 +739,33 @@ class BlsGpuVerifier {
     });
   }
 
-  /** Jobs for one package: priority pages first, then FIFO, up to maxSigsPerPackage sigs, a
-   * job at a time as index.ts:400-418 takes them (a page may be split between packages). */
+  /** blocks for one package: priority blocks first, then FIFO, up to maxSigsPerPackage sigs
+   * (a block is never split; index.ts:400-418 takes whole jobs the same way) */
   _prepareWork() {
-    const ranges = [];
+    const blocks = [];
     let totalSigs = 0;
     let totalJobs = 0;
-    const max = this.maxSigsPerPackage;
-    while (totalSigs < max) {
-      const prio = this.priorityPages.length > 0;
-      const page = prio ? this.priorityPages[this.priorityPages.length - 1] : this.jobs.peek();
-      if (page === undefined) break;
-      page.open = false;
-      if (page === this.tail) this.tail = null;
-      const start = page.taken;
-      let end = start;
-      if (!page.multi) {
-        // single-set jobs (the gossip shape): one sig per job
-        end = Math.min(page.n, start + (max - totalSigs));
-        totalSigs += end - start;
-      } else {
-        const sets = page.sets;
-        while (end < page.n && totalSigs < max) totalSigs += sets[end++].length;
-      }
-      page.taken = end;
-      totalJobs += end - start;
-      ranges.push(page, start, end);
-      if (end === page.n) {
-        if (prio) this.priorityPages.pop();
-        else this.jobs.shift();
-      }
+    while (totalSigs < this.maxSigsPerPackage) {
+      const b = this.priorityJobs.length ? this.priorityJobs.pop() : this.jobs.shift();
+      if (!b) break;
+      blocks.push(b);
+      totalSigs += b.nSigs;
+      totalJobs += b.sets.length;
     }
     this.queuedSigs -= totalSigs;
     this.queuedJobs -= totalJobs;
-    return {ranges, nSigs: totalSigs, nJobs: totalJobs};
+    return blocks;
   }
 
   _runBufferedJobs() {
-    const buf = this.buffer;
+    const buf = this.bufferedJobs;
     if (buf) {
       // the buffer goes to the tail of the queue as a whole (index.ts:425-431)
-      this.buffer = null;
-      this.jobs.push(buf);
-      this.tail = buf;
-      this.queuedJobs += buf.n;
-      this.queuedSigs += buf.nSigs;
+      this.bufferedJobs = null;
+      buf.block.seal();
+      this.jobs.push(buf.block);
+      this.queuedJobs += buf.block.sets.length;
+      this.queuedSigs += buf.block.nSigs;
       this._schedule();
     }
   }
@@ -885,7 +834,7 @@ module.exports = {
   SignatureSetType,
   chunkifyMaximizeChunkSize,
   errorMessage,
-  packJobs,
+  packBlocks,
   DEFAULT_MAX_SIGS_PER_PACKAGE,
   MAX_SIGNATURE_SETS_PER_JOB,
   MAX_BUFFERED_SIGS,
