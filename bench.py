@@ -385,6 +385,9 @@ def main():
     ap.add_argument("--devices", type=int, default=0,
                     help="one process over N GPUs (lsg_init_devices, in-library RCCL exchange: the context "
                          "BlsGpuVerifier({devices}) opens); packages of sets-per-step x N sets")
+    ap.add_argument("--devices-same", action="store_true",
+                    help="with --devices N: the context's N devices are all this process's GPU (duplicate ids, "
+                         "device copies instead of RCCL) -- rehearses the multi-device host path on one GPU")
     args = ap.parse_args()
     if args.workload == "node":
         return run_node_workload(args)
@@ -428,15 +431,22 @@ def main():
     # packages whose per-kernel HIP-event times are read back in the timed region (the
     # reading costs host time: a sample, not every package of a 640-step small-package run)
     KT_SAMPLE = 30
+    t_start = time.perf_counter()
+
+    def progress(what):  # (stderr: a long input generation or reservation is not a hang)
+        print(f"[bench {time.perf_counter() - t_start:7.1f} s] {what}", file=sys.stderr, flush=True)
+
     n_dev = max(args.devices, 1)
     if args.devices:
         if world > 1:
             raise SystemExit("--devices runs one process over several GPUs (no torch.distributed launch)")
-        ctx = Context(devices=list(range(args.devices)))
+        ctx = Context(devices=[local] * args.devices if args.devices_same else list(range(args.devices)))
     else:
         ctx = Context(local)
+    progress("context open; generating inputs")
     wl = Workload(ctx, args.workload, rank, args.sets_per_step * n_dev, args.packages, blocks=args.blocks,
                   validators=args.validators)
+    progress("inputs generated")
     prepared = [PreparedJobs(jobs) for jobs, _ in wl.packages]
     n_sets = wl.sets_per_package
     max_pks = int(n_sets * wl.pks_per_set) + 1
@@ -446,6 +456,7 @@ def main():
     ctx.reserve(n_sets * co, max_pks * co, 32 * n_sets * co, n_slots=args.depth + 1 + (NODE_LAG if world > 1 or rehearse else 0))
     if args.coalesce:
         ctx.set_coalesce(args.coalesce, args.coalesce_inflight)
+    progress("slots reserved")
 
     import numpy as np
 
@@ -683,6 +694,7 @@ def main():
             dist.barrier()
 
     run(max(args.warmup, args.depth), args.depth)
+    progress("warmup done")
     allocs0 = ctx.allocation_count()
     stats_acc.clear()
     barrier()
@@ -801,7 +813,8 @@ def main():
             "config": {"workload": desc, "sets_per_step_per_gpu": n_sets // n_dev, "global_batch": n_sets * world,
                        "jobs_per_package": len(wl.packages[0][0]), "pubkeys_per_set": round(wl.pks_per_set, 1),
                        "keys": N_KEYS, "validators": args.validators if args.workload == "block" else None,
-                       "parallelism": f"devices{args.devices} (one context, RCCL exchange)" if args.devices else f"shard{world}"},
+                       "parallelism": (f"devices{args.devices}x{local} (one context, one GPU: duplicate ids)" if args.devices_same
+                                       else f"devices{args.devices} (one context, RCCL exchange)") if args.devices else f"shard{world}"},
             "p50_batch_latency_ms": round(1e3 * statistics.median(lat), 3),
             "p50_unloaded_latency_ms": round(1e3 * statistics.median(lat1), 3),
             "pipeline_depth": args.depth, "distinct_packages": len(prepared),

@@ -145,7 +145,10 @@ const char* lsg_last_error(lsg_ctx* ctx);
 int lsg_device_name(lsg_ctx* ctx, char* buf, size_t len);
 /* Preallocate every device and pinned buffer of the first n_slots pipeline slots (0 = all) of
  * every device for packages of up to max_sets sets, max_pks keys and max_msg_bytes message
- * bytes, so that submissions within those bounds allocate nothing. */
+ * bytes, so that submissions within those bounds allocate nothing.  A context over n devices
+ * reserves each device for its share: 1/n of each bound plus one 4,096-set job's worth.
+ * lsg_submit_jobs stages a package with the context lock released (several host threads may
+ * stage packages at once; the devices of a multi-device context are staged in parallel). */
 int lsg_reserve(lsg_ctx* ctx, size_t max_sets, size_t max_pks, size_t max_msg_bytes, int32_t n_slots);
 /* Device + pinned allocations made by this process so far (steady-state checks). */
 int lsg_allocation_count(lsg_ctx* ctx, uint64_t* n);

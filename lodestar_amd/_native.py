@@ -447,7 +447,8 @@ class Context:
         out = ctypes.create_string_buffer(96 * n)
         err = (ctypes.c_int32 * n)()
         self._check(self.lib.lsg_aggregate_pubkeys_multi(self.h, b.arr, n, out, err), "lsg_aggregate_pubkeys_multi")
-        return [(out.raw[96 * i:96 * i + 96], err[i]) for i in range(n)]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [(raw[96 * i:96 * i + 96], err[i]) for i in range(n)]
 
     def pubkey_table_set(self, first_index, pks):
         """index2pubkey[first_index + k] = pks[k] on the device; returns per-key BLST codes."""
@@ -472,7 +473,8 @@ class Context:
         out = ctypes.create_string_buffer(96 * n)
         err = (ctypes.c_int32 * n)()
         self._check(self.lib.lsg_pubkey_validate(self.h, b"".join(pks), pk_len, n, out, err), "lsg_pubkey_validate")
-        return [(out.raw[96 * k:96 * k + 96], err[k]) for k in range(n)]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [(raw[96 * k:96 * k + 96], err[k]) for k in range(n)]
 
     def aggregate_signatures(self, groups):
         """Op-pool Signature.aggregate over each list of signatures in `groups` (one device
@@ -490,7 +492,8 @@ class Context:
         err = (ctypes.c_int32 * ng)()
         self._check(self.lib.lsg_aggregate_signatures(self.h, b"".join(flat), sl, offs, ng, out, err),
                     "lsg_aggregate_signatures")
-        return [(out.raw[96 * g:96 * g + 96], err[g]) for g in range(ng)]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [(raw[96 * g:96 * g + 96], err[g]) for g in range(ng)]
 
     def _signing_roots(self, fn, objs, size, domains):
         n = len(objs)
@@ -505,7 +508,8 @@ class Context:
         assert len(dom) == (32 if stride == 0 else 32 * n)
         out = ctypes.create_string_buffer(32 * n)
         self._check(getattr(self.lib, fn)(self.h, b"".join(objs), n, dom, stride, out), fn)
-        return [out.raw[32 * i:32 * i + 32] for i in range(n)]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [raw[32 * i:32 * i + 32] for i in range(n)]
 
     def signing_roots(self, object_roots, domains):
         """computeSigningRoot from object roots; `domains` is one 32-byte domain or a list."""
@@ -522,7 +526,8 @@ class Context:
         assert all(len(m) == ml for m in msgs)
         out = ctypes.create_string_buffer(192 * len(msgs))
         self._check(self.lib.lsg_hash_to_g2(self.h, b"".join(msgs), ml, len(msgs), dst, len(dst), out), "lsg_hash_to_g2")
-        return [out.raw[192 * i:192 * i + 192] for i in range(len(msgs))]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [raw[192 * i:192 * i + 192] for i in range(len(msgs))]
 
     def sig_decode(self, sigs):
         if not sigs:
@@ -532,7 +537,8 @@ class Context:
         out = ctypes.create_string_buffer(192 * len(sigs))
         err = (ctypes.c_int32 * len(sigs))()
         self._check(self.lib.lsg_sig_decode(self.h, b"".join(sigs), sl, len(sigs), out, err), "lsg_sig_decode")
-        return [(out.raw[192 * i:192 * i + 192], err[i]) for i in range(len(sigs))]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [(raw[192 * i:192 * i + 192], err[i]) for i in range(len(sigs))]
 
     def batch_partial(self, sets, seed=0):
         b = SetBuffer(sets)
@@ -591,7 +597,8 @@ class Context:
         out = ctypes.create_string_buffer(96 * len(sks))
         skb = b"".join(int(k).to_bytes(32, "big") for k in sks)
         self._check(self.lib.lsg_sign(self.h, skb, b"".join(msgs), ml, len(sks), out), "lsg_sign")
-        return [out.raw[96 * i:96 * i + 96] for i in range(len(sks))]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [raw[96 * i:96 * i + 96] for i in range(len(sks))]
 
     def sk_to_pk(self, sks):
         if not sks:
@@ -599,7 +606,8 @@ class Context:
         out = ctypes.create_string_buffer(96 * len(sks))
         skb = b"".join(int(k).to_bytes(32, "big") for k in sks)
         self._check(self.lib.lsg_sk_to_pk(self.h, skb, len(sks), out), "lsg_sk_to_pk")
-        return [out.raw[96 * i:96 * i + 96] for i in range(len(sks))]
+        raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
+        return [raw[96 * i:96 * i + 96] for i in range(len(sks))]
 
     def probe_fp_mul_rate(self):
         a, b = ctypes.c_double(), ctypes.c_double()

@@ -35,6 +35,7 @@
 #include <condition_variable>
 #include <chrono>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <unordered_map>
 #include <string>
@@ -248,7 +249,13 @@ SegPlan plan_seg(std::vector<int32_t>& A, int op, const std::vector<int32_t>& se
 // ---------------------------------------------------------------------------- state
 namespace {
 
-enum SlotKind { SLOT_FREE = 0, SLOT_JOBS = 1, SLOT_FINAL = 3, SLOT_MERGE = 4 /* tickets of coalesced packages */ };
+enum SlotKind {
+  SLOT_FREE = 0,
+  SLOT_JOBS = 1,
+  SLOT_STAGING = 2, /* reserved by a submission staging it with the context lock released */
+  SLOT_FINAL = 3,
+  SLOT_MERGE = 4 /* tickets of coalesced packages */
+};
 
 // a small package held for a coalesced launch (lsg_set_coalesce): the caller's jobs, sets
 // and bytes copied, so the caller's buffers are free once lsg_submit_jobs returns
@@ -452,6 +459,13 @@ struct lsg_ctx {
   std::mutex mu;
   std::condition_variable cv;  // waiters of a coalesced slot being resolved by another thread
   std::string err;
+  // Packages are staged with `mu` released (submit_pkg): `tab_mu` keeps the validator pubkey
+  // table they read from changing meanwhile (shared while staging, exclusive in
+  // lsg_pubkey_table_set, always taken before `mu`), `xmu` orders the RCCL exchanges of
+  // packages staged at the same time, `staging` counts the submissions in flight.
+  std::shared_mutex tab_mu;
+  std::mutex xmu;
+  int staging = 0;
   // coalescing (lsg_set_coalesce): packages of <= co_max_sets sets wait in `pending` while
   // co_inflight launches are on the device, then go out as one launch
   uint32_t co_max_sets = 0;
@@ -469,8 +483,18 @@ struct lsg_ctx {
 
 namespace {
 
+// A thread staging a package without the context lock reports its errors here; the
+// submitter copies them into c->err once it holds the lock again (submit_pkg).
+thread_local std::string* t_err_sink = nullptr;
+void set_err(lsg_ctx* c, std::string m) {
+  if (t_err_sink)
+    *t_err_sink = std::move(m);
+  else
+    c->err = std::move(m);
+}
+
 int fail_c(lsg_ctx* c, const char* what, hipError_t e) {
-  c->err = std::string(what) + ": " + hipGetErrorString(e);
+  set_err(c, std::string(what) + ": " + hipGetErrorString(e));
   return LSG_ERR_DEVICE;
 }
 int fail(Slot* s, const char* what, hipError_t e) { return fail_c(s->d->c, what, e); }
@@ -1176,13 +1200,13 @@ int stage_sets(Slot* s, const lsg_set* const* sets, size_t n, uint64_t seed, boo
   if (scale && n) {
     if (seed == 0) {
       if (!os_random(rnd, 8 * n)) {
-        s->d->c->err = "no entropy for the RLC randomizers (getrandom failed)";
+        set_err(s->d->c, "no entropy for the RLC randomizers (getrandom failed)");
         return LSG_ERR_ENTROPY;
       }
       for (size_t i = 0; i < n; i++)
         while (rnd[i] == 0)
           if (!os_random(&rnd[i], 8)) {
-            s->d->c->err = "no entropy for the RLC randomizers (getrandom failed)";
+            set_err(s->d->c, "no entropy for the RLC randomizers (getrandom failed)");
             return LSG_ERR_ENTROPY;
           }
     } else {
@@ -2061,7 +2085,7 @@ int export_partial_dev(Slot* s, const uint8_t** src, hipStream_t xs = nullptr) {
   } else {
     do {
       if (!os_random(&r, 8)) {
-        s->d->c->err = "no entropy for the exported partial's randomizer (getrandom failed)";
+        set_err(s->d->c, "no entropy for the exported partial's randomizer (getrandom failed)");
         return LSG_ERR_ENTROPY;
       }
     } while (r == 0);
@@ -2664,7 +2688,7 @@ int pkg_exchange(lsg_ctx* c, int p) {
     if (r == ncclSuccess) r = r2;
     (void)hipSetDevice(c->dev[0]->device);
     if (r != ncclSuccess) {
-      c->err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
+      set_err(c, std::string("ncclAllGather: ") + ncclGetErrorString(r));
       return LSG_ERR_DEVICE;
     }
   } else {
@@ -2683,7 +2707,118 @@ int pkg_exchange(lsg_ctx* c, int p) {
   return pkg_node_check(s0, n);
 }
 
-int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket,
+// Each device's share of a package (pkg_part1 .. pkg_part2), staged with the context lock
+// released: device 0 on the calling thread, every other device on a thread of its own, so that
+// a context over N GPUs spends one device's staging time per package instead of N (VERDICT r5
+// item 3), and host threads submitting packages to different slots stage them side by side.
+// Errors go to *err (t_err_sink), not to c->err.
+int stage_pkg(lsg_ctx* c, int p, const lsg_job* jobs, size_t n_jobs, uint64_t seed, bool lone_ok, bool exch,
+              std::string* err) {
+  const int n = c->n_dev;
+  std::vector<std::vector<size_t>> ids(n);
+  {
+    std::vector<uint32_t> sizes(n_jobs);
+    std::vector<int32_t> owner(n_jobs);
+    for (size_t j = 0; j < n_jobs; j++) sizes[j] = jobs[j].n_sets;
+    assign_jobs(sizes.data(), n_jobs, n, owner.data());
+    for (size_t j = 0; j < n_jobs; j++) ids[(size_t)owner[j]].push_back(j);
+  }
+  std::vector<int> rcs(n, LSG_OK);
+  std::vector<std::string> errs(n);
+  auto part1 = [&](int d) {
+    t_err_sink = &errs[d];
+    (void)hipSetDevice(c->dev[d]->device);
+    // distinct seeds per device for tests; 0 stays 0 (OS CSPRNG on every device)
+    const uint64_t sd = seed ? seed + 0x9e3779b97f4a7c15ull * (uint64_t)d : 0;
+    rcs[d] = pkg_part1(&c->dev[d]->slots[p], jobs, ids[d], sd, (d == 0 && exch) ? n : 0, nullptr, lone_ok && !exch);
+    t_err_sink = nullptr;
+  };
+  auto part2 = [&](int d) {
+    t_err_sink = &errs[d];
+    (void)hipSetDevice(c->dev[d]->device);
+    rcs[d] = pkg_part2(&c->dev[d]->slots[p], exch);
+    t_err_sink = nullptr;
+  };
+  // first error in device order
+  auto first_rc = [&]() {
+    for (int d = 0; d < n; d++)
+      if (rcs[d]) {
+        *err = errs[d];
+        return rcs[d];
+      }
+    return (int)LSG_OK;
+  };
+  std::shared_lock<std::shared_mutex> tab(c->tab_mu);  // (the sets may name table rows)
+  int rc = LSG_OK;
+  // A/B build: LSG_STAGE_PAR=0 stages the devices one after another (round 5), 1 runs part 1
+  // on threads and part 2 serially, 2 (shipped) both on threads
+  const long par = n == 1 ? 0 : lsg_ab_long("LSG_STAGE_PAR", 2);
+  if (par == 0) {
+    for (int d = 0; d < n && !rc; d++) {
+      part1(d);
+      rc = first_rc();
+    }
+    if (!rc && exch) {
+      std::lock_guard<std::mutex> x(c->xmu);
+      t_err_sink = err;
+      rc = pkg_exchange(c, p);
+      t_err_sink = nullptr;
+    }
+    for (int d = 0; d < n && !rc; d++) {
+      part2(d);
+      rc = first_rc();
+    }
+    return rc;
+  }
+  // devices 1..n-1 on threads of their own: part 1, then (after the exchange, which needs every
+  // device's partial) part 2
+  std::mutex m;
+  std::condition_variable cv;
+  int n_part1 = 1;  // devices done with part 1 (device 0 counted when it is)
+  int phase2 = 0;   // 1: run part 2, -1: stop (an error before the exchange or in it)
+  std::vector<std::thread> th;
+  for (int d = 1; d < n; d++)
+    th.emplace_back([&, d] {
+      part1(d);
+      std::unique_lock<std::mutex> l(m);
+      n_part1++;
+      cv.notify_all();
+      cv.wait(l, [&] { return phase2 != 0; });
+      const bool go = phase2 > 0 && par >= 2;
+      l.unlock();
+      if (go) part2(d);
+    });
+  part1(0);
+  {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [&] { return n_part1 == n; });
+  }
+  rc = first_rc();
+  if (!rc && exch) {
+    std::lock_guard<std::mutex> x(c->xmu);  // one exchange at a time over the communicators
+    t_err_sink = err;
+    rc = pkg_exchange(c, p);
+    t_err_sink = nullptr;
+  }
+  {
+    std::lock_guard<std::mutex> l(m);
+    phase2 = rc ? -1 : 1;
+  }
+  cv.notify_all();
+  if (!rc) part2(0);
+  for (int d = 1; d < n && !rc && par < 2; d++) {
+    part2(d);
+    rc = first_rc();
+  }
+  for (auto& t : th) t.join();
+  if (!rc) rc = first_rc();
+  return rc;
+}
+
+// A package: its slot is reserved on every device under the context lock (`lk`, held on entry
+// and on return), staged with the lock released (stage_pkg), and its ticket committed under the
+// lock again.  A reserved slot is SLOT_STAGING: no other call takes, reserves or waits on it.
+int submit_pkg(lsg_ctx* c, CtxLock& lk, const lsg_job* jobs, size_t n_jobs, uint64_t seed, lsg_ticket* ticket,
                bool lone_ok = true) {
   int p = -1;
   for (int i = 0; i < LSG_SLOTS && p < 0; i++)
@@ -2701,30 +2836,21 @@ int submit_pkg(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t seed, ls
     LSG_RC(slot_ready(c->dev[d], &c->dev[d]->slots[p], p));
     LSG_RC(slot_streams(&c->dev[d]->slots[p], prio));
   }
+  for (int d = 0; d < n; d++) c->dev[d]->slots[p].kind = SLOT_STAGING;
+  c->staging++;
+  lk.unlock();
+  std::string err;
+  const int rc = stage_pkg(c, p, jobs, n_jobs, seed, lone_ok, exch, &err);
+  lk.lock();
   (void)hipSetDevice(c->dev[0]->device);
-  std::vector<std::vector<size_t>> ids(n);
-  {
-    std::vector<uint32_t> sizes(n_jobs);
-    std::vector<int32_t> owner(n_jobs);
-    for (size_t j = 0; j < n_jobs; j++) sizes[j] = jobs[j].n_sets;
-    assign_jobs(sizes.data(), n_jobs, n, owner.data());
-    for (size_t j = 0; j < n_jobs; j++) ids[(size_t)owner[j]].push_back(j);
-  }
-  int rc = LSG_OK;
-  for (int d = 0; d < n && !rc; d++) {
-    (void)hipSetDevice(c->dev[d]->device);
-    // distinct seeds per device for tests; 0 stays 0 (OS CSPRNG on every device)
-    const uint64_t sd = seed ? seed + 0x9e3779b97f4a7c15ull * (uint64_t)d : 0;
-    rc = pkg_part1(&c->dev[d]->slots[p], jobs, ids[d], sd, (d == 0 && exch) ? n : 0, nullptr, lone_ok && !exch);
-  }
-  if (!rc && exch) rc = pkg_exchange(c, p);
-  for (int d = 0; d < n && !rc; d++) {
-    (void)hipSetDevice(c->dev[d]->device);
-    rc = pkg_part2(&c->dev[d]->slots[p], exch);
-  }
-  (void)hipSetDevice(c->dev[0]->device);
+  c->staging--;
+  c->cv.notify_all();
   if (rc) {
-    for (int d = 0; d < n; d++) sync_slot(&c->dev[d]->slots[p]);
+    for (int d = 0; d < n; d++) {
+      sync_slot(&c->dev[d]->slots[p]);
+      c->dev[d]->slots[p].kind = SLOT_FREE;
+    }
+    c->err = err;
     return rc;
   }
   uint64_t serial;
@@ -2960,8 +3086,9 @@ int wait_merged(lsg_ctx* c, lsg_ticket t, lsg_job_result* results, lsg_stats* st
     k = it->second.sub;
     ev = c->dev[0]->slots[p].ev_done;
   }
-  if (event_wait(ev) != hipSuccess) return fail_c(c, "hipEventSynchronize", hipGetLastError());
+  const hipError_t wr = event_wait(ev);
   CtxLock lk(c->mu);
+  if (wr != hipSuccess) return fail_c(c, "hipEventSynchronize", wr);
   LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
   Slot* s = &c->dev[0]->slots[p];
   c->cv.wait(lk, [&] { return !s->resolving; });
@@ -3016,7 +3143,10 @@ int presync_pkg(lsg_ctx* c, lsg_ticket t, bool partial_only) {
   for (auto& e : evs) {
     (void)hipSetDevice(e.first);
     hipError_t r = event_wait(e.second);
-    if (r != hipSuccess) return fail_c(c, "hipEventSynchronize", r);
+    if (r != hipSuccess) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      return fail_c(c, "hipEventSynchronize", r);
+    }
   }
   return LSG_OK;
 }
@@ -3260,7 +3390,14 @@ int lsg_device_count(lsg_ctx* c, int32_t* n) {
   return LSG_OK;
 }
 
-const char* lsg_last_error(lsg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+// a copy per calling thread: another thread's failing call may replace c->err meanwhile
+const char* lsg_last_error(lsg_ctx* c) {
+  if (!c) return "null context";
+  thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(c->mu);
+  copy = c->err;
+  return copy.c_str();
+}
 
 int lsg_device_name(lsg_ctx* c, char* buf, size_t len) {
   if (!c || !buf || !len) return LSG_ERR_INVALID_ARG;
@@ -3275,6 +3412,15 @@ int lsg_reserve(lsg_ctx* c, size_t max_sets, size_t max_pks, size_t max_msg_byte
   if (!c || n_slots < 0) return LSG_ERR_INVALID_ARG;
   LSG_ENTER(c);
   const int ns = std::min(n_slots == 0 ? LSG_SLOTS : n_slots, LSG_SLOTS);
+  if (c->n_dev > 1) {
+    // a device stages its share of a package: whole jobs by cumulative set count (assign_jobs),
+    // so at most 1/n of the sets plus one job's -- reserved with a job's worth of slack (a larger
+    // share grows its slot's buffers when it comes)
+    const size_t n = (size_t)c->n_dev;
+    max_sets = std::min(max_sets, max_sets / n + 4096);
+    max_pks = std::min(max_pks, max_pks / n + 4096 * 512);
+    max_msg_bytes = std::min(max_msg_bytes, max_msg_bytes / n + 4096 * 32);
+  }
   for (int d = 0; d < c->n_dev; d++) {
     LSG_HIPC(c, hipSetDevice(c->dev[d]->device));
     for (int i = 0; i < ns; i++) {
@@ -3317,7 +3463,8 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
   if (!c || !ticket || (n_jobs && !jobs)) return LSG_ERR_INVALID_ARG;
   for (size_t j = 0; j < n_jobs; j++)
     if (jobs[j].n_sets && !jobs[j].sets) return LSG_ERR_INVALID_ARG;
-  LSG_ENTER(c);
+  CtxLock lk(c->mu);
+  LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
   bool prio = false;
   for (size_t j = 0; j < n_jobs; j++) prio = prio || (jobs[j].flags & LSG_JOB_PRIORITY) != 0;
   if (c->co_max_sets && c->n_dev == 1 && !prio) {  // (a priority package is never held back)
@@ -3325,7 +3472,7 @@ int lsg_submit_jobs(lsg_ctx* c, const lsg_job* jobs, size_t n_jobs, uint64_t see
     for (size_t j = 0; j < n_jobs; j++) ns += jobs[j].n_sets;
     if (ns <= c->co_max_sets) return submit_merged(c, jobs, n_jobs, seed, ns, ticket);
   }
-  return submit_pkg(c, jobs, n_jobs, seed, ticket);
+  return submit_pkg(c, lk, jobs, n_jobs, seed, ticket);
 }
 
 int lsg_set_coalesce(lsg_ctx* c, uint32_t max_sets, int32_t max_inflight) {
@@ -3428,7 +3575,10 @@ int lsg_jobs_partial_device(lsg_ctx* c, lsg_ticket ticket, void* dev_out576, int
   // the copy completes without the context lock held: submissions and resolutions of other
   // packages go on meanwhile
   (void)hipSetDevice(c->dev[0]->device);
-  if (hipError_t e = event_wait(xev)) return fail_c(c, "hipEventSynchronize", e);
+  if (hipError_t e = event_wait(xev)) {
+    std::lock_guard<std::mutex> lk(c->mu);  // (c->err is written under the lock)
+    return fail_c(c, "hipEventSynchronize", e);
+  }
   if (has_batch) *has_batch = has ? 1 : 0;
   return LSG_OK;
 }
@@ -3507,12 +3657,13 @@ int lsg_batch_partial(lsg_ctx* c, const lsg_set* sets, size_t n_sets, uint64_t s
   }
   lsg_ticket t;
   {
-    LSG_ENTER(c);
+    CtxLock lk(c->mu);
+    LSG_HIPC(c, hipSetDevice(c->dev[0]->device));
     lsg_job job;
     job.sets = sets;
     job.n_sets = (uint32_t)n_sets;
     job.flags = LSG_JOB_BATCHABLE;
-    int rc = submit_pkg(c, &job, 1, seed, &t, false);  // the partial leaves: every r_i random
+    int rc = submit_pkg(c, lk, &job, 1, seed, &t, false);  // the partial leaves: every r_i random
     if (rc) return rc;
   }
   const int prc = presync_pkg(c, t, false);
@@ -3609,8 +3760,8 @@ static int final_wait(lsg_ctx* c, lsg_ticket ticket, int32_t* valid, bool single
   }
   (void)hipSetDevice(c->dev[0]->device);
   hipError_t e = event_wait(ev);
-  if (e != hipSuccess) return fail_c(c, "hipEventSynchronize", e);
   LSG_ENTER(c);
+  if (e != hipSuccess) return fail_c(c, "hipEventSynchronize", e);
   Slot* s = ticket_final(c, ticket);
   if (!s) return LSG_ERR_INVALID_ARG;
   if (single && s->n_sets > 1) {
@@ -3722,6 +3873,7 @@ int lsg_aggregate_pubkeys_multi(lsg_ctx* c, const lsg_set* sets, size_t n_sets, 
 
 int lsg_pubkey_table_set(lsg_ctx* c, size_t first, const uint8_t* pks, uint32_t pk_len, size_t n, int32_t* err) {
   if (!c || (n && !pks) || (pk_len != 48 && pk_len != 96) || first + n > 0xffffffffull) return LSG_ERR_INVALID_ARG;
+  std::unique_lock<std::shared_mutex> tab(c->tab_mu);  // no package is being staged from the table
   LSG_ENTER(c);
   if (n == 0) return LSG_OK;
   std::vector<int32_t> pkerr;

@@ -424,7 +424,17 @@ static void* engine_main(void* arg) {
         struct timespec ts = {0, 200000};
         nanosleep(&ts, NULL);
       }
-      if (r->rc == LSG_OK) r->rc = lsg_wait_jobs(a->c, r->ticket, r->results, &r->stats);
+      /* a coalesced ticket still held while every slot is busy waits with LSG_ERR_BUSY until
+       * another package's wait frees one (lsg_host.hip wait_merged): back off and wait again */
+      for (int tries = 0; r->rc == LSG_OK; tries++) {
+        const int wrc = lsg_wait_jobs(a->c, r->ticket, r->results, &r->stats);
+        if (wrc != LSG_ERR_BUSY || tries > 100000) {
+          r->rc = wrc;
+          break;
+        }
+        struct timespec ts = {0, 200000};
+        nanosleep(&ts, NULL);
+      }
     }
     if (r->rc) snprintf(r->err, sizeof r->err, "lsg_submit_jobs/lsg_wait_jobs failed (status %d): %s", r->rc, lsg_last_error(a->c));
     free(sets);
@@ -487,14 +497,16 @@ static int engine_start(napi_env env, addon_ctx* a) {
   int32_t slots = LSG_NAPI_THREADS;
   lsg_pipeline_slots(a->c, &slots);
   /* package threads: min(slots - 1, LSG_NAPI_THREADS), so that the priority thread always finds
-   * a free slot (with fewer slots than threads it would spin on BUSY behind the packages) */
+   * a free slot (with fewer slots than threads it would spin on BUSY behind the packages).  One
+   * slot: one thread, which serves the priority queue first like every package thread. */
   int pkg_threads = slots - 1 < LSG_NAPI_THREADS ? slots - 1 : LSG_NAPI_THREADS;
+  const int prio_thread = pkg_threads >= 1;
   if (pkg_threads < 1) pkg_threads = 1;
-  a->n_threads = pkg_threads + 1;
+  a->n_threads = pkg_threads + prio_thread;
   a->started = 1;
   for (int i = 0; i < a->n_threads; i++) {
     a->targ[i].a = a;
-    a->targ[i].prio_only = i == a->n_threads - 1;
+    a->targ[i].prio_only = prio_thread && i == a->n_threads - 1;
     pthread_create(&a->th[i], NULL, engine_main, &a->targ[i]);
   }
   return 0;

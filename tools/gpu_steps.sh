@@ -37,6 +37,7 @@ for step in "$@"; do
     depth-*) a=${step#depth-}; w=${a%%:*}; d=${a#*:}; run "bench_${w}_d$d" 400 python -u bench.py --workload "$w" --depth "$d" --no-cpu-baseline ;;
     co-*) a=${step#co-}; w=${a%%:*}; r=${a#*:}; d=${r%%:*}; f=${r#*:}; run "bench_${w}_d${d}_f$f" 400 python -u bench.py --workload "$w" --depth "$d" --coalesce-inflight "$f" --no-cpu-baseline ;;
     devices1) run bench_devices1 400 python -u bench.py --devices 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    devhost-*) n=${step#devhost-}; run "bench_devhost_$n" 400 python -u bench.py --devices "$n" --devices-same --depth 3 --steps 12 --warmup 3 --packages 2 --no-cpu-baseline ;;
     node) run bench_node 400 python -u bench.py --workload node --no-cpu-baseline ;;
     node-semi128) run bench_node_semi128 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=128" ;;
     node-semi256) run bench_node_semi256 400 python -u bench.py --workload node --no-cpu-baseline "--node-flags=--max-old-space-size=4096 --max-semi-space-size=256" ;;
