@@ -311,6 +311,12 @@ int lsg_attestation_signing_roots(lsg_ctx* ctx, const uint8_t* data128, size_t n
 int lsg_sign(lsg_ctx* ctx, const uint8_t* sks32, const uint8_t* msgs, uint32_t msg_len, size_t n, uint8_t* out96);
 int lsg_sk_to_pk(lsg_ctx* ctx, const uint8_t* sks32, size_t n, uint8_t* out96);
 
+/* Parity hook of the device Fp2 product (tests only): for n items of four field elements
+ * (a0, a1, b0, b1) in the pair layout -- 14 signed radix-2^29 limbs each, word k of element e
+ * of item i at in[(4 i + e) * 14 + 2 (k mod 7) + k / 7] -- writes c0, c1 with
+ * c0 + c1 u = (a0 + a1 u)(b0 + b1 u) / 2^406 mod p, raw (lazy, not canonical), same layout, 2
+ * elements per item.  Not on the verification path. */
+int lsg_check_fp2_mul(lsg_ctx* ctx, const uint32_t* in, size_t n, uint32_t* out);
 /* Integer-VALU roofline probe: runs a throughput kernel of dependent-free 381-bit
  * Montgomery multiplications; reports Fp-mul/s and v_mad_u64_u32/s (x300 per mul). */
 int lsg_probe_fp_mul_rate(lsg_ctx* ctx, double* fp_mul_per_s, double* mad_per_s);

@@ -6,6 +6,7 @@ raises ``NativeUnavailable``.
 """
 import ctypes
 import os
+import struct
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -102,7 +103,7 @@ EXPORTS = [
     "lsg_pubkey_table_set", "lsg_pubkey_table_size", "lsg_pubkey_validate",
     "lsg_final_submit_groups", "lsg_final_wait_groups", "lsg_aggregate_signatures",
     "lsg_signing_roots", "lsg_attestation_signing_roots", "lsg_jobs_partial_device", "lsg_final_submit_device",
-    "lsg_set_coalesce", "lsg_aggregate_pubkeys_multi",
+    "lsg_set_coalesce", "lsg_aggregate_pubkeys_multi", "lsg_check_fp2_mul",
 ]
 
 
@@ -162,6 +163,7 @@ def load_library(path=LIB_PATH):
         lib.lsg_final_wait.argtypes = [vp, u64, pi32]
         lib.lsg_pipeline_slots.argtypes = [vp, pi32]
         lib.lsg_set_coalesce.argtypes = [vp, u32, i32]
+        lib.lsg_check_fp2_mul.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p]
         lib.lsg_probe_mad_peak.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         for name in EXPORTS:
             if name != "lsg_last_error":
@@ -608,6 +610,16 @@ class Context:
         self._check(self.lib.lsg_sk_to_pk(self.h, skb, len(sks), out), "lsg_sk_to_pk")
         raw = out.raw  # (one copy: .raw copies the whole buffer on every access)
         return [raw[96 * i:96 * i + 96] for i in range(len(sks))]
+
+    def check_fp2_mul(self, words):
+        """lsg_check_fp2_mul: `words` = 56 u32 per item (a0, a1, b0, b1 in the pair layout,
+        lodestar_bls.h); returns 28 u32 per item (c0, c1, raw)."""
+        n = len(words) // 56
+        assert len(words) == 56 * n
+        out = ctypes.create_string_buffer(4 * 28 * n)
+        src = struct.pack(f"<{len(words)}I", *words)
+        self._check(self.lib.lsg_check_fp2_mul(self.h, src, n, out), "lsg_check_fp2_mul")
+        return list(struct.unpack(f"<{28 * n}I", out.raw))
 
     def probe_fp_mul_rate(self):
         a, b = ctypes.c_double(), ctypes.c_double()

@@ -1432,6 +1432,10 @@ int launch_accum(Slot* s, size_t n_items, size_t item_off, uint32_t* fall, bool 
   return LSG_OK;
 }
 
+// kernel-time label of a serial stage: the straight-line program that runs it (slp_*), or the
+// row kernel with LSG_SERIAL=row in the A/B build (k_row_*)
+#define SERIAL_LABEL(name) (lsg_serial_mode() == LSG_SERIAL_SLP ? "slp_" #name : "k_row_" #name)
+
 // side stream: signature sums -> ML(-G1, S_g) -> fall slots; main stream: products, export, FE
 // rs: the scaled points [r_i] sig_i the plain groups sum; rs_msm: the unscaled points the
 // bucket MSM groups read (phase A: one buffer holds both kinds, by set)
@@ -1447,7 +1451,7 @@ int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fal
     LSG_RC(run_seg(s, 1, "msm_bits", Ph.bits, P_<uint32_t>(s->d_bkt), P_<uint32_t>(s->d_bits)));
     KL(s, "k_g2p_to_canon", lsgk::g2p_to_canon(S_(s), (int)(MSM_BITS * Ph.n_msm), P_<uint32_t>(s->d_bits),
                                                P_<uint8_t>(s->d_Sb)));
-    KL(s, "k_row_horner_miller",
+    KL(s, SERIAL_LABEL(horner_miller),
        lsg_row_horner_miller(S_(s), (int)Ph.n_msm, P_<uint8_t>(s->d_Sb), P_<uint8_t>(s->d_fgb)));
   }
   if (Ph.n_msm < ng) {
@@ -1455,7 +1459,7 @@ int launch_phase(Slot* s, const PhasePlan& Ph, const uint32_t* rs, uint32_t* fal
     LSG_RC(run_seg(s, 1, "sig_sums", Ph.sums, rs, P_<uint32_t>(s->d_S)));
     uint8_t* sb = P_<uint8_t>(s->d_Sb) + (size_t)288 * MSM_BITS * Ph.n_msm;
     KL(s, "k_g2p_to_canon", lsgk::g2p_to_canon(S_(s), nsm, P_<uint32_t>(s->d_S) + W_G2P * Ph.n_msm, sb));
-    KL(s, "k_row_miller_neg_g1",
+    KL(s, SERIAL_LABEL(miller_neg_g1),
        lsg_row_miller_neg_g1(S_(s), nsm, sb, P_<uint8_t>(s->d_fgb) + 576 * Ph.n_msm));
   }
   KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S_(s), (int)ng, P_<uint8_t>(s->d_fgb), fall + W_F12 * Ph.term_base));
@@ -1474,7 +1478,7 @@ int launch_fe_range(Slot* s, size_t g0, size_t g1) {
   if (g1 <= g0) return LSG_OK;
   s->cur = 0;
   const size_t ng = g1 - g0;
-  KL(s, "k_row_final_exp",
+  KL(s, SERIAL_LABEL(final_exp),
      lsg_row_final_exp(S_(s), (int)ng, P_<uint8_t>(s->d_Fb) + 576 * g0, P_<int32_t>(s->d_verdict) + g0));
   LSG_HIP(s, hipMemcpyAsync(H_<int32_t>(s->h_verdict) + g0, P_<int32_t>(s->d_verdict) + g0, 4 * ng,
                             hipMemcpyDeviceToHost, s->st[0]));
@@ -2111,7 +2115,7 @@ int pkg_node_check(Slot* s, int n) {
   LSG_RC(run_seg(s, 2, "fp12_product", s->phA_node, nf, P_<uint32_t>(s->d_nodeF) + W_F12 * (size_t)n));
   uint8_t* blob = P_<uint8_t>(s->d_gath) + 576 * (size_t)(LSG_MAX_DEVICES + 1);
   KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S_(s), 1, P_<uint32_t>(s->d_nodeF) + W_F12 * (size_t)n, blob));
-  KL(s, "k_row_final_exp", lsg_row_final_exp(S_(s), 1, blob, P_<int32_t>(s->d_nodeV)));
+  KL(s, SERIAL_LABEL(final_exp), lsg_row_final_exp(S_(s), 1, blob, P_<int32_t>(s->d_nodeV)));
   LSG_HIP(s, hipMemcpyAsync(s->h_nodeV.p, s->d_nodeV.p, 4, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipEventRecord(s->ev_node, s->st[0]));
   return LSG_OK;
@@ -3181,7 +3185,7 @@ int submit_final(Slot* s, const uint8_t* partials576, size_t ng, size_t pg, bool
     KL(s, "k_blobs_to_fp12", lsgk::blobs_to_fp12(S, (int)n, P_<uint8_t>(s->d_Fb), P_<uint32_t>(s->d_aux)));
     LSG_RC(run_seg(s, 2, "fp12_product", P, P_<uint32_t>(s->d_aux), P_<uint32_t>(s->d_F)));
     KL(s, "k_fp12_to_canon", lsgk::fp12_to_canon(S, (int)ng, P_<uint32_t>(s->d_F), P_<uint8_t>(s->d_Fb)));
-    KL(s, "k_row_final_exp", lsg_row_final_exp(S, (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
+    KL(s, SERIAL_LABEL(final_exp), lsg_row_final_exp(S, (int)ng, P_<uint8_t>(s->d_Fb), P_<int32_t>(s->d_verdict)));
     LSG_HIP(s, hipMemcpyAsync(s->h_verdict.p, s->d_verdict.p, 4 * ng, hipMemcpyDeviceToHost, S));
   } else {
     s->n_sets = 0;
@@ -4090,6 +4094,21 @@ int lsg_sk_to_pk(lsg_ctx* c, const uint8_t* sks32, size_t n, uint8_t* out96) {
   LSG_HIP(s, hipMemcpyAsync(s->d_Fb.p, sks32, 32 * n, hipMemcpyHostToDevice, s->st[0]));
   KL(s, "k_sk_to_pk", lsgk::sk_to_pk(S_(s), (int)n, P_<uint8_t>(s->d_Fb), P_<uint8_t>(s->d_aux)));
   LSG_HIP(s, hipMemcpyAsync(out96, s->d_aux.p, 96 * n, hipMemcpyDeviceToHost, s->st[0]));
+  LSG_HIP(s, hipStreamSynchronize(s->st[0]));
+  return LSG_OK;
+}
+
+int lsg_check_fp2_mul(lsg_ctx* c, const uint32_t* in, size_t n, uint32_t* out) {
+  if (!c || (n && (!in || !out)) || n > 0x7fffffffull / (4 * W_FP)) return LSG_ERR_INVALID_ARG;
+  LSG_ENTER(c);
+  if (n == 0) return LSG_OK;
+  Slot* s = &c->dev[0]->util;
+  timer_reset(s);
+  LSG_RC(ensure(s, s->d_aux, 4 * 4 * W_FP * n));
+  LSG_RC(ensure(s, s->d_Fb, 4 * 2 * W_FP * n));
+  LSG_HIP(s, hipMemcpyAsync(s->d_aux.p, in, 4 * 4 * W_FP * n, hipMemcpyHostToDevice, s->st[0]));
+  KL(s, "k_check_fp2_mul", lsgk::check_fp2_mul(S_(s), (int)n, P_<uint32_t>(s->d_aux), P_<uint32_t>(s->d_Fb)));
+  LSG_HIP(s, hipMemcpyAsync(out, s->d_Fb.p, 4 * 2 * W_FP * n, hipMemcpyDeviceToHost, s->st[0]));
   LSG_HIP(s, hipStreamSynchronize(s->st[0]));
   return LSG_OK;
 }

@@ -190,6 +190,19 @@ __global__ void LSG_KERNEL_ATTR_W(1) k_fp12_pow_u64(const uint8_t* __restrict__ 
   fp12_to_canon_bytes(out576, acc);
 }
 
+// parity hook of the Fp2 product leaf (pair_fp2_mul_v: the SOP form) at its lazy bounds: per
+// item, c0 + c1 u = (a0 + a1 u)(b0 + b1 u) R^-1 from four raw pair-layout operands, stored raw
+// (not reduced, not canonical) so that the test checks the value and the leaf's output bound
+__global__ void LSG_KERNEL_ATTR k_check_fp2_mul(int n, const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  LANE_ITEM(n);
+  (void)lead;
+  const fp2_t a(lane_load<fp_t>(in, 4 * item), lane_load<fp_t>(in, 4 * item + 1));
+  const fp2_t b(lane_load<fp_t>(in, 4 * item + 2), lane_load<fp_t>(in, 4 * item + 3));
+  const fp2_t c = fp2_mul(a, b);
+  lane_store(out, 2 * item, c.c0);
+  lane_store(out, 2 * item + 1, c.c1);
+}
+
 // roofline probe: 4 independent limb-parallel Montgomery chains per pair
 __global__ void LSG_KERNEL_ATTR k_probe_fp_mul(int n, int iters, uint32_t* __restrict__ io) {
   LANE_ITEM(n);
@@ -257,6 +270,9 @@ hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out
 }
 hipError_t fp12_pow_u64(hipStream_t st, const uint8_t* in576, uint64_t r, uint8_t* out576) {
   LSG_LAUNCH_ITEMS(k_fp12_pow_u64, 1, st, in576, r, out576);
+}
+hipError_t check_fp2_mul(hipStream_t st, int n, const uint32_t* in, uint32_t* out) {
+  LSG_LAUNCH_ITEMS(k_check_fp2_mul, n, st, n, in, out);
 }
 hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io) {
   LSG_LAUNCH_ITEMS(k_probe_fp_mul, items, st, items, iters, io);

@@ -129,5 +129,6 @@ hipError_t fp12_to_canon(hipStream_t st, int n, const uint32_t* in, uint8_t* out
 // out576 = in576^r (canonical Fp12 blobs, one item): an exported partial's RLC randomizer
 hipError_t fp12_pow_u64(hipStream_t st, const uint8_t* in576, uint64_t r, uint8_t* out576);
 hipError_t probe_fp_mul(hipStream_t st, int items, int iters, uint32_t* io);
+hipError_t check_fp2_mul(hipStream_t st, int n, const uint32_t* in, uint32_t* out);
 hipError_t probe_mad(hipStream_t st, int blocks, int iters, uint32_t seed, uint64_t* io);
 }  // namespace lsgk

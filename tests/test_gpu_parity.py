@@ -707,3 +707,60 @@ def test_attestation_signing_roots_feed_verification(ctx):
     bad[0] ^= 1
     sets[7] = (sets[7][0], ctx.attestation_signing_roots([bytes(bad)], domain)[0], sets[7][2])
     assert ctx.verify_sets(sets, seed=3)[0] == 0
+
+
+def test_device_fp2_leaf_at_lazy_bounds(ctx):
+    """The device Fp2 product leaf (lsg_fp_pair.hpp pair_fp2_mul_v, the SOP form) at the lazy
+    bounds of its inputs: limbs at the edges of [-8, 2^29 + 8), signed top limbs with
+    |v| < 2^12.6 p -- on gfx950 an accumulator column lives 7 steps per lane and the argued bound
+    is |t| < 2^62.6, which random field elements never approach -- against exact integers:
+    out = (a0 b0 - a1 b1, a0 b1 + a1 b0) / 2^406 mod p, |out| < 3p, limbs 0..12 normalised
+    (lsg_check_fp2_mul runs the leaf the kernels call)."""
+    import itertools
+    import random
+    P = h2c.P
+    Rinv = pow(1 << 406, -1, P)
+    bound = int(2 ** 12.6 * P)
+    top_max = bound >> (29 * 13)
+
+    def value(limbs):
+        return sum(v << (29 * k) for k, v in enumerate(limbs))
+
+    def clamp(limbs):  # the top limb's magnitude lowered until |value| < 2^12.6 p
+        while abs(value(limbs)) >= bound:
+            limbs[13] += -1 if limbs[13] > 0 else 1
+        return limbs
+
+    patterns = [clamp([lo] * 13 + [top]) for lo, top in
+                itertools.product(((1 << 29) + 7, -8, 0, (1 << 29) - 1), (top_max, -top_max, 0, 1))]
+    r = random.Random(77)
+    patterns += [clamp([r.randrange(-8, (1 << 29) + 8) for _ in range(13)] + [r.randrange(-top_max, top_max + 1)])
+                 for _ in range(60)]
+    # alternating extremes: the largest positive and negative partial products in one column
+    patterns += [clamp([((1 << 29) + 7) if k % 2 else -8 for k in range(13)] + [top_max]),
+                 clamp([-8 if k % 2 else ((1 << 29) + 7) for k in range(13)] + [-top_max])]
+
+    def pair_words(limbs):  # pair layout of one element: limb L at word 2 (L mod 7) + L / 7
+        w = [0] * 14
+        for L, v in enumerate(limbs):
+            w[2 * (L % 7) + L // 7] = v & 0xFFFFFFFF
+        return w
+
+    def from_words(w):
+        limbs = [w[2 * (L % 7) + L // 7] for L in range(14)]
+        return [x - (1 << 32) if x >= (1 << 31) else x for x in limbs]
+
+    items = []
+    n = len(patterns)
+    for k in range(4 * n):
+        items.append((patterns[k % n], patterns[(3 * k + 1) % n], patterns[(5 * k + 2) % n], patterns[(7 * k + 3) % n]))
+    words = [w for it in items for e in it for w in pair_words(e)]
+    out = ctx.check_fp2_mul(words)
+    for i, (a0, a1, b0, b1) in enumerate(items):
+        va0, va1, vb0, vb1 = map(value, (a0, a1, b0, b1))
+        c0, c1 = from_words(out[28 * i:28 * i + 14]), from_words(out[28 * i + 14:28 * i + 28])
+        v0, v1 = value(c0), value(c1)
+        assert (v0 - (va0 * vb0 - va1 * vb1) * Rinv) % P == 0, i
+        assert (v1 - (va0 * vb1 + va1 * vb0) * Rinv) % P == 0, i
+        assert abs(v0) < 3 * P and abs(v1) < 3 * P, i
+        assert all(0 <= c < (1 << 29) for c in c0[:13] + c1[:13]), i

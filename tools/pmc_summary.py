@@ -14,7 +14,7 @@ iso_write/ (rocprofv3 --pmc CSVs).  For every kernel, per dispatch:
 Writes profiles/<tag>_pmc_isolation.json, profiles/<tag>_pmc_traffic.json (read by bench.py
 for roofline.traffic) and a text table on stdout.
 
-    python tools/pmc_summary.py gpurun_out --sets 32768 --peak 3.25e13 --tag r02
+    python tools/pmc_summary.py gpurun_out --sets 32768 --tag r06   (--peak: override the run's probe)
 """
 import argparse
 import csv
@@ -74,9 +74,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--sets", type=int, required=True, help="sets per package in the profiled run")
-    ap.add_argument("--peak", type=float, required=True, help="measured v_mad_u64_u32 peak, mad/s")
+    ap.add_argument("--peak", type=float, default=None,
+                    help="v_mad_u64_u32 peak, mad/s (default: the profiled run's own probe, roofline.peak of the "
+                         "bench line in <dir>/iso_trace.log)")
     ap.add_argument("--tag", default="r02")
     a = ap.parse_args()
+    peak_source = "--peak"
+    if a.peak is None:  # the same run's probe (lsg_probe_mad_peak, measured live by bench.py)
+        lines = [l for l in open(os.path.join(a.dir, "iso_trace.log")) if l.startswith("{")]
+        a.peak = json.loads(lines[-1])["roofline"]["peak"] * 1e12
+        peak_source = "probe of the profiled run (iso_trace.log roofline.peak)"
     dur = durations(os.path.join(a.dir, "iso_trace", "run_results.db"))
     ser = serial_durations(os.path.join(a.dir, "iso_sq"))
     cnt = {}
@@ -113,7 +120,7 @@ def main():
             if k in ser:
                 r["frac_of_peak_serial"] = round(mads / (ser[k] * 1e-9) / a.peak, 4)
         rows[k] = r
-    out = {"sets_per_launch": a.sets, "peak_mad_per_s": a.peak, "kernels": rows,
+    out = {"sets_per_launch": a.sets, "peak_mad_per_s": a.peak, "peak_source": peak_source, "kernels": rows,
            "source": "tools/gpu_pmc.sh (depth-1 bench, one package at a time) -> tools/pmc_summary.py",
            "columns": "avg_us: kernel trace of the depth-1 run (the package's two streams overlap); serial_us: the "
                       "same dispatches under --pmc, which serialises them (each kernel alone on the GPU); "
