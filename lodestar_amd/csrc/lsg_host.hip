@@ -3332,11 +3332,20 @@ int lsg_init_devices(const int* device_ids, int n_devices, lsg_ctx** out) {
   // (1..32, default LSG_DEFAULT_HW_QUEUES), overriding a process-wide default such as the
   // GPU_MAX_HW_QUEUES=4 some hosts export.  It takes effect when HIP is not yet initialised --
   // the first lsg_init of a Node process; INTEGRATION.md section 5.
+  // setenv is not safe against getenv on other threads: a host calls lsg_init before it
+  // starts threads that read the environment.  A value already in the
+  // environment is replaced, and said so once: if HIP was initialised before (by another
+  // library), the replacement comes too late to take effect.
   static std::once_flag hwq_once;
   std::call_once(hwq_once, [] {
     const char* want = getenv("LSG_HW_QUEUES");
     const int q = want ? atoi(want) : 0;
-    setenv("GPU_MAX_HW_QUEUES", (q >= 1 && q <= 32) ? want : LSG_DEFAULT_HW_QUEUES, 1);
+    const char* v = (q >= 1 && q <= 32) ? want : LSG_DEFAULT_HW_QUEUES;
+    const char* had = getenv("GPU_MAX_HW_QUEUES");
+    if (had && strcmp(had, v) != 0)
+      fprintf(stderr, "lodestar_bls: GPU_MAX_HW_QUEUES=%s replaced by %s (LSG_HW_QUEUES); effective unless HIP was "
+                      "initialised earlier in this process\n", had, v);
+    setenv("GPU_MAX_HW_QUEUES", v, 1);
   });
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return LSG_ERR_NO_DEVICE;

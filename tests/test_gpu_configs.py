@@ -642,3 +642,90 @@ def test_merged_nonbatchable_group_matches_per_job(ab_ctx, keys, monkeypatch):
         got = out["1"][0]
         assert [(g[0], g[1] if g[0] == 2 else 0) for g in got] == exp
         assert out["1"][1:] == (retries, success)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]], ids=["one-device", "three-duplicate-ids"])
+def test_concurrent_submitters_match_oracle(keys, devices):
+    """Packages are staged with the context lock released (lsg_host.hip submit_pkg / stage_pkg):
+    four host threads submit and wait mixed packages at once -- on a one-device context and on
+    one over three duplicate ids, whose devices' shares stage on threads of their own -- while a
+    fifth thread rewrites the pubkey table that the packages' index sets read (it waits for the
+    packages being staged).  Every job's verdict and every package's batch counters must be the
+    oracle's (worker.ts:30-106) -- the counters over each device's share of the jobs."""
+    import threading
+    from lodestar_amd._native import Context, PkIndices, assign_jobs
+    c0 = Context(0)
+    c = Context(devices=devices)
+    try:
+        sks, pks = keys
+        assert c.pubkey_table_set(0, pks) == [0] * N_KEYS
+        sets = single_sets(c0, keys, b"concurrent", 1024)
+        bad, _ = corrupt(c0, keys, sets, 0.03, 11)
+        per = oracle_each(bad)
+        packages = []
+        for t in range(8):
+            chunk = list(range(128 * t, 128 * t + 128))
+            js = [[i] for i in chunk[:48]]                                   # gossip singles
+            js += [chunk[48 + 4 * k:52 + 4 * k] for k in range(16)]          # 4-set batches
+            js += [[i] for i in chunk[112:124]]                              # singles by validator index
+            js += [chunk[124:128]]                                           # one non-batchable job
+            flags = [1] * (len(js) - 1) + [0]
+            jobs = []
+            for q, idx in enumerate(js):
+                if 64 <= q < 76:  # the index-named singles
+                    i = idx[0]
+                    jobs.append(([(PkIndices([i % N_KEYS]), bad[i][1], bad[i][2])], flags[q]))
+                else:
+                    jobs.append(([bad[i] for i in idx], flags[q]))
+            # verdicts are the package's whatever the split; the batch counters are those of each
+            # device's share of whole jobs (lsg_assign_jobs), chunked on its own, as a reference
+            # pool's counters are those of each worker's jobs (multithread/index.ts:400-418)
+            owner = assign_jobs([len(idx) for idx in js], len(devices))
+            verd, retries, success = [None] * len(js), 0, 0
+            for d in range(len(devices)):
+                mine = [q for q in range(len(js)) if owner[q] == d]
+                flat = [i for q in mine for i in js[q]]
+                pos = {i: k for k, i in enumerate(flat)}
+                e, r, sc = co.expected_jobs([[pos[i] for i in js[q]] for q in mine], [bool(flags[q]) for q in mine],
+                                            [per[i] for i in flat])
+                for q, v in zip(mine, e):
+                    verd[q] = v
+                retries += r
+                success += sc
+            packages.append((jobs, (verd, retries, success)))
+        errors = []
+        stop = threading.Event()
+
+        def submitter(k):
+            try:
+                for rep in range(3):
+                    jobs, (exp, retries, success) = packages[(2 * k + rep) % len(packages)]
+                    got, st = c.verify_jobs(jobs)
+                    got = [(s, e if s == 2 else 0) for s, e in got]
+                    if got != exp:
+                        errors.append(("verdicts", k, rep, [(j, g, x) for j, (g, x) in enumerate(zip(got, exp)) if g != x][:5]))
+                    if (st["batch_retries"], st["batch_sigs_success"]) != (retries, success):
+                        errors.append(("counters", k, rep, st, retries, success))
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(("raised", k, repr(e)))
+
+        def table_writer():
+            while not stop.is_set():
+                if c.pubkey_table_set(0, pks) != [0] * N_KEYS:
+                    errors.append(("table", "pubkey_table_set failed"))
+                    return
+
+        th = [threading.Thread(target=submitter, args=(k,)) for k in range(4)]
+        tw = threading.Thread(target=table_writer)
+        tw.start()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=150)
+        stop.set()
+        tw.join(timeout=60)
+        assert not any(t.is_alive() for t in th) and not tw.is_alive(), "a submitter or the table writer hung"
+        assert not errors, errors[:5]
+    finally:
+        c.close()
+        c0.close()
