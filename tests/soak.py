@@ -50,27 +50,36 @@ def main():
     ap.add_argument("--committee-every", type=int, default=2,
                     help="every K-th package signs committee messages: 64 distinct messages, set i of the "
                          "package in committee (i + i // 1024) mod 64 (hash_to_G2 once per message); 0: never")
+    ap.add_argument("--devices", type=int, default=1,
+                    help="> 1: one context over this many duplicate ids of GPU 0 (each device's share of a "
+                         "package staged on a thread of its own, device-copy exchange)")
+    ap.add_argument("--submitters", type=int, default=1,
+                    help="host threads submitting and waiting packages at once (packages are staged with the "
+                         "context lock released)")
     args = ap.parse_args()
-    rng = random.Random(args.seed)
+    import threading
     import numpy as np
 
-    ctx = N.Context(0)
-    ctx.reserve(args.package + 256, n_slots=args.depth + 1)
+    ctx = N.Context(0) if args.devices <= 1 else N.Context(devices=[0] * args.devices)
+    ctx.reserve(args.package + 256, n_slots=min(16, args.submitters * args.depth + 1))
     sks = [interop_sk(i) for i in range(1024)]
     pks = ctx.sk_to_pk(sks)
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sig_decode.json")))
     non_subgroup = [bytes.fromhex(c["sig"]) for c in gold["cases"] if c["err"] == 3 and len(c["sig"]) == 192]
     counter = 0
     n_pkg = 0
+    lock = threading.Lock()
 
-    def make_package():
+    def make_package(rng):
         nonlocal counter
         nonlocal n_pkg
         n = args.package
-        base = counter
-        counter += n
-        n_pkg += 1
-        if args.committee_every and n_pkg % args.committee_every == 0:
+        with lock:  # distinct messages across the submitting threads
+            base = counter
+            counter += n
+            n_pkg += 1
+            pkg_no = n_pkg
+        if args.committee_every and pkg_no % args.committee_every == 0:
             # base + c: distinct from every other package's messages (bases step by n >= 64)
             msgs = [hashlib.sha256(b"lodestar-mi355x" + b"soak" + (base + (i + i // 1024) % 64).to_bytes(8, "little"))
                     .digest() for i in range(n)]
@@ -124,49 +133,70 @@ def main():
         return N.PreparedJobs(jobs), np.array(jexp, dtype=np.int32), n
 
     done_sets = done_jobs = mismatches = retries = n_false = n_err = 0
-    pend = []
-    t_start = t_last = time.time()
+    t_start = time.time()
+    t_last = [t_start]
+    failures = []
 
-    def drain_one():
+    def drain_one(pend):
         nonlocal done_sets, done_jobs, mismatches, retries, n_false, n_err
         t, exp, n, _pj = pend.pop(0)
         res, st = ctx.wait_jobs(t, raw=True)
         got = np.frombuffer(res, dtype=np.int32, count=2 * len(exp)).reshape(-1, 2).copy()
         got[got[:, 0] != N.LSG_ERROR, 1] = 0
         bad = np.nonzero((got != exp).any(axis=1))[0]
-        for k in bad[:max(0, 10 - mismatches)]:
-            print(f"MISMATCH job {done_jobs + int(k)}: got {tuple(got[k])} expected {tuple(exp[k])}", flush=True)
-        mismatches += len(bad)
-        n_false += int((got[:, 0] == N.LSG_INVALID).sum())
-        n_err += int((got[:, 0] == N.LSG_ERROR).sum())
-        retries += st["batch_retries"]
-        done_sets += n
-        done_jobs += len(exp)
+        with lock:
+            for k in bad[:max(0, 10 - mismatches)]:
+                print(f"MISMATCH job {done_jobs + int(k)}: got {tuple(got[k])} expected {tuple(exp[k])}", flush=True)
+            mismatches += len(bad)
+            n_false += int((got[:, 0] == N.LSG_INVALID).sum())
+            n_err += int((got[:, 0] == N.LSG_ERROR).sum())
+            retries += st["batch_retries"]
+            done_sets += n
+            done_jobs += len(exp)
+            if time.time() - t_last[0] > 10:
+                t_last[0] = time.time()
+                print(f"{done_sets} sets / {done_jobs} jobs verified, {mismatches} mismatches, {n_false} false, "
+                      f"{n_err} rejected, {retries} batch retries ({t_last[0] - t_start:.0f} s, generation included)",
+                      flush=True)
 
-    submitted = 0
-    while submitted < args.sets or pend:
-        if submitted < args.sets and len(pend) < args.depth:
-            pj, exp, n = make_package()
-            t = ctx.submit_jobs(pj)
-            if t is None:
-                drain_one()
-                t = ctx.submit_jobs(pj)
-            pend.append((t, exp, n, pj))
-            submitted += n
-            continue
-        drain_one()
-        if time.time() - t_last > 10:
-            t_last = time.time()
-            el = t_last - t_start
-            print(f"{done_sets} sets / {done_jobs} jobs verified, {mismatches} mismatches, {n_false} false, "
-                  f"{n_err} rejected, {retries} batch retries ({el:.0f} s, generation included)", flush=True)
+    def submitter(k, quota):
+        try:
+            rng = random.Random(args.seed * 1000003 + k)
+            pend = []
+            submitted = 0
+            while submitted < quota or pend:
+                if submitted < quota and len(pend) < args.depth:
+                    pj, exp, n = make_package(rng)
+                    t = ctx.submit_jobs(pj)
+                    while t is None:  # every slot busy (other threads' packages): wait one of ours
+                        if pend:
+                            drain_one(pend)
+                        else:
+                            time.sleep(0.001)
+                        t = ctx.submit_jobs(pj)
+                    pend.append((t, exp, n, pj))
+                    submitted += n
+                    continue
+                drain_one(pend)
+        except BaseException as e:  # noqa: BLE001 -- reported as a failure of the soak
+            failures.append(repr(e))
+
+    per = -(-args.sets // args.submitters)
+    threads = [threading.Thread(target=submitter, args=(k, max(0, min(per, args.sets - k * per)))) for k in range(args.submitters)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    if failures:
+        raise SystemExit(f"soak: a submitting thread failed: {failures[:3]}")
     el = time.time() - t_start
     print(json.dumps({"sets": done_sets, "distinct_sets": done_sets, "committee_every": args.committee_every,
                       "jobs": done_jobs, "mismatches": mismatches,
                       "jobs_false": n_false, "jobs_rejected": n_err, "batch_retries": retries,
                       "bad_rate": args.bad_rate, "seconds_incl_generation": round(el, 1),
                       "path": "lsg_submit_jobs/lsg_wait_jobs (one RLC group per package + worker.ts fallback)",
-                      "package_sets": args.package, "depth": args.depth}), flush=True)
+                      "package_sets": args.package, "depth": args.depth, "devices": args.devices,
+                      "submitters": args.submitters}), flush=True)
     ctx.close()
     return 1 if mismatches else 0
 

@@ -5,7 +5,7 @@
 #   tools/gpu_final_r06.sh core        GPU suite, smoke, default bench x3, Node drop-in x3
 #   tools/gpu_final_r06.sh workloads   every bench workload once, lone set, 2 x committees
 #   tools/gpu_final_r06.sh prof        rocprofv3 kernel stats of the default bench + PMC isolation
-#   tools/gpu_final_r06.sh soak        10^7-set verdict soak
+#   tools/gpu_final_r06.sh soak        10^7-set verdict soak (soak-threads: 4 submitters, 3 duplicate device ids)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -35,6 +35,8 @@ for part in "$@"; do
       run pmc 900 bash tools/gpu_pmc.sh ;;
     soak)
       run soak 1100 python -u tests/soak.py --sets 10000000 ;;
+    soak-threads)  # four submitting threads on a context over three duplicate ids of the GPU
+      run soak_threads 1100 python -u tests/soak.py --sets 10000000 --seed 2 --devices 3 --submitters 4 ;;
     *) echo "unknown part $part"; exit 2 ;;
   esac
 done
