@@ -585,7 +585,7 @@ LSG_INL int g1_deserialize(g1a_t& out, bool& inf, const uint8_t* in, int len) {
   out.x = fp_to_mont(x);
   if (compressed) {
     fp_t rhs = fp_add(fp_mul(fp_sqr(out.x), out.x), FP_B_G1);
-    fp_t y = fp_pow_fixed(rhs, LSG_EXP_P_PLUS_1_DIV_4);
+    fp_t y = fp_pow_id(rhs, LSG_POW_SQRT);
     if (!fp_eq(fp_sqr(y), rhs)) return LSG_BLST_POINT_NOT_ON_CURVE;
     bool want = (in0 & 0x20) != 0;
     if (fp_canon_gt_half(fp_from_mont(y)) != want) y = fp_neg(y);

@@ -613,6 +613,129 @@ LSG_PLEAF fp_t pair_pow_fixed(fp_t a, const uint32_t* __restrict__ e) {
 #define LSG_POW_LEAF 1  // lsg_tower.hpp's fp_pow_fixed calls pair_pow_fixed
 #endif
 
+// The same sliding window, planned at compile time.  pair_pow_fixed walks the exponent bit by
+// bit through a pointer argument: every bit test is a vector load and a wait (the pointer is
+// not known to be uniform inside the leaf), ~7 dependent loads per window against ~5
+// products.  Here the plan of each of the three fixed exponents is a constant table read with
+// scalar loads at a wave-uniform index, and the control flow is scalar.
+//   step[0] = k:             r = a^(2k+1)
+//   step[w] = (s << 8) | k:  r = r^(2^s) * a^(2k+1)
+//   then `tail` squarings
+enum lsg_pow_id { LSG_POW_INV = 0, LSG_POW_SQRT = 1, LSG_POW_SQRT34 = 2 };  // p-2, (p+1)/4, (p-3)/4
+#define LSG_POW_IDS 1
+struct pow_plan_t {
+  int n, tail;
+  uint32_t step[128];
+};
+constexpr pow_plan_t make_pow_plan(const uint32_t (&e)[12]) {
+  pow_plan_t P{};
+  int i = 383;
+  while (i >= 0 && !((e[i >> 5] >> (i & 31)) & 1u)) i--;
+  int sq = 0;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      sq++;
+      i--;
+      continue;
+    }
+    int j = i - 3 < 0 ? 0 : i - 3;  // window e[i..j] ends in a set bit
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) j++;
+    uint32_t v = 0;
+    for (int t = i; t >= j; t--) v = (v << 1) | ((e[t >> 5] >> (t & 31)) & 1u);
+    if (P.n > 0) sq += i - j + 1;
+    P.step[P.n++] = ((uint32_t)sq << 8) | (v >> 1);
+    sq = 0;
+    i = j - 1;
+  }
+  P.tail = sq;
+  return P;
+}
+// the plan's exponent, rebuilt step by step, is e (checked at compile time below)
+constexpr bool pow_plan_is(const pow_plan_t& P, const uint32_t (&e)[12]) {
+  uint32_t x[13] = {};
+  for (int w = 0; w <= P.n; w++) {
+    const int s = w == P.n ? P.tail : (int)(P.step[w] >> 8);
+    for (int b = 0; b < s; b++) {  // x <<= 1
+      if (x[12] >> 31) return false;
+      for (int k = 12; k > 0; k--) x[k] = (x[k] << 1) | (x[k - 1] >> 31);
+      x[0] <<= 1;
+    }
+    if (w < P.n) {  // x += 2k + 1 (x is even here but for w = 0, where it is 0)
+      uint64_t c = 2 * (P.step[w] & 0xffu) + 1;
+      for (int k = 0; k < 13; k++) {
+        c += x[k];
+        x[k] = (uint32_t)c;
+        c >>= 32;
+      }
+    }
+  }
+  for (int k = 0; k < 12; k++)
+    if (x[k] != e[k]) return false;
+  return x[12] == 0 && P.n > 0;
+}
+LSG_CONST pow_plan_t LSG_POW_PLANS[3] = {make_pow_plan(LSG_EXP_P_MINUS_2), make_pow_plan(LSG_EXP_P_PLUS_1_DIV_4),
+                                        make_pow_plan(LSG_EXP_P_MINUS_3_DIV_4)};
+static_assert(pow_plan_is(LSG_POW_PLANS[LSG_POW_INV], LSG_EXP_P_MINUS_2), "p-2 plan");
+static_assert(pow_plan_is(LSG_POW_PLANS[LSG_POW_SQRT], LSG_EXP_P_PLUS_1_DIV_4), "(p+1)/4 plan");
+static_assert(pow_plan_is(LSG_POW_PLANS[LSG_POW_SQRT34], LSG_EXP_P_MINUS_3_DIV_4), "(p-3)/4 plan");
+
+LSG_PLEAF fp_t pair_pow_plan(fp_t a, int id) {
+#if LSG_PAIR_G == 2
+  id = __builtin_amdgcn_readfirstlane(id);  // a literal at every call site
+#endif
+  const pow_plan_t& P = LSG_POW_PLANS[id];
+  auto mul = [](const fp_t& x, const fp_t& y) {
+    LSG_COUNT_MUL();
+    fp_t r;
+    pair_mont_mul_n<1>(&r, &x, &y);
+    return r;
+  };
+  auto pick = [](const fp_t* T, uint32_t k) {
+    fp_t tv = T[0];
+#pragma unroll
+    for (uint32_t q = 1; q < 8; q++) tv = fp_select(k == q, T[q], tv);
+    return tv;
+  };
+  fp_t T[8];  // T[k] = a^(2k+1), written out as in pair_pow_fixed
+  const fp_t a2 = mul(a, a);
+  T[0] = a;
+  T[1] = mul(T[0], a2);
+  T[2] = mul(T[1], a2);
+  T[3] = mul(T[2], a2);
+  T[4] = mul(T[3], a2);
+  T[5] = mul(T[4], a2);
+  T[6] = mul(T[5], a2);
+  T[7] = mul(T[6], a2);
+  // the operands made opaque at each product: known non-negative limbs (a product's masked
+  // output) would turn the mads into v_mad_u64_u32 plus accumulator moves
+  auto hide = [](fp_t x) {
+#if LSG_PAIR_G == 2
+#pragma unroll
+    for (int k = 0; k < LSG_PL; k++) asm volatile("" : "+v"(x.l[k]));
+#endif
+    return x;
+  };
+  auto sqr = [&](const fp_t& x) {
+    const fp_t y = hide(x);
+    return mul(y, y);
+  };
+  fp_t r = pick(T, P.step[0] & 0xffu);
+  const int n = P.n;
+#pragma unroll 1
+  for (int w = 1; w < n; w++) {
+    const uint32_t s = P.step[w];
+#pragma unroll 1
+    for (uint32_t b = s >> 8; b; b--) r = sqr(r);
+    r = mul(hide(r), hide(pick(T, s & 0xffu)));
+  }
+#pragma unroll 1
+  for (int b = P.tail; b; b--) r = sqr(r);
+  return r;
+}
+#if defined(LSG_POW_LEAF) && !defined(LSG_NO_POW_PLAN)  // (A/B builds: -DLSG_NO_POW_PLAN)
+#define LSG_POW_PLAN 1  // lsg_tower.hpp's fp_pow_id calls pair_pow_plan
+#endif
+
 // ---- canonical values
 // v in (-p, 2p) -> the representative in [0, p), fully normalised
 LSG_PFN fp_t pair_canon_small(const fp_t& v0) {

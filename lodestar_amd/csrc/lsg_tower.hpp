@@ -66,7 +66,21 @@ LSG_BIGFN fp_t fp_pow_fixed(fp_t a, const uint32_t* e) {
 #endif
 }
 
-LSG_INL fp_t fp_inv(const fp_t& a) { return fp_pow_fixed(a, LSG_EXP_P_MINUS_2); }  // inv(0) = 0
+// a^e for the three fixed exponents by id (LSG_POW_INV p-2, LSG_POW_SQRT (p+1)/4,
+// LSG_POW_SQRT34 (p-3)/4); the pair backend runs the compile-time plan (pair_pow_plan)
+#ifndef LSG_POW_IDS
+enum { LSG_POW_INV = 0, LSG_POW_SQRT = 1, LSG_POW_SQRT34 = 2 };
+#endif
+LSG_BIGFN fp_t fp_pow_id(fp_t a, int id) {
+#ifdef LSG_POW_PLAN
+  return pair_pow_plan(a, id);
+#else
+  return fp_pow_fixed(a, id == LSG_POW_INV ? LSG_EXP_P_MINUS_2
+                         : id == LSG_POW_SQRT ? LSG_EXP_P_PLUS_1_DIV_4 : LSG_EXP_P_MINUS_3_DIV_4);
+#endif
+}
+
+LSG_INL fp_t fp_inv(const fp_t& a) { return fp_pow_id(a, LSG_POW_INV); }  // inv(0) = 0
 
 LSG_INL fp_t fp_mul12(const fp_t& a) {
   fp_t a2 = fp_dbl(a);
@@ -235,7 +249,7 @@ LSG_INL bool fp2_lexi_largest(const fp2_t& y) {
 // Stage 1: the norm's candidate root s = n^((p+1)/4); *is_sq = (s^2 == n).
 LSG_INL fp_t fp2_norm_sqrt_candidate(const fp2_t& a, bool* is_sq) {
   fp_t n = fp2_norm(a);
-  fp_t s = fp_pow_fixed(n, LSG_EXP_P_PLUS_1_DIV_4);
+  fp_t s = fp_pow_id(n, LSG_POW_SQRT);
   *is_sq = fp_eq(fp_sqr(s), n);
   return s;
 }
@@ -243,7 +257,7 @@ LSG_INL fp_t fp2_norm_sqrt_candidate(const fp2_t& a, bool* is_sq) {
 LSG_BIGFN bool fp2_sqrt_with_norm_root(fp2_t& out, fp2_t a, fp_t s) {
   fp_t c = fp_mul(fp_add(a.c0, s), fp_t(FP_HALF));
   c = fp_select(fp_is_zero(c), a.c0, c);
-  fp_t t = fp_pow_fixed(c, LSG_EXP_P_MINUS_3_DIV_4);
+  fp_t t = fp_pow_id(c, LSG_POW_SQRT34);
   fp_t ct = fp_mul(c, t);
   bool c_sq = fp_eq(fp_mul(ct, t), fp_one()) || fp_is_zero(c);
   fp_t h = fp_mul(fp_mul(a.c1, t), fp_t(FP_HALF));
