@@ -395,6 +395,14 @@ LSG_DEVI void mf_add_line(uint32_t* lds, int wl, bool use, const uint32_t* __res
   mf_put2(lds, tb + 4, fp2_mul(E, mf_get2(lds, tb + 4)));
 }
 
+// Issue priority of the fused kernel's waves (s_setprio; 0 = the default of every wave).  Its
+// four waves meet at eight barriers per doubling while the per-set kernels of other packages
+// share their SIMDs: ahead of those, a workgroup's slowest wave reaches each barrier sooner
+// and the other waves fill the SIMD while it waits.  Firehose +0.9 % (8 of 8 pairs) and
+// +1.7 % (5 rounds) on one MI355X, `profiles/r06_mf_prio_ab.txt`.  (A/B: -DLSG_MF_PRIO=0.)
+#ifndef LSG_MF_PRIO
+#define LSG_MF_PRIO 2
+#endif
 #ifndef LSG_MF_WAVES
 #define LSG_MF_WAVES 2  // waves per SIMD the register budget is sized for (256 VGPR + AGPR)
 #endif
@@ -406,6 +414,9 @@ k_miller_fused(int n_items, const int32_t* __restrict__ item_first, const int32_
   // LSG_MF_WAVES waves per SIMD instead of the one workgroup per CU the LDS allows, so the
   // other kernels of the pipeline can share the SIMDs while this one waits at its barriers
   extern __shared__ uint32_t lds[];
+#if LSG_MF_PRIO
+  __builtin_amdgcn_s_setprio(LSG_MF_PRIO);
+#endif
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform: an SGPR
   const size_t it = (size_t)blockIdx.x * MF_ITEMS + ((threadIdx.x & 63) >> 1);
   const bool live = it < (size_t)n_items;  // lanes past the end run item 0's data and store nothing

@@ -68,6 +68,9 @@ LSG_SLP_PROG(SLP_G2_SCALE, g2_scale, G2_SCALE)
 // flight while the current step computes (the program lives in global memory / L2)
 template <class PR>
 __device__ __forceinline__ void slp_steps(uint32_t* lds, const uint8_t* inp, uint32_t q, uint32_t h) {
+#if LSG_SLP_PRIO  // A/B builds: issue priority of the programs' waves over co-resident kernels'
+  __builtin_amdgcn_s_setprio(LSG_SLP_PRIO);
+#endif
   const uint32_t* ops = PR::ops();
   const uint32_t* steps = PR::steps();
   uint32_t d = steps[0];
