@@ -47,6 +47,9 @@ __global__ void LSG_KERNEL_ATTR_W(OP == 2 ? 1 : LSG_WAVES_PER_EU)
   typedef seg_op<OP> O;
   typedef typename O::T T;
   lsg_lane_setup();
+#if LSG_RED_PRIO  // A/B builds: issue priority of the reductions' waves
+  __builtin_amdgcn_s_setprio(LSG_RED_PRIO);
+#endif
   const size_t item = gtid() / LSG_GROUP;
   const size_t c = item >> ips_log2;
   const int ips = 1 << ips_log2, j = (int)(item & (size_t)(ips - 1));
@@ -136,6 +139,9 @@ __global__ void LSG_KERNEL_ATTR k_binv_block(int n, int T, int zero_to_one, cons
                                              uint32_t* __restrict__ pre, uint32_t* __restrict__ out) {
   __shared__ uint32_t H[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP], I[2 * LSG_ITEMS_PER_BLOCK * lsgl::W_FP];
   lsg_lane_setup();
+#if LSG_RED_PRIO
+  __builtin_amdgcn_s_setprio(LSG_RED_PRIO);
+#endif
   const int l = (int)(threadIdx.x / LSG_GROUP);
   const int64_t first = ((int64_t)blockIdx.x * LSG_ITEMS_PER_BLOCK + l) * T;
   const int64_t last = first + T < (int64_t)n ? first + T : (int64_t)n;
